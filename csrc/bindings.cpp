@@ -1,0 +1,335 @@
+// PyTorch bindings for the gfx950 kernel library (module `_C`).
+// Every op validates device / dtype / shape on the host BEFORE launching: a bad
+// launch shape on the GPU box can fault the device for every tenant, so nothing
+// reaches a kernel unchecked.  Kernels run on PyTorch's current HIP stream, so the
+// ops compose with torch.cuda.graphs (hipGraph capture) and stream semantics.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include "kernels.h"
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bfloat16")
+#define CHECK_I32(x) TORCH_CHECK((x).scalar_type() == at::kInt, #x " must be int32")
+#define CHECK_F32(x) TORCH_CHECK((x).scalar_type() == at::kFloat, #x " must be float32")
+#define CHECK_LASTDIM(x) TORCH_CHECK((x).stride(-1) == 1, #x " must be contiguous in its last dim")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define CHECK_RC(rc, name) TORCH_CHECK((rc) == 0, name ": unsupported shape/config (code ", rc, ")")
+
+inline bf16_t* bp(const at::Tensor& t) { return reinterpret_cast<bf16_t*>(t.data_ptr()); }
+inline bf16_t* bpo(const c10::optional<at::Tensor>& t) { return t ? bp(*t) : nullptr; }
+inline const int* ip(const at::Tensor& t) { return t.data_ptr<int>(); }
+inline const int* ipo(const c10::optional<at::Tensor>& t) { return t ? ip(*t) : nullptr; }
+
+// 16-byte alignment of every row start (vector loads)
+void check_rows16(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+  if (t.dim() >= 2) TORCH_CHECK((t.stride(0) * t.element_size()) % 16 == 0, name, " row stride must be a multiple of 16 bytes");
+}
+
+at::Tensor rmsnorm(const at::Tensor& x, const at::Tensor& w, double eps,
+                   const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& out_) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_LASTDIM(x);
+  TORCH_CHECK(x.dim() == 2, "x must be [T, H]");
+  const long T = x.size(0);
+  const int H = x.size(1);
+  TORCH_CHECK(w.numel() == H && w.is_contiguous(), "weight shape");
+  check_rows16(x, "x");
+  at::Tensor out = out_ ? *out_ : at::empty({T, H}, x.options());
+  CHECK_LASTDIM(out); check_rows16(out, "out");
+  TORCH_CHECK(out.size(0) == T && out.size(1) == H, "out shape");
+  long rs = 0;
+  if (residual) {
+    CHECK_BF16(*residual); CHECK_LASTDIM(*residual); check_rows16(*residual, "residual");
+    TORCH_CHECK(residual->size(0) == T && residual->size(1) == H, "residual shape");
+    rs = residual->stride(0);
+  }
+  int rc = lk_rmsnorm(bp(out), bpo(residual), bp(x), bp(w), T, H, (float)eps, x.stride(0),
+                      out.stride(0), rs, cur_stream());
+  CHECK_RC(rc, "rmsnorm");
+  return out;
+}
+
+at::Tensor layernorm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,
+                     double eps, const c10::optional<at::Tensor>& residual, bool write_residual) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_LASTDIM(x);
+  TORCH_CHECK(x.dim() == 2, "x must be [T, H]");
+  const long T = x.size(0);
+  const int H = x.size(1);
+  TORCH_CHECK(w.numel() == H, "weight shape");
+  if (b) { CHECK_BF16(*b); TORCH_CHECK(b->numel() == H, "bias shape"); }
+  check_rows16(x, "x");
+  at::Tensor out = at::empty({T, H}, x.options());
+  long rs = 0;
+  if (residual) {
+    CHECK_BF16(*residual); CHECK_LASTDIM(*residual); check_rows16(*residual, "residual");
+    TORCH_CHECK(residual->size(0) == T && residual->size(1) == H, "residual shape");
+    rs = residual->stride(0);
+  }
+  int rc = lk_layernorm(bp(out), bp(x), bpo(residual), (residual && write_residual) ? bp(*residual) : nullptr,
+                        bp(w), bpo(b), T, H, (float)eps, x.stride(0), out.stride(0), rs, cur_stream());
+  CHECK_RC(rc, "layernorm");
+  return out;
+}
+
+at::Tensor embed_layernorm(const at::Tensor& ids, const c10::optional<at::Tensor>& pos_ids,
+                           const c10::optional<at::Tensor>& type_ids, const at::Tensor& tok,
+                           const c10::optional<at::Tensor>& pos, const c10::optional<at::Tensor>& typ,
+                           const at::Tensor& w, const at::Tensor& b, double eps) {
+  CHECK_CUDA(ids); CHECK_I32(ids); CHECK_BF16(tok); CHECK_CONTIG(tok); CHECK_CONTIG(ids);
+  const long T = ids.numel();
+  const int H = tok.size(1);
+  if (pos) { CHECK_BF16(*pos); CHECK_CONTIG(*pos); TORCH_CHECK(pos_ids.has_value(), "pos_ids required"); CHECK_I32(*pos_ids); TORCH_CHECK(pos_ids->numel() == T, "pos_ids"); TORCH_CHECK(pos->size(1) == H, "pos table"); }
+  if (typ) { CHECK_BF16(*typ); CHECK_CONTIG(*typ); TORCH_CHECK(typ->size(1) == H, "type table"); }
+  if (type_ids) { CHECK_I32(*type_ids); TORCH_CHECK(type_ids->numel() == T, "type_ids"); }
+  at::Tensor out = at::empty({T, H}, tok.options());
+  int rc = lk_embed_layernorm(bp(out), ip(ids), ipo(pos_ids), ipo(type_ids), bp(tok), bpo(pos), bpo(typ),
+                              bp(w), bp(b), T, H, (float)eps, cur_stream());
+  CHECK_RC(rc, "embed_layernorm");
+  return out;
+}
+
+at::Tensor silu_mul(const at::Tensor& x, const c10::optional<at::Tensor>& out_) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_LASTDIM(x);
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % 2 == 0, "x must be [T, 2I]");
+  check_rows16(x, "x");
+  const long T = x.size(0);
+  const int I = x.size(1) / 2;
+  at::Tensor out = out_ ? *out_ : at::empty({T, I}, x.options());
+  TORCH_CHECK(out.size(0) == T && out.size(1) == I, "out shape"); CHECK_LASTDIM(out);
+  int rc = lk_silu_mul(bp(out), bp(x), T, I, x.stride(0), out.stride(0), cur_stream());
+  CHECK_RC(rc, "silu_mul");
+  return out;
+}
+
+void activation_(at::Tensor& x, const c10::optional<at::Tensor>& bias, int64_t kind) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_LASTDIM(x);
+  TORCH_CHECK(x.dim() == 2, "x must be 2-D");
+  check_rows16(x, "x");
+  if (bias) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == x.size(1), "bias shape"); }
+  int rc = lk_activation(bp(x), bpo(bias), x.size(0), x.size(1), x.stride(0), (int)kind, cur_stream());
+  CHECK_RC(rc, "activation");
+}
+
+void rope_kv_(at::Tensor& qkv, const at::Tensor& positions, const at::Tensor& cos_sin, int64_t Hq,
+              int64_t Hkv, int64_t D, const c10::optional<at::Tensor>& k_cache,
+              const c10::optional<at::Tensor>& v_cache, const c10::optional<at::Tensor>& slots,
+              bool neox, bool write_k_inplace) {
+  CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_LASTDIM(qkv); CHECK_I32(positions); CHECK_F32(cos_sin);
+  CHECK_CONTIG(cos_sin); CHECK_CONTIG(positions);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) >= (Hq + 2 * Hkv) * D, "qkv must be [T, >=(Hq+2Hkv)*D]");
+  TORCH_CHECK(cos_sin.size(1) == D, "cos_sin must be [max_pos, D]");
+  check_rows16(qkv, "qkv");
+  const long T = qkv.size(0);
+  TORCH_CHECK(positions.numel() == T, "positions");
+  int BS = 1;
+  if (k_cache || v_cache) {
+    TORCH_CHECK(k_cache && v_cache && slots, "k_cache, v_cache and slots go together");
+    CHECK_BF16(*k_cache); CHECK_BF16(*v_cache); CHECK_CONTIG(*k_cache); CHECK_CONTIG(*v_cache);
+    CHECK_I32(*slots); TORCH_CHECK(slots->numel() == T, "slots");
+    TORCH_CHECK(k_cache->dim() == 4 && k_cache->size(1) == Hkv && k_cache->size(3) == D, "k_cache must be [NB, Hkv, BS, D]");
+    TORCH_CHECK(v_cache->sizes() == k_cache->sizes(), "v_cache shape");
+    BS = k_cache->size(2);
+  }
+  int rc = lk_rope_kv(bp(qkv), qkv.stride(0), ip(positions), cos_sin.data_ptr<float>(), T, Hq, Hkv, D,
+                      bpo(k_cache), bpo(v_cache), ipo(slots), BS, neox ? 1 : 0, write_k_inplace ? 1 : 0,
+                      cur_stream());
+  CHECK_RC(rc, "rope_kv");
+}
+
+void kv_write(const at::Tensor& k, const at::Tensor& v, at::Tensor& k_cache, at::Tensor& v_cache,
+              const at::Tensor& slots) {
+  CHECK_CUDA(k); CHECK_BF16(k); CHECK_BF16(v); CHECK_I32(slots);
+  TORCH_CHECK(k.dim() == 3 && v.sizes() == k.sizes(), "k/v must be [T, Hkv, D]");
+  TORCH_CHECK(k.stride(2) == 1 && k.stride(1) == k.size(2) && v.stride(2) == 1 && v.stride(1) == v.size(2), "k/v inner layout");
+  const int Hkv = k.size(1), D = k.size(2);
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == D && k_cache.is_contiguous() && v_cache.is_contiguous(), "cache layout");
+  int rc = lk_kv_write(bp(k), k.stride(0), bp(v), v.stride(0), bp(k_cache), bp(v_cache), ip(slots),
+                       k.size(0), Hkv, D, k_cache.size(2), cur_stream());
+  CHECK_RC(rc, "kv_write");
+}
+
+int64_t decode_splits(int64_t max_context) { return lk_decode_splits((int)max_context); }
+
+at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                        const at::Tensor& block_tables, const at::Tensor& ctx_lens, int64_t max_splits,
+                        double scale, const c10::optional<at::Tensor>& part_o,
+                        const c10::optional<at::Tensor>& part_ml, const c10::optional<at::Tensor>& out_) {
+  CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  CHECK_I32(block_tables); CHECK_I32(ctx_lens); CHECK_CONTIG(ctx_lens);
+  TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == q.size(2), "q must be [B, Hq, D] (row-strided)");
+  const int B = q.size(0), Hq = q.size(1), D = q.size(2);
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.is_contiguous() && v_cache.sizes() == k_cache.sizes(), "cache layout");
+  const int Hkv = k_cache.size(1), BS = k_cache.size(2);
+  TORCH_CHECK(k_cache.size(3) == D, "head dim mismatch");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && block_tables.stride(1) == 1, "block_tables");
+  TORCH_CHECK(ctx_lens.numel() >= B, "ctx_lens");
+  TORCH_CHECK(max_splits >= 1 && (long)max_splits * 512 <= (long)block_tables.size(1) * BS + 511, "max_splits exceeds block table capacity");
+  check_rows16(q, "q");
+  at::Tensor out = out_ ? *out_ : at::empty({B, Hq, D}, q.options());
+  TORCH_CHECK(out.size(0) == B && out.size(1) == Hq && out.size(2) == D && out.stride(2) == 1 && out.stride(1) == D, "out layout");
+  at::Tensor po, pm;
+  if (max_splits > 1) {
+    po = part_o ? *part_o : at::empty({B, Hq, max_splits, D}, q.options().dtype(at::kFloat));
+    pm = part_ml ? *part_ml : at::empty({B, Hq, max_splits, 2}, q.options().dtype(at::kFloat));
+    TORCH_CHECK(po.numel() >= (long)B * Hq * max_splits * D && pm.numel() >= (long)B * Hq * max_splits * 2, "partials too small");
+    CHECK_F32(po); CHECK_F32(pm);
+  }
+  int rc = lk_paged_decode(bp(q), q.stride(0), bp(k_cache), bp(v_cache), ip(block_tables), block_tables.stride(0),
+                           ip(ctx_lens), bp(out), out.stride(0), max_splits > 1 ? po.data_ptr<float>() : nullptr,
+                           max_splits > 1 ? pm.data_ptr<float>() : nullptr, B, Hq, Hkv, D, BS, (int)max_splits,
+                           (float)scale, cur_stream());
+  CHECK_RC(rc, "paged_decode");
+  return out;
+}
+
+int64_t prefill_rows_per_tile(int64_t G) { return lk_prefill_rows_per_tile((int)G); }
+
+at::Tensor flash_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                         const c10::optional<at::Tensor>& block_tables, const at::Tensor& cu_q,
+                         const c10::optional<at::Tensor>& ctx_lens, const at::Tensor& tile_seq,
+                         const at::Tensor& tile_q0, int64_t Hq, int64_t Hkv, int64_t D, double scale,
+                         bool causal, const c10::optional<at::Tensor>& out_) {
+  CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); CHECK_LASTDIM(q);
+  CHECK_I32(cu_q); CHECK_I32(tile_seq); CHECK_I32(tile_q0);
+  TORCH_CHECK(q.dim() == 2 && q.size(1) >= Hq * D, "q must be [T, >=Hq*D] (head-major rows)");
+  check_rows16(q, "q");
+  const long T = q.size(0);
+  const bool paged = block_tables.has_value();
+  int BS = 0, bt_stride = 0;
+  long ks = 0, vs = 0;
+  if (paged) {
+    CHECK_I32(*block_tables);
+    TORCH_CHECK(ctx_lens.has_value(), "ctx_lens required for paged prefill");
+    TORCH_CHECK(k.dim() == 4 && k.size(1) == Hkv && k.size(3) == D && k.is_contiguous() && v.is_contiguous() && v.sizes() == k.sizes(), "cache layout");
+    BS = k.size(2);
+    bt_stride = block_tables->stride(0);
+  } else {
+    TORCH_CHECK(k.dim() == 2 && v.dim() == 2 && k.size(0) == T && v.size(0) == T && k.size(1) >= Hkv * D && v.size(1) >= Hkv * D, "dense k/v must be [T, >=Hkv*D]");
+    CHECK_LASTDIM(k); CHECK_LASTDIM(v); check_rows16(k, "k"); check_rows16(v, "v");
+    ks = k.stride(0);
+    vs = v.stride(0);
+  }
+  if (ctx_lens) CHECK_I32(*ctx_lens);
+  TORCH_CHECK(tile_seq.numel() == tile_q0.numel(), "tile arrays");
+  at::Tensor out = out_ ? *out_ : at::empty({T, Hq * D}, q.options());
+  CHECK_LASTDIM(out); check_rows16(out, "out");
+  TORCH_CHECK(out.size(0) == T && out.size(1) >= Hq * D, "out shape");
+  int rc = lk_flash_prefill(bp(q), q.stride(0), bp(k), bp(v), ks, vs, paged ? ip(*block_tables) : nullptr,
+                            bt_stride, ip(cu_q), ipo(ctx_lens), ip(tile_seq), ip(tile_q0), tile_seq.numel(),
+                            bp(out), out.stride(0), Hq, Hkv, D, BS, (float)scale, causal ? 1 : 0, paged ? 1 : 0,
+                            cur_stream());
+  CHECK_RC(rc, "flash_prefill");
+  return out;
+}
+
+std::vector<at::Tensor> knn_topk(const at::Tensor& corpus, const at::Tensor& cnorm, const at::Tensor& queries,
+                                 const at::Tensor& qnorm, int64_t K) {
+  CHECK_CUDA(corpus); CHECK_BF16(corpus); CHECK_CONTIG(corpus); CHECK_F32(cnorm); CHECK_CONTIG(cnorm);
+  CHECK_BF16(queries); CHECK_CONTIG(queries); CHECK_F32(qnorm); CHECK_CONTIG(qnorm);
+  TORCH_CHECK(corpus.dim() == 2 && queries.dim() == 2 && corpus.size(1) == queries.size(1), "dimension mismatch");
+  const long N = corpus.size(0);
+  const int D = corpus.size(1), nq = queries.size(0);
+  TORCH_CHECK(cnorm.numel() == N && qnorm.numel() == nq, "norm shapes");
+  TORCH_CHECK(K >= 1 && K <= 64, "K in [1, 64]");
+  auto fo = corpus.options().dtype(at::kFloat);
+  auto io = corpus.options().dtype(at::kInt);
+  const int kk = (int)std::min<long>(K, std::max<long>(N, 1));
+  at::Tensor out_s = at::full({nq, (long)K}, -INFINITY, fo);
+  at::Tensor out_i = at::full({nq, (long)K}, -1, io);
+  if (N == 0 || nq == 0) return {out_s, out_i};
+  const int nb = lk_knn_nblocks(N);
+  at::Tensor ps = at::empty({nq, nb, kk}, fo);
+  at::Tensor pi = at::empty({nq, nb, kk}, io);
+  int rc = lk_knn_partial(bp(corpus), cnorm.data_ptr<float>(), N, D, bp(queries), qnorm.data_ptr<float>(), nq, kk,
+                          ps.data_ptr<float>(), pi.data_ptr<int>(), cur_stream());
+  CHECK_RC(rc, "knn_partial");
+  rc = lk_knn_merge(ps.data_ptr<float>(), pi.data_ptr<int>(), nq, nb * kk, (int)K, out_s.data_ptr<float>(),
+                    out_i.data_ptr<int>(), cur_stream());
+  CHECK_RC(rc, "knn_merge");
+  return {out_s, out_i};
+}
+
+std::vector<at::Tensor> knn_merge(const at::Tensor& cand_s, const at::Tensor& cand_i, int64_t K) {
+  CHECK_CUDA(cand_s); CHECK_F32(cand_s); CHECK_I32(cand_i); CHECK_CONTIG(cand_s); CHECK_CONTIG(cand_i);
+  TORCH_CHECK(cand_s.dim() == 2 && cand_s.sizes() == cand_i.sizes(), "candidates [nq, ncand]");
+  const int nq = cand_s.size(0), nc = cand_s.size(1);
+  at::Tensor out_s = at::empty({nq, K}, cand_s.options());
+  at::Tensor out_i = at::empty({nq, K}, cand_i.options());
+  int rc = lk_knn_merge(cand_s.data_ptr<float>(), cand_i.data_ptr<int>(), nq, nc, (int)K, out_s.data_ptr<float>(),
+                        out_i.data_ptr<int>(), cur_stream());
+  CHECK_RC(rc, "knn_merge");
+  return {out_s, out_i};
+}
+
+at::Tensor pool_normalize(const at::Tensor& hidden, const at::Tensor& cu, int64_t mode, bool normalize) {
+  CHECK_CUDA(hidden); CHECK_BF16(hidden); CHECK_LASTDIM(hidden); CHECK_I32(cu); CHECK_CONTIG(cu);
+  check_rows16(hidden, "hidden");
+  const int B = cu.numel() - 1, H = hidden.size(1);
+  at::Tensor out = at::empty({B, H}, hidden.options().dtype(at::kFloat));
+  int rc = lk_pool_normalize(bp(hidden), hidden.stride(0), ip(cu), B, H, (int)mode, normalize ? 1 : 0,
+                             out.data_ptr<float>(), cur_stream());
+  CHECK_RC(rc, "pool_normalize");
+  return out;
+}
+
+at::Tensor row_norms(const at::Tensor& x) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  at::Tensor out = at::empty({x.size(0)}, x.options().dtype(at::kFloat));
+  int rc = lk_row_norms(bp(x), x.size(0), x.size(1), out.data_ptr<float>(), cur_stream());
+  CHECK_RC(rc, "row_norms");
+  return out;
+}
+
+at::Tensor select_tokens(const at::Tensor& logits, const c10::optional<at::Tensor>& temps, int64_t seed,
+                         int64_t step, const c10::optional<at::Tensor>& out_) {
+  CHECK_CUDA(logits); CHECK_LASTDIM(logits);
+  TORCH_CHECK(logits.dim() == 2, "logits [B, V]");
+  const bool is_bf16 = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(is_bf16 || logits.scalar_type() == at::kFloat, "logits must be bf16 or f32");
+  TORCH_CHECK(logits.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(logits.data_ptr()) % 32 == 0, "logits rows must be 32-byte aligned");
+  const int B = logits.size(0), V = logits.size(1);
+  if (temps) { CHECK_F32(*temps); TORCH_CHECK(temps->numel() >= B, "temps"); }
+  at::Tensor out = out_ ? *out_ : at::empty({B}, logits.options().dtype(at::kInt));
+  CHECK_I32(out);
+  int rc = lk_select_tokens(logits.data_ptr(), is_bf16 ? 1 : 0, logits.stride(0), B, V,
+                            temps ? temps->data_ptr<float>() : nullptr, (unsigned long long)seed, (int)step,
+                            out.data_ptr<int>(), cur_stream());
+  CHECK_RC(rc, "select_tokens");
+  return out;
+}
+
+void repeat_penalty_(at::Tensor& logits, const at::Tensor& window, const at::Tensor& penalty) {
+  CHECK_CUDA(logits); CHECK_I32(window); CHECK_F32(penalty); CHECK_CONTIG(window);
+  const bool is_bf16 = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(window.dim() == 2 && window.size(0) == logits.size(0), "window [B, W]");
+  int rc = lk_repeat_penalty(logits.data_ptr(), is_bf16 ? 1 : 0, logits.stride(0), logits.size(0), ip(window),
+                             window.size(1), penalty.data_ptr<float>(), cur_stream());
+  CHECK_RC(rc, "repeat_penalty");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 (MI355X) HIP kernel library";
+  m.def("rmsnorm", &rmsnorm, "", py::arg("x"), py::arg("w"), py::arg("eps"), py::arg("residual") = py::none(), py::arg("out") = py::none());
+  m.def("layernorm", &layernorm, "", py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"), py::arg("residual") = py::none(), py::arg("write_residual") = false);
+  m.def("embed_layernorm", &embed_layernorm);
+  m.def("silu_mul", &silu_mul, "", py::arg("x"), py::arg("out") = py::none());
+  m.def("activation_", &activation_);
+  m.def("rope_kv_", &rope_kv_);
+  m.def("kv_write", &kv_write);
+  m.def("decode_splits", &decode_splits);
+  m.def("paged_decode", &paged_decode, "", py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("max_splits"), py::arg("scale"), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("out") = py::none());
+  m.def("prefill_rows_per_tile", &prefill_rows_per_tile);
+  m.def("flash_prefill", &flash_prefill, "", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("block_tables"), py::arg("cu_q"), py::arg("ctx_lens"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("out") = py::none());
+  m.def("knn_topk", &knn_topk);
+  m.def("knn_merge", &knn_merge);
+  m.def("pool_normalize", &pool_normalize);
+  m.def("row_norms", &row_norms);
+  m.def("select_tokens", &select_tokens, "", py::arg("logits"), py::arg("temps") = py::none(), py::arg("seed") = 0, py::arg("step") = 0, py::arg("out") = py::none());
+  m.def("repeat_penalty_", &repeat_penalty_);
+}

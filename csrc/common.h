@@ -1,0 +1,85 @@
+// Shared device helpers for the gfx950 (CDNA4) kernel library.
+//
+// Everything here is written for wave64 / MFMA hardware directly: bf16 values
+// travel as raw 16-bit patterns (ushort) so loads vectorise to 16 B/lane, and
+// reductions are 64-lane butterflies.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define LK_DEVICE __device__ __forceinline__
+
+typedef unsigned short bf16_t;  // raw bf16 bits
+typedef short short8 __attribute__((ext_vector_type(8)));
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef unsigned int uint4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+LK_DEVICE float bf2f(bf16_t v) { return __uint_as_float(((unsigned)v) << 16); }
+
+// round-to-nearest-even f32 -> bf16: gfx950 has v_cvt_pk_bf16_f32, which the
+// __bf16 cast lowers to (NaN stays NaN, unlike the integer rounding trick).
+LK_DEVICE bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+LK_DEVICE unsigned pack_bf2(float lo, float hi) {
+  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+}
+
+LK_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+LK_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block-wide sum for blockDim.x = NW*64; `red` must hold NW floats.
+template <int NW>
+LK_DEVICE float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  if constexpr (NW == 1) {
+    return v;
+  } else {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) t += red[i];
+    return t;
+  }
+}
+
+// 8 x bf16 <-> 8 x f32 through one 16-byte access
+LK_DEVICE void load8(const bf16_t* p, float* f) {
+  short8 v = *reinterpret_cast<const short8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = bf2f((bf16_t)v[i]);
+}
+LK_DEVICE void store8(bf16_t* p, const float* f) {
+  short8 v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (short)f2bf(f[i]);
+  *reinterpret_cast<short8*>(p) = v;
+}
+
+// Bijective XCD-aware remap of a flat workgroup id (8 XCDs, round-robin dispatch):
+// consecutive logical tiles land on the same XCD so they share its L2.
+LK_DEVICE int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = bid % 8, idx = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+#define LK_CHECK_LAUNCH() (void)hipGetLastError()

@@ -1,0 +1,63 @@
+// Host-callable launchers of the gfx950 kernel library.  Raw pointers + an explicit
+// stream keep the .hip translation units free of torch headers (fast rebuilds) and
+// make every launcher capturable in a hipGraph (no allocation, no sync inside).
+// Return 0 on success, <0 for an unsupported shape (checked before launch).
+#pragma once
+#include <hip/hip_runtime.h>
+
+typedef unsigned short bf16_t;
+
+// norm.hip
+int lk_rmsnorm(bf16_t* out, bf16_t* residual, const bf16_t* x, const bf16_t* w, long rows, int H,
+               float eps, long xs, long os, long rs, hipStream_t st);
+int lk_layernorm(bf16_t* out, const bf16_t* x, const bf16_t* res, bf16_t* res_out, const bf16_t* w,
+                 const bf16_t* b, long rows, int H, float eps, long xs, long os, long rs,
+                 hipStream_t st);
+int lk_embed_layernorm(bf16_t* out, const int* ids, const int* pos_ids, const int* type_ids,
+                       const bf16_t* tok, const bf16_t* pos, const bf16_t* typ, const bf16_t* w,
+                       const bf16_t* b, long rows, int H, float eps, hipStream_t st);
+
+// activation.hip
+int lk_silu_mul(bf16_t* out, const bf16_t* x, long rows, int I, long xs, long os, hipStream_t st);
+int lk_activation(bf16_t* x, const bf16_t* bias, long rows, int N, long xs, int kind,
+                  hipStream_t st);
+
+// rope_kv.hip
+int lk_rope_kv(bf16_t* qkv, long qs, const int* positions, const float* cos_sin, long T, int Hq,
+               int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,
+               int write_k_inplace, hipStream_t st);
+int lk_kv_write(const bf16_t* k, long ks, const bf16_t* v, long vs, bf16_t* kc, bf16_t* vc,
+                const int* slots, long T, int Hkv, int D, int BS, hipStream_t st);
+
+// attn_decode.hip
+int lk_decode_splits(int max_context);
+int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc,
+                    const int* block_tables, int bt_stride, const int* ctx_lens, bf16_t* out,
+                    long os, float* part_o, float* part_ml, int B, int Hq, int Hkv, int D, int BS,
+                    int max_splits, float scale, hipStream_t st);
+
+// attn_prefill.hip
+int lk_prefill_rows_per_tile(int G);
+int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v, long ks, long vs,
+                     const int* block_tables, int bt_stride, const int* cu_q, const int* ctx_lens,
+                     const int* tile_seq, const int* tile_q0, int ntiles, bf16_t* out, long os,
+                     int Hq, int Hkv, int D, int BS, float scale, int causal, int paged,
+                     hipStream_t st);
+
+// knn.hip
+int lk_knn_nblocks(long N);
+int lk_knn_partial(const bf16_t* corpus, const float* cnorm, long N, int D, const bf16_t* queries,
+                   const float* qnorm, int nq, int K, float* part_s, int* part_i, hipStream_t st);
+int lk_knn_merge(const float* cand_s, const int* cand_i, int nq, int ncand, int K, float* out_s,
+                 int* out_i, hipStream_t st);
+
+// pooling.hip
+int lk_pool_normalize(const bf16_t* hidden, long hs, const int* cu, int B, int H, int mode,
+                      int normalize, float* out, hipStream_t st);
+int lk_row_norms(const bf16_t* x, long N, int D, float* out, hipStream_t st);
+
+// sampling.hip
+int lk_select_tokens(const void* logits, int is_bf16, long ls, int B, int V, const float* temps,
+                     unsigned long long seed, int step, int* out, hipStream_t st);
+int lk_repeat_penalty(void* logits, int is_bf16, long ls, int B, const int* window, int W,
+                      const float* penalty, hipStream_t st);

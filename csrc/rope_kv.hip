@@ -1,0 +1,128 @@
+// K9 rotary embedding fused with the paged KV-cache write.
+//
+// Input is the packed output of the fused QKV projection, [T, (Hq + 2*Hkv) * D].
+// Q (and optionally K) are rotated in place; rotated K and raw V are scattered
+// into the paged cache [num_blocks, Hkv, BS, D] at slot_mapping[t] (slot = block*BS
+// + offset; negative slot = padding token, skipped).  One workgroup per token;
+// each work item moves 16 bytes per half (8 rotation pairs), so the op is a single
+// HBM-bound pass over Q, K, V and the cos/sin table row.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+template <bool NEOX>
+__global__ __launch_bounds__(128) void rope_kv_kernel(
+    bf16_t* __restrict__ qkv, long qs, const int* __restrict__ positions,
+    const float* __restrict__ cos_sin, int Hq, int Hkv, int D, bf16_t* __restrict__ kc,
+    bf16_t* __restrict__ vc, const int* __restrict__ slots, int BS, int write_k_inplace) {
+  const long t = blockIdx.x;
+  const int pos = positions[t];
+  const int half = D >> 1;
+  const float* cs = cos_sin + (long)pos * D;  // [cos(D/2) | sin(D/2)]
+  bf16_t* row = qkv + t * qs;
+  const int slot = slots ? slots[t] : -1;
+  const long blk = slot >= 0 ? slot / BS : 0;
+  const int off = slot >= 0 ? slot % BS : 0;
+  const int ipr = NEOX ? (D >> 4) : (D >> 3);  // items per head
+  const int nrot = (Hq + Hkv) * ipr;
+  for (int it = threadIdx.x; it < nrot; it += blockDim.x) {
+    const int head = it / ipr;
+    const int v = it - head * ipr;
+    bf16_t* hp = row + head * D;
+    const bool is_k = head >= Hq;
+    const int kvh = head - Hq;
+    bf16_t* kdst = (is_k && kc && slot >= 0) ? kc + ((blk * Hkv + kvh) * BS + off) * D : nullptr;
+    const bool store_src = !is_k || write_k_inplace;
+    if constexpr (NEOX) {
+      const int i0 = v * 8;
+      float x1[8], x2[8], c[8], s[8], y1[8], y2[8];
+      load8(hp + i0, x1);
+      load8(hp + half + i0, x2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        c[j] = cs[i0 + j];
+        s[j] = cs[half + i0 + j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        y1[j] = x1[j] * c[j] - x2[j] * s[j];
+        y2[j] = x2[j] * c[j] + x1[j] * s[j];
+      }
+      if (store_src) {
+        store8(hp + i0, y1);
+        store8(hp + half + i0, y2);
+      }
+      if (kdst) {
+        store8(kdst + i0, y1);
+        store8(kdst + half + i0, y2);
+      }
+    } else {
+      const int e0 = v * 8;  // elements e0..e0+7 = pairs e0/2 .. e0/2+3
+      float x[8], y[8];
+      load8(hp + e0, x);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const float c = cs[(e0 >> 1) + p], s = cs[half + (e0 >> 1) + p];
+        y[2 * p] = x[2 * p] * c - x[2 * p + 1] * s;
+        y[2 * p + 1] = x[2 * p + 1] * c + x[2 * p] * s;
+      }
+      if (store_src) store8(hp + e0, y);
+      if (kdst) store8(kdst + e0, y);
+    }
+  }
+  if (vc && slot >= 0) {
+    const int vpr = D >> 3;
+    const bf16_t* vsrc = row + (long)(Hq + Hkv) * D;
+    for (int it = threadIdx.x; it < Hkv * vpr; it += blockDim.x) {
+      const int h = it / vpr, c = (it - h * vpr) * 8;
+      *reinterpret_cast<short8*>(vc + ((blk * Hkv + h) * BS + off) * D + c) =
+          *reinterpret_cast<const short8*>(vsrc + h * D + c);
+    }
+  }
+}
+
+// plain paged write of K/V (no rotation): k,v [T, Hkv, D] with token strides ks/vs
+__global__ __launch_bounds__(128) void kv_write_kernel(const bf16_t* __restrict__ k, long ks,
+                                                       const bf16_t* __restrict__ v, long vs,
+                                                       bf16_t* __restrict__ kc,
+                                                       bf16_t* __restrict__ vc,
+                                                       const int* __restrict__ slots, int Hkv,
+                                                       int D, int BS) {
+  const long t = blockIdx.x;
+  const int slot = slots[t];
+  if (slot < 0) return;
+  const long blk = slot / BS;
+  const int off = slot % BS;
+  const int vpr = D >> 3;
+  for (int it = threadIdx.x; it < Hkv * vpr; it += blockDim.x) {
+    const int h = it / vpr, c = (it - h * vpr) * 8;
+    const long dst = ((blk * Hkv + h) * BS + off) * D + c;
+    *reinterpret_cast<short8*>(kc + dst) = *reinterpret_cast<const short8*>(k + t * ks + h * D + c);
+    *reinterpret_cast<short8*>(vc + dst) = *reinterpret_cast<const short8*>(v + t * vs + h * D + c);
+  }
+}
+
+}  // namespace
+
+int lk_rope_kv(bf16_t* qkv, long qs, const int* positions, const float* cos_sin, long T, int Hq,
+               int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,
+               int write_k_inplace, hipStream_t st) {
+  if (D % 16 || T < 0) return -1;
+  if (T == 0) return 0;
+  if (neox)
+    rope_kv_kernel<true><<<dim3(T), 128, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc,
+                                                  slots, BS, write_k_inplace);
+  else
+    rope_kv_kernel<false><<<dim3(T), 128, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc,
+                                                   vc, slots, BS, write_k_inplace);
+  return 0;
+}
+
+int lk_kv_write(const bf16_t* k, long ks, const bf16_t* v, long vs, bf16_t* kc, bf16_t* vc,
+                const int* slots, long T, int Hkv, int D, int BS, hipStream_t st) {
+  if (D % 8 || T < 0) return -1;
+  if (T == 0) return 0;
+  kv_write_kernel<<<dim3(T), 128, 0, st>>>(k, ks, v, vs, kc, vc, slots, Hkv, D, BS);
+  return 0;
+}

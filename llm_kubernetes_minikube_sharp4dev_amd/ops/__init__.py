@@ -1,0 +1,216 @@
+"""Kernel entry points.  GPU tensors -> hand-written gfx950 HIP kernels (``_C``);
+CPU tensors -> fp32 torch references (``reference``).  See ``_ext`` for the policy.
+
+Layouts are documented in :mod:`.reference`.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import reference as ref
+from ._ext import available, force_reference, lib, use_hip  # noqa: F401
+
+__all__ = [
+    "rmsnorm", "layernorm", "embed_layernorm", "silu_mul", "gelu_", "relu_", "rope_kv_",
+    "kv_write", "paged_decode", "flash_prefill", "prefill_tiles", "knn_topk", "knn_merge",
+    "pool_normalize", "row_norms", "select_tokens", "repeat_penalty_", "linear",
+    "decode_splits", "rope_cos_sin",
+]
+
+rope_cos_sin = ref.rope_cos_sin
+DECODE_SPLIT = 512  # keys per decode workgroup (csrc/attn_decode.hip kSplit)
+
+
+def rmsnorm(x, w, eps: float, residual: Optional[torch.Tensor] = None, out=None):
+    """out = RMSNorm(x [+ residual]) * w; if ``residual`` is given it is updated in
+    place to ``x + residual`` (fused add+norm of the pre-norm decoder block)."""
+    if use_hip(x):
+        return lib().rmsnorm(x, w, eps, residual, out)
+    y = ref.rmsnorm(x, w, eps, residual)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def layernorm(x, w, b, eps: float, residual=None, write_residual: bool = False):
+    if use_hip(x):
+        return lib().layernorm(x, w, b, eps, residual, write_residual)
+    return ref.layernorm(x, w, b, eps, residual, write_residual)
+
+
+def embed_layernorm(ids, pos_ids, type_ids, tok, pos, typ, w, b, eps: float):
+    if use_hip(tok):
+        return lib().embed_layernorm(ids, pos_ids, type_ids, tok, pos, typ, w, b, eps)
+    return ref.embed_layernorm(ids, pos_ids, type_ids, tok, pos, typ, w, b, eps)
+
+
+def silu_mul(x, out=None):
+    if use_hip(x):
+        return lib().silu_mul(x, out)
+    y = ref.silu_mul(x)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def gelu_(x, bias=None, approximate: str = "none"):
+    kind = 1 if approximate == "tanh" else 0
+    if use_hip(x):
+        lib().activation_(x, bias, kind)
+        return x
+    return ref.activation_(x, bias, kind)
+
+
+def relu_(x, bias=None):
+    if use_hip(x):
+        lib().activation_(x, bias, 2)
+        return x
+    return ref.activation_(x, bias, 2)
+
+
+def rope_kv_(qkv, positions, cos_sin, Hq: int, Hkv: int, D: int, k_cache=None, v_cache=None,
+             slots=None, neox: bool = True, write_k_inplace: bool = False):
+    if use_hip(qkv):
+        lib().rope_kv_(qkv, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache, slots, neox,
+                       write_k_inplace)
+        return qkv
+    return ref.rope_kv_(qkv, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache, slots, neox,
+                        write_k_inplace)
+
+
+def kv_write(k, v, k_cache, v_cache, slots):
+    if use_hip(k):
+        return lib().kv_write(k, v, k_cache, v_cache, slots)
+    return ref.kv_write(k, v, k_cache, v_cache, slots)
+
+
+def decode_splits(max_context: int) -> int:
+    return max(1, (int(max_context) + DECODE_SPLIT - 1) // DECODE_SPLIT)
+
+
+def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_splits: int,
+                 part_o=None, part_ml=None, out=None):
+    """q [B, Hq, D] -> [B, Hq, D].  ``max_splits`` = decode_splits(max context the
+    block tables can hold) — static, so the launch is hipGraph-capturable."""
+    if use_hip(q):
+        return lib().paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, max_splits, scale,
+                                  part_o, part_ml, out)
+    y = ref.paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def prefill_rows_per_tile(G: int) -> int:
+    return 32 if G >= 4 else 32 * (4 // G)
+
+
+def prefill_tiles(q_lens: Sequence[int], ctx_lens: Sequence[int], G: int, causal: bool):
+    """Query tiles (seq, q0) for the flash kernel, heaviest first (LPT scheduling:
+    with causal masking a tile's cost grows with the keys it sees)."""
+    qb = prefill_rows_per_tile(G)
+    seqs, q0s, cost = [], [], []
+    for b, (ql, cl) in enumerate(zip(q_lens, ctx_lens)):
+        past = cl - ql
+        for q0 in range(0, ql, qb):
+            seqs.append(b)
+            q0s.append(q0)
+            cost.append(min(cl, past + q0 + qb) if causal else cl)
+    order = np.argsort(-np.asarray(cost, dtype=np.int64), kind="stable")
+    return (np.asarray(seqs, dtype=np.int32)[order], np.asarray(q0s, dtype=np.int32)[order])
+
+
+def flash_prefill(q, k, v, cu_q, Hq: int, Hkv: int, D: int, scale: float, causal: bool,
+                  block_tables=None, ctx_lens=None, q_lens_cpu=None, ctx_lens_cpu=None,
+                  tiles=None, out=None):
+    """Varlen flash attention.  Paged when ``block_tables`` is given (K/V caches
+    ``[NB, Hkv, BS, D]``), else dense K/V rows ``[T, >=Hkv*D]`` (encoder).
+
+    ``q_lens_cpu`` / ``ctx_lens_cpu``: host copies of the lengths (the scheduler has
+    them), used to build the tile list without a device sync."""
+    if use_hip(q):
+        if tiles is None:
+            if q_lens_cpu is None:
+                cu = cu_q.cpu().tolist()
+                q_lens_cpu = [cu[i + 1] - cu[i] for i in range(len(cu) - 1)]
+            if ctx_lens_cpu is None:
+                ctx_lens_cpu = ctx_lens.cpu().tolist() if ctx_lens is not None else list(q_lens_cpu)
+            if block_tables is not None:
+                BS = k.shape[2]
+                need = max((int(c) + BS - 1) // BS for c in ctx_lens_cpu) if ctx_lens_cpu else 0
+                if need > block_tables.shape[1]:
+                    raise ValueError("block table too narrow for the context lengths")
+            ts, tq = prefill_tiles(q_lens_cpu, ctx_lens_cpu, Hq // Hkv, causal)
+            tiles = (torch.from_numpy(ts).to(q.device, non_blocking=True),
+                     torch.from_numpy(tq).to(q.device, non_blocking=True))
+        return lib().flash_prefill(q, k, v, block_tables, cu_q, ctx_lens, tiles[0], tiles[1], Hq,
+                                   Hkv, D, scale, causal, out)
+    y = ref.flash_prefill(q, k, v, block_tables, cu_q, ctx_lens, Hq, Hkv, D, scale, causal)
+    if out is not None:
+        out[:, : Hq * D].copy_(y)
+        return out
+    return y
+
+
+def knn_topk(corpus, cnorm, queries, qnorm, K: int):
+    """Cosine top-K (scores f32 [nq,K], indices int32 [nq,K]; -1 pads)."""
+    if use_hip(corpus):
+        s, i = lib().knn_topk(corpus, cnorm, queries, qnorm, K)
+        return s, i
+    return ref.knn_topk(corpus, cnorm, queries, qnorm, K)
+
+
+def knn_merge(cand_s, cand_i, K: int):
+    if use_hip(cand_s):
+        return tuple(lib().knn_merge(cand_s.contiguous(), cand_i.contiguous(), K))
+    nq = cand_s.shape[0]
+    out_s = torch.full((nq, K), float("-inf"))
+    out_i = torch.full((nq, K), -1, dtype=torch.int32)
+    for r in range(nq):
+        pairs = [(float(s), int(i)) for s, i in zip(cand_s[r].tolist(), cand_i[r].tolist()) if int(i) >= 0]
+        pairs.sort(key=lambda p: (-p[0], p[1]))
+        for j, (s, i) in enumerate(pairs[:K]):
+            out_s[r, j] = s
+            out_i[r, j] = i
+    return out_s, out_i
+
+
+def pool_normalize(hidden, cu, mode: int, normalize: bool = True):
+    if use_hip(hidden):
+        return lib().pool_normalize(hidden, cu, mode, normalize)
+    return ref.pool_normalize(hidden, cu, mode, normalize)
+
+
+def row_norms(x):
+    if use_hip(x):
+        return lib().row_norms(x.contiguous())
+    return ref.row_norms(x)
+
+
+def select_tokens(logits, temps=None, seed: int = 0, step: int = 0, out=None):
+    if use_hip(logits):
+        return lib().select_tokens(logits, temps, int(seed) & ((1 << 63) - 1), int(step), out)
+    return ref.select_tokens(logits, temps, seed, step)
+
+
+def repeat_penalty_(logits, window, penalty):
+    if use_hip(logits):
+        lib().repeat_penalty_(logits, window, penalty)
+        return logits
+    return ref.repeat_penalty_(logits, window, penalty)
+
+
+def linear(x, w, b=None):
+    """Plain projection GEMM (hipBLASLt through torch on the GPU)."""
+    return torch.nn.functional.linear(x, w, b)
+
+
+def softmax_scale(D: int) -> float:
+    return 1.0 / math.sqrt(D)

@@ -1,0 +1,81 @@
+"""Tensor-parallel process group helpers (RCCL over xGMI through torch.distributed's
+``nccl`` backend on ROCm; ``gloo`` for CPU tests).
+
+Sharding scheme (Megatron-style, sized for 8xMI355X xGMI full mesh):
+  * column-parallel: fused QKV (whole heads per rank), fused gate_up (I/tp per rank)
+  * row-parallel:    o_proj, down_proj -> one all-reduce each per layer
+  * vocab-parallel:  embedding (masked lookup + all-reduce) and LM head
+                     (local logits; greedy = all-gather of per-rank (max, argmax))
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class TPGroup:
+    rank: int = 0
+    size: int = 1
+    group: Optional[object] = None
+
+    @property
+    def enabled(self) -> bool:
+        return self.size > 1
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.size > 1:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+    def all_gather_cat(self, t: torch.Tensor, dim: int = -1) -> torch.Tensor:
+        if self.size == 1:
+            return t
+        parts = [torch.empty_like(t) for _ in range(self.size)]
+        dist.all_gather(parts, t.contiguous(), group=self.group)
+        return torch.cat(parts, dim=dim)
+
+    def shard(self, n: int) -> tuple[int, int]:
+        """[start, end) of this rank's slice of a dimension of size n (n % size == 0)."""
+        if n % self.size:
+            raise ValueError(f"dimension {n} not divisible by tp={self.size}")
+        per = n // self.size
+        return self.rank * per, (self.rank + 1) * per
+
+
+SINGLE = TPGroup()
+
+
+def init_distributed(backend: Optional[str] = None) -> TPGroup:
+    """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* env (torchrun) and return
+    a TP group spanning the world.  No-op (single rank) when WORLD_SIZE is unset."""
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws <= 1:
+        return SINGLE
+    if not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        if backend == "nccl":
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        dist.init_process_group(backend=backend)
+    return TPGroup(dist.get_rank(), dist.get_world_size(), dist.group.WORLD)
+
+
+def new_tp_groups(tp_size: int) -> TPGroup:
+    """Split the world into contiguous TP groups of ``tp_size`` (DP across groups)."""
+    ws, rank = dist.get_world_size(), dist.get_rank()
+    if ws % tp_size:
+        raise ValueError("world size must be a multiple of tp size")
+    mine = None
+    for g in range(ws // tp_size):
+        ranks = list(range(g * tp_size, (g + 1) * tp_size))
+        grp = dist.new_group(ranks)
+        if rank in ranks:
+            mine = TPGroup(ranks.index(rank), tp_size, grp)
+    return mine

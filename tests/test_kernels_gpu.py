@@ -1,0 +1,269 @@
+"""Numerics of every HIP kernel vs the plain-PyTorch fp32 reference (ops.reference)."""
+import math
+
+import pytest
+import torch
+
+from llm_kubernetes_minikube_sharp4dev_amd import ops
+from llm_kubernetes_minikube_sharp4dev_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, atol, rtol=0.0, msg=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item() if a.numel() else 0.0
+    tol = atol + rtol * b.abs().max().item() if b.numel() else atol
+    assert err <= tol, f"{msg} max abs err {err:.4g} > {tol:.4g}"
+
+
+@pytest.mark.parametrize("H", [384, 768, 4096, 8192])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rmsnorm(hip, H, with_res):
+    torch.manual_seed(0)
+    x = torch.randn(37, H, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(H, device=DEV, dtype=torch.bfloat16)
+    res = torch.randn(37, H, device=DEV, dtype=torch.bfloat16) if with_res else None
+    res2 = res.clone() if with_res else None
+    y = hip.rmsnorm(x, w, 1e-5, res, None)
+    y_ref = ref.rmsnorm(x, w, 1e-5, res2)
+    _close(y, y_ref, 0.05, 0.01, "rmsnorm")
+    if with_res:
+        _close(res, res2, 1e-2, 0, "residual")
+
+
+@pytest.mark.parametrize("H", [384, 768, 1024])
+def test_layernorm(hip, H):
+    torch.manual_seed(1)
+    x = torch.randn(29, H, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn(29, H, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(H, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(H, device=DEV, dtype=torch.bfloat16)
+    r2 = r.clone()
+    y = hip.layernorm(x, w, b, 1e-12, r, True)
+    y_ref = ref.layernorm(x, w, b, 1e-12, r2, True)
+    _close(y, y_ref, 0.05, 0.01, "layernorm")
+    _close(r, r2, 1e-2, 0, "residual")
+
+
+def test_embed_layernorm(hip):
+    torch.manual_seed(2)
+    V, P, H, T = 1000, 512, 768, 50
+    tok = torch.randn(V, H, device=DEV, dtype=torch.bfloat16)
+    pos = torch.randn(P, H, device=DEV, dtype=torch.bfloat16)
+    typ = torch.randn(2, H, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(H, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(H, device=DEV, dtype=torch.bfloat16)
+    ids = torch.randint(0, V, (T,), device=DEV, dtype=torch.int32)
+    pids = torch.randint(0, P, (T,), device=DEV, dtype=torch.int32)
+    tids = torch.randint(0, 2, (T,), device=DEV, dtype=torch.int32)
+    y = hip.embed_layernorm(ids, pids, tids, tok, pos, typ, w, b, 1e-12)
+    _close(y, ref.embed_layernorm(ids, pids, tids, tok, pos, typ, w, b, 1e-12), 0.05, 0.01)
+
+
+def test_activations(hip):
+    torch.manual_seed(3)
+    x = torch.randn(33, 2 * 1536, device=DEV, dtype=torch.bfloat16)
+    _close(hip.silu_mul(x, None), ref.silu_mul(x), 0.02, 0.01, "silu_mul")
+    for kind in (0, 1, 2):
+        y = torch.randn(17, 3072, device=DEV, dtype=torch.bfloat16)
+        bias = torch.randn(3072, device=DEV, dtype=torch.bfloat16)
+        y2 = y.clone()
+        hip.activation_(y, bias, kind)
+        ref.activation_(y2, bias, kind)
+        _close(y, y2, 0.02, 0.01, f"act{kind}")
+
+
+@pytest.mark.parametrize("neox", [True, False])
+def test_rope_kv(hip, neox):
+    torch.manual_seed(4)
+    T, Hq, Hkv, D, BS, NB = 45, 32, 8, 128, 16, 8
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
+    cs = ref.rope_cos_sin(4096, D, 500000.0, device=DEV)
+    kc = torch.zeros(NB, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    slots = torch.randperm(NB * BS, device=DEV)[:T].int()
+    slots[3] = -1
+    qkv2, kc2, vc2 = qkv.clone(), kc.clone(), vc.clone()
+    hip.rope_kv_(qkv, pos, cs, Hq, Hkv, D, kc, vc, slots, neox, True)
+    ref.rope_kv_(qkv2, pos, cs, Hq, Hkv, D, kc2, vc2, slots, neox, True)
+    _close(qkv, qkv2, 0.03, 0.0, "qkv")
+    _close(kc, kc2, 0.03, 0.0, "k cache")
+    _close(vc, vc2, 0.0, 0.0, "v cache")
+
+
+def _paged_setup(B, ctx, Hkv, D, BS, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    nblk = [(c + BS - 1) // BS for c in ctx]
+    NB = sum(nblk) + 3
+    kc = torch.randn(NB, Hkv, BS, D, generator=g).to(DEV, torch.bfloat16)
+    vc = torch.randn(NB, Hkv, BS, D, generator=g).to(DEV, torch.bfloat16)
+    perm = torch.randperm(NB, generator=g).tolist()
+    width = max(nblk)
+    bt = torch.zeros(B, width, dtype=torch.int32)
+    p = 0
+    for b in range(B):
+        for j in range(nblk[b]):
+            bt[b, j] = perm[p]
+            p += 1
+    return kc, vc, bt.to(DEV)
+
+
+@pytest.mark.parametrize("G", [1, 4, 8])
+@pytest.mark.parametrize("D", [64, 128])
+def test_paged_decode(hip, G, D):
+    torch.manual_seed(6)
+    Hkv, BS = 2, 16
+    Hq = Hkv * G
+    ctx = [1, 17, 511, 512, 513, 1500, 2100]
+    B = len(ctx)
+    kc, vc, bt = _paged_setup(B, ctx, Hkv, D, BS)
+    q = torch.randn(B, Hq, D, device=DEV, dtype=torch.bfloat16)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    max_splits = ops.decode_splits(bt.shape[1] * BS)
+    scale = 1 / math.sqrt(D)
+    y = hip.paged_decode(q, kc, vc, bt, cl, max_splits, scale, None, None, None)
+    y_ref = ref.paged_decode(q, kc, vc, bt, cl, scale)
+    _close(y, y_ref, 0.02, 0.0, "paged decode")
+
+
+@pytest.mark.parametrize("G", [1, 2, 4, 8])
+@pytest.mark.parametrize("D", [64, 128])
+def test_flash_prefill_paged(G, D):
+    torch.manual_seed(7)
+    Hkv, BS = 2, 16
+    Hq = Hkv * G
+    q_lens = [1, 33, 100, 257, 64]
+    past = [0, 5, 0, 40, 700]
+    ctx = [a + b for a, b in zip(q_lens, past)]
+    B = len(q_lens)
+    kc, vc, bt = _paged_setup(B, ctx, Hkv, D, BS, seed=8)
+    T = sum(q_lens)
+    q = torch.randn(T, Hq * D, device=DEV, dtype=torch.bfloat16)
+    cu = torch.tensor([0] + list(torch.tensor(q_lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    scale = 1 / math.sqrt(D)
+    y = ops.flash_prefill(q, kc, vc, cu, Hq, Hkv, D, scale, True, block_tables=bt, ctx_lens=cl,
+                          q_lens_cpu=q_lens, ctx_lens_cpu=ctx)
+    y_ref = ref.flash_prefill(q, kc, vc, bt, cu.cpu(), cl.cpu(), Hq, Hkv, D, scale, True)
+    _close(y, y_ref, 0.02, 0.0, "flash prefill paged")
+
+
+@pytest.mark.parametrize("D", [32, 64, 128])
+def test_flash_encoder_dense(D):
+    torch.manual_seed(9)
+    H = 4
+    q_lens = [7, 128, 300, 1]
+    T = sum(q_lens)
+    qkv = torch.randn(T, 3 * H * D, device=DEV, dtype=torch.bfloat16)
+    q, k, v = qkv[:, : H * D], qkv[:, H * D: 2 * H * D], qkv[:, 2 * H * D:]
+    cu = torch.tensor([0] + list(torch.tensor(q_lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    scale = 1 / math.sqrt(D)
+    y = ops.flash_prefill(q, k, v, cu, H, H, D, scale, False, q_lens_cpu=q_lens)
+    y_ref = ref.flash_prefill(q, k, v, None, cu.cpu(), None, H, H, D, scale, False)
+    _close(y, y_ref, 0.02, 0.0, "encoder attention")
+
+
+def test_flash_prefill_causal_dense_long():
+    torch.manual_seed(10)
+    Hq, Hkv, D = 8, 2, 128
+    q_lens = [1030]
+    T = sum(q_lens)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    q = qkv[:, : Hq * D]
+    k = qkv[:, Hq * D:(Hq + Hkv) * D]
+    v = qkv[:, (Hq + Hkv) * D:]
+    cu = torch.tensor([0, T], dtype=torch.int32, device=DEV)
+    y = ops.flash_prefill(q, k, v, cu, Hq, Hkv, D, 1 / math.sqrt(D), True, q_lens_cpu=q_lens)
+    y_ref = ref.flash_prefill(q, k, v, None, cu.cpu(), None, Hq, Hkv, D, 1 / math.sqrt(D), True)
+    _close(y, y_ref, 0.02, 0.0, "causal dense")
+
+
+def test_flash_softmax_spike():
+    """Force a large running-max jump mid-sequence (online rescale path)."""
+    Hq = Hkv = 1
+    D = 128
+    T = 200
+    q = torch.full((T, D), 0.1, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(T, D, device=DEV, dtype=torch.bfloat16) * 0.1
+    k[150] = 4.0
+    v = torch.randn(T, D, device=DEV, dtype=torch.bfloat16)
+    cu = torch.tensor([0, T], dtype=torch.int32, device=DEV)
+    y = ops.flash_prefill(q, k, v, cu, Hq, Hkv, D, 1.0, True, q_lens_cpu=[T])
+    y_ref = ref.flash_prefill(q, k, v, None, cu.cpu(), None, Hq, Hkv, D, 1.0, True)
+    _close(y, y_ref, 0.03, 0.0, "spike")
+
+
+@pytest.mark.parametrize("N,D", [(1, 384), (1000, 768), (70000, 768), (5000, 1024)])
+def test_knn_topk(hip, N, D):
+    torch.manual_seed(11)
+    corpus = torch.randn(N, D, device=DEV).to(torch.bfloat16)
+    if N > 10:
+        corpus[7] = corpus[3]  # exact duplicate -> tie must keep insertion order
+    qs = torch.randn(5, D, device=DEV).to(torch.bfloat16)
+    if N > 10:
+        qs[0] = corpus[3]
+    cn = hip.row_norms(corpus)
+    qn = hip.row_norms(qs)
+    _close(cn, corpus.float().norm(dim=-1), 1e-2, 1e-3, "row norms")
+    K = 10
+    s, i = hip.knn_topk(corpus, cn, qs, qn, K)
+    sc = ref.cosine_scores(corpus.float().cpu(), cn.cpu(), qs.float().cpu(), qn.cpu())
+    rs, ri = ref.stable_topk(sc, K)
+    kk = min(K, N)
+    _close(s[:, :kk], rs[:, :kk], 2e-3, 0.0, "knn scores")
+    # indices agree wherever scores are separated by more than the fp32 accumulation noise
+    for q in range(5):
+        for j in range(kk):
+            if int(i[q, j]) != int(ri[q, j]):
+                assert abs(float(sc[q, int(i[q, j])]) - float(rs[q, j])) < 2e-3
+    if N > 10:
+        assert int(i[0, 0]) == 3 and int(i[0, 1]) == 7
+
+
+def test_pool_normalize(hip):
+    torch.manual_seed(12)
+    lens = [3, 1, 40]
+    T, H = sum(lens), 768
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+    cu = torch.tensor([0, 3, 4, 44], dtype=torch.int32, device=DEV)
+    for mode in (0, 1):
+        _close(hip.pool_normalize(x, cu, mode, True), ref.pool_normalize(x, cu.cpu(), mode, True), 1e-3, 0.0)
+
+
+def test_select_tokens(hip):
+    torch.manual_seed(13)
+    for dt in (torch.bfloat16, torch.float32):
+        lg = torch.randn(9, 128256, device=DEV).to(dt)
+        lg[2, 77] = 100.0
+        lg[2, 5] = 100.0  # tie -> lowest index
+        t = hip.select_tokens(lg, None, 0, 0, None)
+        assert torch.equal(t.cpu(), lg.float().argmax(-1).int().cpu())
+        temps = torch.zeros(9, device=DEV)
+        t2 = hip.select_tokens(lg, temps, 123, 4, None)
+        assert torch.equal(t2.cpu(), t.cpu())
+        temps.fill_(1.0)
+        t3 = hip.select_tokens(lg, temps, 123, 4, None)
+        assert int(t3[2]) in (5, 77)
+
+
+def test_select_tokens_distribution(hip):
+    """Gumbel-max sampling follows softmax(logits / T)."""
+    lg = torch.tensor([[0.0, 1.0, 2.0, -1.0] + [-1e9] * 4], device=DEV).repeat(4000, 1)
+    temps = torch.full((4000,), 1.0, device=DEV)
+    t = hip.select_tokens(lg, temps, 7, 1, None).cpu()
+    freq = torch.bincount(t.long(), minlength=8)[:4].float() / 4000
+    p = torch.softmax(torch.tensor([0.0, 1.0, 2.0, -1.0]), 0)
+    assert (freq - p).abs().max() < 0.04
+
+
+def test_repeat_penalty(hip):
+    lg = torch.randn(3, 1000, device=DEV)
+    win = torch.tensor([[1, 2, 2, -1], [5, 5, 5, 5], [-1, -1, -1, -1]], device=DEV, dtype=torch.int32)
+    pen = torch.tensor([1.1, 2.0, 1.5], device=DEV)
+    a, b = lg.clone(), lg.clone()
+    hip.repeat_penalty_(a, win, pen)
+    ref.repeat_penalty_(b, win.cpu(), pen.cpu())
+    _close(a, b, 1e-6)
