@@ -1,0 +1,193 @@
+"""The generation engine: request admission, the step loop, stop conditions and
+streaming callbacks.  ``AsyncLLMEngine`` runs the step loop on a background thread
+for the HTTP server (one engine per GPU / TP group; DP replicas are routed by
+``parallel.router``)."""
+from __future__ import annotations
+
+import asyncio
+import threading
+import time
+from typing import Callable, Optional
+
+import torch
+
+from ..utils import metrics as M
+from ..utils.logging import get_logger
+from .block_manager import make_allocator
+from .model_runner import ModelRunner
+from .sampling import Sampler, SamplingParams
+from .scheduler import Scheduler
+from .sequence import Sequence, Status
+
+log = get_logger("engine")
+
+
+class LLMEngine:
+    def __init__(self, model, tokenizer=None, block_size: int = 16, max_model_len: int = 8192,
+                 max_num_seqs: int = 256, max_num_batched_tokens: int = 65536,
+                 enable_prefix_caching: bool = True, use_graphs: bool = True, num_blocks: Optional[int] = None,
+                 kv_cache_gb: Optional[float] = None, gpu_memory_fraction: float = 0.85, seed: int = 0,
+                 eos_ids: Optional[set] = None):
+        self.model = model
+        self.tokenizer = tokenizer
+        self.runner = ModelRunner(model, block_size, max_model_len, max_num_seqs, num_blocks, kv_cache_gb,
+                                  gpu_memory_fraction, use_graphs)
+        self.allocator = make_allocator(self.runner.num_blocks, block_size, enable_prefix_caching)
+        self.scheduler = Scheduler(self.allocator, block_size, max_num_seqs, max_num_batched_tokens, max_model_len)
+        self.sampler = Sampler(model.cfg.vocab_size, seed)
+        self.max_model_len = max_model_len
+        if eos_ids is None:
+            eos_ids = set(tokenizer.eos_ids) if tokenizer is not None else set(model.cfg.eos_token_ids)
+        self.eos_ids = set(eos_ids)
+        self.lock = threading.RLock()
+        self.steps = 0
+
+    # ------------------------------------------------------------------ API
+    def add_request(self, prompt_ids: list, params: Optional[SamplingParams] = None,
+                    req_id: Optional[str] = None, on_token: Optional[Callable] = None) -> Sequence:
+        params = params or SamplingParams()
+        seq = Sequence(list(prompt_ids), params)
+        if req_id:
+            seq.req_id = req_id
+        seq.on_token = on_token
+        budget = self.max_model_len - len(seq.prompt_ids)
+        if budget <= 0:
+            raise ValueError("prompt longer than max_model_len")
+        params.max_tokens = min(params.max_tokens, budget)
+        with self.lock:
+            self.scheduler.add(seq)
+        M.REQUESTS.inc()
+        return seq
+
+    def abort(self, req_id: str) -> bool:
+        with self.lock:
+            return self.scheduler.abort(req_id)
+
+    def has_work(self) -> bool:
+        return self.scheduler.has_work()
+
+    # ------------------------------------------------------------------ step
+    def step(self) -> list:
+        """One scheduler iteration.  Returns the sequences that produced a token."""
+        with self.lock:
+            batch = self.scheduler.schedule()
+            # requests that could never fit were finished by the scheduler
+            if batch.empty:
+                return []
+            t0 = time.perf_counter()
+            rows, logits = self.runner.forward_logits(batch.items)
+            for seq, start, n in batch.items:
+                seq.num_computed = start + n
+                self.scheduler.publish_blocks(seq)
+            out = []
+            if rows:
+                seqs = [s for s, _ in rows]
+                ids = self.sampler(logits, [s.params for s in seqs], [s.output_ids for s in seqs])
+                ids = ids.tolist()
+                now = time.perf_counter()
+                for seq, tid in zip(seqs, ids):
+                    self._append(seq, int(tid), now)
+                    out.append(seq)
+            self.steps += 1
+            M.STEP_TOKENS.observe(batch.num_tokens)
+            M.STEP_TIME.observe(time.perf_counter() - t0)
+            M.KV_USAGE.set(self.allocator.usage())
+            M.RUNNING.set(len(self.scheduler.running))
+            return out
+
+    def _append(self, seq: Sequence, tid: int, now: float):
+        if seq.first_token_at is None:
+            seq.first_token_at = now
+        seq.output_ids.append(tid)
+        p = seq.params
+        reason = None
+        n = len(seq.output_ids)
+        if not p.ignore_eos and tid in self.eos_ids and n > p.min_tokens:
+            reason = "stop"
+        elif n >= p.max_tokens:
+            reason = "length"
+        elif seq.length >= self.max_model_len:
+            reason = "length"
+        if p.stop and self.tokenizer is not None and reason is None:
+            tail = self.tokenizer.decode(seq.output_ids[-32:])
+            if any(s and s in tail for s in p.stop):
+                reason = "stop"
+        if reason:
+            self.scheduler.finish(seq, reason)
+            M.GEN_TOKENS.inc(n)
+        if seq.on_token is not None:
+            try:
+                seq.on_token(seq, tid, reason is not None)
+            except Exception:  # pragma: no cover - a client callback must not kill the loop
+                log.exception("on_token callback failed")
+
+    def run_until_done(self, seqs: Optional[list] = None, max_steps: int = 10_000_000):
+        steps = 0
+        while self.has_work() and steps < max_steps:
+            self.step()
+            steps += 1
+            if seqs is not None and all(s.finished for s in seqs):
+                break
+
+    def generate(self, prompts: list, params: Optional[SamplingParams] = None) -> list:
+        """Synchronous batch generation over token-id prompts (list of lists)."""
+        seqs = [self.add_request(p, params if params is not None else SamplingParams.greedy()) for p in prompts]
+        self.run_until_done(seqs)
+        return seqs
+
+
+class AsyncLLMEngine:
+    """Background step loop + asyncio streaming for the HTTP front-end."""
+
+    def __init__(self, engine: LLMEngine):
+        self.engine = engine
+        self._wake = threading.Event()
+        self._stop = False
+        self._thread = threading.Thread(target=self._loop, name="lk-engine", daemon=True)
+        self._thread.start()
+
+    def _loop(self):
+        while not self._stop:
+            if not self.engine.has_work():
+                self._wake.wait(0.05)
+                self._wake.clear()
+                continue
+            try:
+                self.engine.step()
+            except Exception:  # pragma: no cover
+                log.exception("engine step failed; aborting in-flight requests")
+                with self.engine.lock:
+                    for s in list(self.engine.scheduler.running) + list(self.engine.scheduler.waiting):
+                        self.engine.scheduler.abort(s.req_id)
+                        if s.on_token:
+                            s.on_token(s, -1, True)
+
+    def shutdown(self):
+        self._stop = True
+        self._wake.set()
+
+    async def stream(self, prompt_ids: list, params: SamplingParams, req_id: Optional[str] = None):
+        """Async generator of (token_id, finished, seq)."""
+        loop = asyncio.get_running_loop()
+        q: asyncio.Queue = asyncio.Queue()
+
+        def cb(seq, tid, fin):
+            loop.call_soon_threadsafe(q.put_nowait, (tid, fin, seq))
+
+        seq = self.engine.add_request(prompt_ids, params, req_id, cb)
+        self._wake.set()
+        try:
+            while True:
+                tid, fin, s = await q.get()
+                yield tid, fin, s
+                if fin:
+                    break
+        finally:
+            if not seq.finished:
+                self.engine.abort(seq.req_id)
+
+    async def generate(self, prompt_ids: list, params: SamplingParams, req_id: Optional[str] = None):
+        last = None
+        async for _, fin, s in self.stream(prompt_ids, params, req_id):
+            last = s
+        return last

@@ -1,0 +1,230 @@
+"""Model runner: paged KV cache ownership, per-step input/metadata construction, and
+hipGraph-captured decode.
+
+* KV cache: one allocation ``[L, 2, num_blocks, Hkv, BS, D]`` sized from free HBM
+  (288 GB on MI355X: millions of tokens of Llama-3-8B KV at 128 KiB/token).
+* Mixed steps: ``[prefill chunk tokens | decode tokens]`` in one forward; metadata
+  (slots, cu_seqlens, block tables, flash tile list) is built once per step.
+* Pure-decode steps replay a ``torch.cuda.CUDAGraph`` (= hipGraph on ROCm)
+  captured per batch-size bucket with static input buffers: the whole 32/80-layer
+  step (GEMMs, fused norms, RoPE+KV write, split-K paged attention, LM head) is one
+  graph launch instead of ~10 launches per layer from Python.
+"""
+from __future__ import annotations
+
+import bisect
+import math
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.attention import AttnMeta
+from ..utils.logging import get_logger
+
+log = get_logger("engine.runner")
+
+
+class ModelRunner:
+    def __init__(self, model, block_size: int = 16, max_model_len: int = 8192, max_num_seqs: int = 256,
+                 num_blocks: Optional[int] = None, kv_cache_gb: Optional[float] = None,
+                 gpu_memory_fraction: float = 0.85, use_graphs: bool = True,
+                 graph_batch_sizes=(1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)):
+        self.model = model
+        self.device = model.device
+        self.bs = block_size
+        self.max_model_len = max_model_len
+        self.max_blocks = (max_model_len + block_size - 1) // block_size
+        self.max_splits = ops.decode_splits(self.max_blocks * block_size)
+        self.max_num_seqs = max_num_seqs
+        cfg = model.cfg
+        self.L = cfg.num_layers
+        self.hq, self.hkv, self.D = model.hq, model.hkv, model.D
+        dt = model.dtype
+        esz = torch.tensor([], dtype=dt).element_size()
+        block_bytes = self.L * 2 * self.hkv * block_size * self.D * esz
+        if num_blocks is None:
+            if kv_cache_gb is not None:
+                num_blocks = int(kv_cache_gb * (1 << 30) // block_bytes)
+            elif self.device.type == "cuda":
+                free, total = torch.cuda.mem_get_info(self.device)
+                budget = free - (1 - gpu_memory_fraction) * total
+                num_blocks = int(max(budget, 0) // block_bytes)
+            else:
+                num_blocks = 512
+            cap = max_num_seqs * self.max_blocks + 64
+            num_blocks = max(16, min(num_blocks, cap))
+        self.num_blocks = num_blocks
+        self.kv = torch.empty((self.L, 2, num_blocks, self.hkv, block_size, self.D), dtype=dt, device=self.device)
+        self.kv_caches = [(self.kv[l, 0], self.kv[l, 1]) for l in range(self.L)]
+        log.info("kv cache: %d blocks x %d tokens (%.1f GB)", num_blocks, block_size,
+                 num_blocks * block_bytes / 2**30)
+        self.use_graphs = use_graphs and self.device.type == "cuda"
+        self.graph_sizes = sorted(b for b in graph_batch_sizes if b <= max_num_seqs)
+        self.graphs: dict = {}
+        self._graph_pool = None
+        self._ws = None
+        self.vocab = None
+
+    # ----------------------------------------------------------- workspaces
+    def _decode_ws(self, B: int):
+        need = max(B, self.graph_sizes[-1] if self.graph_sizes else B)
+        if self._ws is None or self._ws[0].shape[0] < need:
+            po = torch.empty((need, self.hq, self.max_splits, self.D), dtype=torch.float32, device=self.device)
+            pm = torch.empty((need, self.hq, self.max_splits, 2), dtype=torch.float32, device=self.device)
+            self._ws = (po, pm)
+        return self._ws[0][:B], self._ws[1][:B]
+
+    def _slots(self, table, start, n):
+        pos = np.arange(start, start + n, dtype=np.int64)
+        blk = np.asarray(table, dtype=np.int64)[pos // self.bs]
+        return (blk * self.bs + pos % self.bs).astype(np.int32), pos.astype(np.int32)
+
+    def _bt(self, tables, width):
+        bt = np.zeros((len(tables), width), dtype=np.int32)
+        for i, t in enumerate(tables):
+            bt[i, : len(t)] = t
+        return bt
+
+    # ----------------------------------------------------------- eager step
+    def build(self, items):
+        """items: [(seq, start, n)].  Returns (ids, meta, sample_rows) where
+        sample_rows lists (seq, row) of the rows that produce a next token."""
+        pre = [it for it in items if not it[0].is_decode]
+        dec = [it for it in items if it[0].is_decode]
+        ids, pos, slots = [], [], []
+        q_lens, ctx, tables = [], [], []
+        rows = []
+        r = 0
+        for seq, start, n in pre:
+            ids.extend(seq.tokens(start, start + n))
+            s, p = self._slots(seq.block_table, start, n)
+            slots.append(s)
+            pos.append(p)
+            q_lens.append(n)
+            ctx.append(start + n)
+            tables.append(seq.block_table)
+            r += n
+            if start + n == seq.length:
+                rows.append((seq, r - 1))
+        for seq, start, n in dec:
+            ids.append(seq.token_at(start))
+            s, p = self._slots(seq.block_table, start, 1)
+            slots.append(s)
+            pos.append(p)
+            rows.append((seq, r))
+            r += 1
+        dev = self.device
+        T = r
+        meta = AttnMeta(
+            positions=torch.from_numpy(np.concatenate(pos)).to(dev, non_blocking=True),
+            slots=torch.from_numpy(np.concatenate(slots)).to(dev, non_blocking=True),
+            num_prefill_tokens=sum(q_lens), num_prefill_seqs=len(pre), num_decode=len(dec),
+        )
+        if pre:
+            cu = np.zeros(len(pre) + 1, dtype=np.int32)
+            cu[1:] = np.cumsum(q_lens)
+            width = max(len(t) for t in tables)
+            meta.cu_q = torch.from_numpy(cu).to(dev, non_blocking=True)
+            meta.ctx_lens_p = torch.tensor(ctx, dtype=torch.int32).to(dev, non_blocking=True)
+            meta.block_tables_p = torch.from_numpy(self._bt(tables, width)).to(dev, non_blocking=True)
+            meta.q_lens_cpu, meta.ctx_lens_cpu = q_lens, ctx
+        if dec:
+            dt = [s.block_table for s, _, _ in dec]
+            width = max(len(t) for t in dt)
+            meta.block_tables_d = torch.from_numpy(self._bt(dt, width)).to(dev, non_blocking=True)
+            meta.ctx_lens_d = torch.tensor([s.length for s, _, _ in dec], dtype=torch.int32).to(dev, non_blocking=True)
+            meta.max_splits = ops.decode_splits(width * self.bs)
+            if dev.type == "cuda":
+                meta.part_o, meta.part_ml = None, None  # sized by the op for this width
+        meta.logits_idx = torch.tensor([row for _, row in rows], dtype=torch.long).to(dev, non_blocking=True)
+        ids_t = torch.tensor(ids, dtype=torch.int32).to(dev, non_blocking=True)
+        assert ids_t.shape[0] == T
+        return ids_t, meta, rows
+
+    @torch.inference_mode()
+    def forward_logits(self, items):
+        """Run one step; returns (rows [(seq,row)], logits [R, V] f32)."""
+        if not items:
+            return [], None
+        if self.use_graphs and all(s.is_decode for s, _, _ in items) and len(items) <= self.graph_sizes[-1]:
+            return self._graph_step(items)
+        ids, meta, rows = self.build(items)
+        if not rows:
+            self.model(ids, meta, self.kv_caches)  # partial prefill chunks only: KV write, no logits
+            return [], None
+        h = self.model(ids, meta, self.kv_caches)
+        return rows, self.model.logits(h)
+
+    # ----------------------------------------------------------- hipGraph decode
+    def _graph_bucket(self, B):
+        i = bisect.bisect_left(self.graph_sizes, B)
+        return self.graph_sizes[i]
+
+    def _static(self, B):
+        dev = self.device
+        po, pm = self._decode_ws(B)
+        st = {
+            "ids": torch.zeros(B, dtype=torch.int32, device=dev),
+            "pos": torch.zeros(B, dtype=torch.int32, device=dev),
+            "slots": torch.full((B,), -1, dtype=torch.int32, device=dev),
+            "bt": torch.zeros((B, self.max_blocks), dtype=torch.int32, device=dev),
+            "ctx": torch.ones(B, dtype=torch.int32, device=dev),
+        }
+        st["meta"] = AttnMeta(positions=st["pos"], slots=st["slots"], num_decode=B,
+                              block_tables_d=st["bt"], ctx_lens_d=st["ctx"], max_splits=self.max_splits,
+                              part_o=po, part_ml=pm)
+        return st
+
+    def capture(self, B):
+        st = self._static(B)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm-up (allocator + lazy library init) outside capture
+                h = self.model(st["ids"], st["meta"], self.kv_caches)
+                self.model.logits(h)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        if self._graph_pool is None:
+            self._graph_pool = torch.cuda.graph_pool_handle()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self._graph_pool):
+            h = self.model(st["ids"], st["meta"], self.kv_caches)
+            st["logits"] = self.model.logits(h)
+        st["graph"] = g
+        self.graphs[B] = st
+        return st
+
+    def capture_all(self, max_batch: Optional[int] = None):
+        for B in self.graph_sizes:
+            if max_batch is None or B <= max_batch:
+                if B not in self.graphs:
+                    self.capture(B)
+
+    def _graph_step(self, items):
+        B = len(items)
+        Bg = self._graph_bucket(B)
+        st = self.graphs.get(Bg) or self.capture(Bg)
+        ids = np.zeros(Bg, dtype=np.int32)
+        pos = np.zeros(Bg, dtype=np.int32)
+        slots = np.full(Bg, -1, dtype=np.int32)
+        ctx = np.ones(Bg, dtype=np.int32)
+        bt = np.zeros((Bg, self.max_blocks), dtype=np.int32)
+        rows = []
+        for i, (seq, start, n) in enumerate(items):
+            ids[i] = seq.token_at(start)
+            pos[i] = start
+            blk = seq.block_table[start // self.bs]
+            slots[i] = blk * self.bs + start % self.bs
+            ctx[i] = seq.length
+            bt[i, : len(seq.block_table)] = seq.block_table
+            rows.append((seq, i))
+        st["ids"].copy_(torch.from_numpy(ids), non_blocking=True)
+        st["pos"].copy_(torch.from_numpy(pos), non_blocking=True)
+        st["slots"].copy_(torch.from_numpy(slots), non_blocking=True)
+        st["ctx"].copy_(torch.from_numpy(ctx), non_blocking=True)
+        st["bt"].copy_(torch.from_numpy(bt), non_blocking=True)
+        st["graph"].replay()
+        return rows, st["logits"][:B]

@@ -1,0 +1,123 @@
+"""Sampling parameters (Ollama ``options`` semantics) and the batched sampler.
+
+Fast paths: an all-greedy batch is one HIP argmax kernel over the logits; a batch
+with temperatures but no top-k/top-p is one HIP Gumbel-max kernel; top-k / top-p
+(Ollama's defaults 40 / 0.9) go through a partial top-k on the GPU.  Repetition
+penalty (Ollama default 1.1 over the last 64 tokens) is a HIP kernel on the logits.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Optional
+
+import torch
+
+from .. import ops
+
+
+@dataclass
+class SamplingParams:
+    temperature: float = 0.8
+    top_k: int = 40
+    top_p: float = 0.9
+    repeat_penalty: float = 1.1
+    repeat_last_n: int = 64
+    seed: Optional[int] = None
+    max_tokens: int = 256
+    min_tokens: int = 0
+    stop: list = field(default_factory=list)
+    ignore_eos: bool = False
+    # callable(generated_ids) -> allowed token-id tensor/list or None (constrained decoding)
+    logits_processor: Optional[Callable] = None
+
+    @classmethod
+    def greedy(cls, max_tokens: int = 256, **kw) -> "SamplingParams":
+        return cls(temperature=0.0, top_k=0, top_p=1.0, repeat_penalty=1.0, max_tokens=max_tokens, **kw)
+
+    @classmethod
+    def from_ollama(cls, options: Optional[dict], defaults=None, num_predict_default: int = 256) -> "SamplingParams":
+        """Map an Ollama ``options`` dict (temperature, top_k, top_p, repeat_penalty,
+        repeat_last_n, seed, num_predict, stop) onto SamplingParams."""
+        o = dict(options or {})
+        d = defaults
+        sp = cls(
+            temperature=float(o.get("temperature", d.temperature if d else 0.8)),
+            top_k=int(o.get("top_k", d.top_k if d else 40)),
+            top_p=float(o.get("top_p", d.top_p if d else 0.9)),
+            repeat_penalty=float(o.get("repeat_penalty", d.repeat_penalty if d else 1.1)),
+            repeat_last_n=int(o.get("repeat_last_n", d.repeat_last_n if d else 64)),
+            seed=o.get("seed"),
+        )
+        n = int(o.get("num_predict", d.num_predict if d else -1))
+        sp.max_tokens = num_predict_default if n is None or n < 0 else n
+        stop = o.get("stop") or []
+        sp.stop = [stop] if isinstance(stop, str) else list(stop)
+        return sp
+
+    @property
+    def is_greedy(self) -> bool:
+        return self.temperature <= 0.0 or self.top_k == 1
+
+
+class Sampler:
+    def __init__(self, vocab_size: int, seed: int = 0):
+        self.vocab_size = vocab_size
+        self.seed = seed
+        self.step = 0
+
+    def __call__(self, logits: torch.Tensor, params: list, histories: list) -> torch.Tensor:
+        """logits [B, V] (f32) -> int32 token ids [B] (on logits.device)."""
+        self.step += 1
+        B = logits.shape[0]
+        dev = logits.device
+        # constrained decoding: mask everything outside the allowed set
+        for i, p in enumerate(params):
+            if p.logits_processor is not None:
+                allowed = p.logits_processor(histories[i])
+                if allowed is not None:
+                    mask = torch.full((logits.shape[1],), float("-inf"), device=dev)
+                    mask[torch.as_tensor(allowed, device=dev, dtype=torch.long)] = 0.0
+                    logits[i] += mask
+        # repetition penalty
+        if any(p.repeat_penalty != 1.0 and p.repeat_last_n != 0 for p in params):
+            W = max(max((p.repeat_last_n if p.repeat_last_n > 0 else len(h)) for p, h in zip(params, histories)), 1)
+            win = torch.full((B, W), -1, dtype=torch.int32)
+            pen = torch.ones(B, dtype=torch.float32)
+            for i, (p, h) in enumerate(zip(params, histories)):
+                if p.repeat_penalty != 1.0 and p.repeat_last_n != 0 and h:
+                    n = p.repeat_last_n if p.repeat_last_n > 0 else len(h)
+                    tail = h[-n:]
+                    win[i, : len(tail)] = torch.tensor(tail, dtype=torch.int32)
+                    pen[i] = p.repeat_penalty
+            ops.repeat_penalty_(logits, win.to(dev, non_blocking=True), pen.to(dev, non_blocking=True))
+        if all(p.is_greedy for p in params):
+            return ops.select_tokens(logits)
+        temps = torch.tensor([0.0 if p.is_greedy else p.temperature for p in params], dtype=torch.float32)
+        need_filter = any((not p.is_greedy) and (0 < p.top_k < logits.shape[1] or p.top_p < 1.0) for p in params)
+        seed = self.seed
+        for p in params:
+            if p.seed is not None:
+                seed = int(p.seed)
+                break
+        if not need_filter:
+            return ops.select_tokens(logits, temps.to(dev), seed=seed, step=self.step)
+        return self._filtered(logits, params, temps.to(dev), seed)
+
+    def _filtered(self, logits, params, temps, seed):
+        kmax = max(p.top_k if p.top_k > 0 else 0 for p in params)
+        kmax = kmax if kmax > 0 else 1024
+        kmax = min((kmax + 7) // 8 * 8, logits.shape[1])  # 32-B aligned rows for the HIP select
+        vals, idx = torch.topk(logits, kmax, dim=-1)
+        B = logits.shape[0]
+        for i, p in enumerate(params):
+            if p.is_greedy:
+                continue
+            if 0 < p.top_k < kmax:
+                vals[i, p.top_k:] = float("-inf")
+            if p.top_p < 1.0:
+                probs = torch.softmax(vals[i] / max(p.temperature, 1e-6), -1)
+                cum = probs.cumsum(-1)
+                cut = (cum - probs) > p.top_p
+                vals[i, cut] = float("-inf")
+        pick = ops.select_tokens(vals.contiguous(), temps, seed=seed, step=self.step)
+        return idx.gather(1, pick.long()[:, None]).squeeze(1).int()

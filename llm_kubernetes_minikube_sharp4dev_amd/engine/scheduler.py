@@ -1,0 +1,160 @@
+"""Continuous-batching scheduler with chunked prefill, prefix caching and
+recompute preemption.
+
+Each step has a token budget (``max_num_batched_tokens``).  Running decode
+sequences are served first (1 token each, so latency-bound agent loops never wait
+behind a long RAG prefill), then running prefill chunks, then new requests are
+admitted FIFO while the budget and the KV block pool allow.  When the pool runs
+dry the most recently admitted sequence is preempted (its blocks are freed and it
+is recomputed later — usually mostly from the prefix cache).
+"""
+from __future__ import annotations
+
+import time
+from collections import deque
+from dataclasses import dataclass, field
+
+from .block_manager import NoFreeBlocks
+from .sequence import Sequence, Status
+
+
+@dataclass
+class ScheduledBatch:
+    items: list = field(default_factory=list)   # (seq, start, n_tokens)
+
+    @property
+    def empty(self) -> bool:
+        return not self.items
+
+    @property
+    def num_tokens(self) -> int:
+        return sum(n for _, _, n in self.items)
+
+
+class Scheduler:
+    def __init__(self, allocator, block_size: int, max_num_seqs: int = 256,
+                 max_num_batched_tokens: int = 65536, max_model_len: int = 8192):
+        self.alloc = allocator
+        self.bs = block_size
+        self.max_num_seqs = max_num_seqs
+        self.max_tokens = max_num_batched_tokens
+        self.max_model_len = max_model_len
+        self.waiting: deque[Sequence] = deque()
+        self.running: list[Sequence] = []
+
+    def add(self, seq: Sequence):
+        if len(seq.prompt_ids) >= self.max_model_len:
+            raise ValueError(f"prompt of {len(seq.prompt_ids)} tokens exceeds max_model_len={self.max_model_len}")
+        self.waiting.append(seq)
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    # -------------------------------------------------------------- blocks
+    def _ensure(self, seq: Sequence, total_tokens: int) -> bool:
+        need = (total_tokens + self.bs - 1) // self.bs - len(seq.block_table)
+        got = []
+        try:
+            for _ in range(need):
+                got.append(self.alloc.allocate())
+        except NoFreeBlocks:
+            self.alloc.free_all(got)
+            return False
+        seq.block_table.extend(got)
+        return True
+
+    def release(self, seq: Sequence):
+        self.alloc.free_all(seq.block_table)
+        seq.block_table = []
+
+    def _preempt(self, seq: Sequence):
+        self.release(seq)
+        seq.num_computed = 0
+        seq.num_hashed_blocks = 0
+        seq.last_hash = 0
+        seq.status = Status.WAITING
+        seq.num_preemptions += 1
+        self.waiting.appendleft(seq)
+
+    def _admit_prefix(self, seq: Sequence):
+        if seq.num_computed == 0 and not seq.block_table:
+            ids = seq.tokens(0, seq.length)
+            blocks, parent = self.alloc.match_prefix(ids)
+            if blocks:
+                seq.block_table = list(blocks)
+                seq.num_computed = len(blocks) * self.bs
+                seq.num_hashed_blocks = len(blocks)
+                seq.last_hash = parent
+                seq.num_cached_prefix = max(seq.num_cached_prefix, seq.num_computed)
+
+    # -------------------------------------------------------------- schedule
+    def schedule(self) -> ScheduledBatch:
+        batch = ScheduledBatch()
+        budget = self.max_tokens
+        # decode first, then in-flight prefill chunks (stable within each class)
+        self.running.sort(key=lambda s: 0 if s.is_decode else 1)
+        i = 0
+        while i < len(self.running) and budget > 0:
+            seq = self.running[i]
+            n = min(seq.pending, budget)
+            if not self._ensure(seq, seq.num_computed + n):
+                victim = self.running.pop()
+                self._preempt(victim)
+                if victim is seq:
+                    break
+                continue
+            batch.items.append((seq, seq.num_computed, n))
+            budget -= n
+            i += 1
+        while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs:
+            seq = self.waiting[0]
+            self._admit_prefix(seq)
+            n = min(seq.pending, budget)
+            if not self._ensure(seq, seq.num_computed + n):
+                if not self.running and not batch.items:
+                    # nothing else holds blocks: this request can never fit
+                    self.waiting.popleft()
+                    self.release(seq)
+                    seq.status = Status.FINISHED
+                    seq.finish_reason = "error: kv cache too small"
+                break
+            self.waiting.popleft()
+            seq.status = Status.RUNNING
+            if seq.prefill_started_at is None:
+                seq.prefill_started_at = time.perf_counter()
+            self.running.append(seq)
+            batch.items.append((seq, seq.num_computed, n))
+            budget -= n
+        return batch
+
+    def publish_blocks(self, seq: Sequence):
+        """Register newly completed full blocks in the prefix cache."""
+        full = seq.num_computed // self.bs
+        while seq.num_hashed_blocks < full and seq.num_hashed_blocks < len(seq.block_table):
+            j = seq.num_hashed_blocks
+            toks = seq.tokens(j * self.bs, (j + 1) * self.bs)
+            seq.last_hash = self.alloc.register(seq.block_table[j], seq.last_hash, toks)
+            seq.num_hashed_blocks += 1
+
+    def finish(self, seq: Sequence, reason: str):
+        seq.status = Status.FINISHED
+        seq.finish_reason = reason
+        seq.finished_at = time.perf_counter()
+        if seq in self.running:
+            self.running.remove(seq)
+        self.release(seq)
+
+    def abort(self, req_id: str) -> bool:
+        for q in (self.running, self.waiting):
+            for s in list(q):
+                if s.req_id == req_id:
+                    if s in self.running:
+                        self.running.remove(s)
+                    else:
+                        self.waiting.remove(s)
+                    self.release(s)
+                    s.status = Status.FINISHED
+                    s.finish_reason = "abort"
+                    s.finished_at = time.perf_counter()
+                    return True
+        return False

@@ -1,0 +1,164 @@
+"""Llama-3 family decoder (``llama3.1:8b`` — the generator the reference hard-codes at
+``Minimal_RAG/Program.cs:24`` / ``Minimal_Agent_RAG/Program.cs:12`` — and 70B for TP=8).
+
+MI355X layout decisions:
+  * fused QKV and fused gate|up weights -> one hipBLASLt GEMM each instead of 3 / 2;
+  * the residual stream is carried separately and folded into the RMSNorm kernel
+    (``x = norm(res += y)``), so no standalone add pass ever touches HBM;
+  * RoPE and the paged-KV write are one kernel on the QKV output;
+  * attention reads K/V from the paged cache (flash prefill / split-K decode);
+  * tensor parallel: column-parallel QKV / gate_up, row-parallel o / down with one
+    RCCL all-reduce each, vocab-parallel embedding + LM head.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from ..parallel.tp import SINGLE, TPGroup
+from .attention import AttnMeta, paged_attention
+from .configs import DecoderConfig
+
+
+class LlamaLayerWeights(nn.Module):
+    def __init__(self, cfg: DecoderConfig, tp: TPGroup, dtype, device):
+        super().__init__()
+        H, D = cfg.hidden, cfg.head_dim
+        hq, hkv = cfg.num_heads // tp.size, max(1, cfg.num_kv_heads // tp.size)
+        I = cfg.intermediate // tp.size
+        e = dict(dtype=dtype, device=device)
+        self.input_norm = nn.Parameter(torch.ones(H, **e), requires_grad=False)
+        self.post_norm = nn.Parameter(torch.ones(H, **e), requires_grad=False)
+        self.qkv = nn.Parameter(torch.empty((hq + 2 * hkv) * D, H, **e), requires_grad=False)
+        self.o = nn.Parameter(torch.empty(H, hq * D, **e), requires_grad=False)
+        self.gate_up = nn.Parameter(torch.empty(2 * I, H, **e), requires_grad=False)
+        self.down = nn.Parameter(torch.empty(H, I, **e), requires_grad=False)
+
+
+class LlamaModel(nn.Module):
+    def __init__(self, cfg: DecoderConfig, tp: TPGroup = SINGLE, dtype=torch.bfloat16,
+                 device="cpu"):
+        super().__init__()
+        if cfg.num_heads % tp.size:
+            raise ValueError("num_heads must divide by tp size")
+        self.cfg, self.tp = cfg, tp
+        self.dtype, self.device = dtype, torch.device(device)
+        self.hq = cfg.num_heads // tp.size
+        self.hkv = max(1, cfg.num_kv_heads // tp.size)
+        self.D = cfg.head_dim
+        self.scale = 1.0 / math.sqrt(self.D)
+        self.vocab_lo, self.vocab_hi = tp.shard(cfg.vocab_size) if cfg.vocab_size % tp.size == 0 else (0, cfg.vocab_size)
+        e = dict(dtype=dtype, device=device)
+        vloc = self.vocab_hi - self.vocab_lo
+        self.embed = nn.Parameter(torch.empty(vloc, cfg.hidden, **e), requires_grad=False)
+        self.layers = nn.ModuleList([LlamaLayerWeights(cfg, tp, dtype, device) for _ in range(cfg.num_layers)])
+        self.final_norm = nn.Parameter(torch.ones(cfg.hidden, **e), requires_grad=False)
+        self.lm_head = self.embed if cfg.tie_word_embeddings else nn.Parameter(
+            torch.empty(vloc, cfg.hidden, **e), requires_grad=False)
+        max_pos = min(cfg.max_position, 1 << 17)
+        self.register_buffer("cos_sin", ops.rope_cos_sin(max_pos, self.D, cfg.rope_theta,
+                                                         cfg.rope_scaling, device=device),
+                             persistent=False)
+
+    # ------------------------------------------------------------------ weights
+    @torch.no_grad()
+    def random_init(self, seed: int = 0, std: float = 0.02):
+        """Deterministic random weights (per-parameter seeds; generated on the
+        target device so 8B/70B init takes seconds, not minutes)."""
+        gen_dev = self.device if self.device.type == "cuda" else torch.device("cpu")
+        for i, (name, p) in enumerate(self.named_parameters()):
+            if name.endswith("norm"):
+                p.fill_(1.0)
+                continue
+            g = torch.Generator(device=gen_dev).manual_seed(seed * 7919 + i * 104729 + self.tp.rank)
+            p.copy_(torch.randn(p.shape, generator=g, device=gen_dev, dtype=torch.float32).mul_(std).to(p.dtype))
+        return self
+
+    # ------------------------------------------------------------------ forward
+    def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
+        if not self.tp.enabled:
+            return self.embed[ids.long()]
+        local = ids.long() - self.vocab_lo
+        mask = (local < 0) | (local >= self.embed.shape[0])
+        h = self.embed[local.clamp(0, self.embed.shape[0] - 1)]
+        h = h.masked_fill(mask[:, None], 0)
+        return self.tp.all_reduce_(h)
+
+    def forward(self, ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
+        """ids [T] -> final hidden states of rows ``meta.logits_idx`` (or all rows)."""
+        cfg = self.cfg
+        res = self.embed_tokens(ids)
+        x = ops.rmsnorm(res, self.layers[0].input_norm, cfg.norm_eps)
+        attn_out = None
+        n = len(self.layers)
+        for li, L in enumerate(self.layers):
+            qkv = ops.linear(x, L.qkv)
+            kc, vc = kv_caches[li]
+            ops.rope_kv_(qkv, meta.positions, self.cos_sin, self.hq, self.hkv, self.D, kc, vc,
+                         meta.slots, True, False)
+            attn_out = paged_attention(qkv, kc, vc, meta, self.hq, self.hkv, self.D, self.scale, attn_out)
+            o = ops.linear(attn_out, L.o)
+            self.tp.all_reduce_(o)
+            x = ops.rmsnorm(o, L.post_norm, cfg.norm_eps, residual=res)
+            gu = ops.linear(x, L.gate_up)
+            a = ops.silu_mul(gu)
+            d = ops.linear(a, L.down)
+            self.tp.all_reduce_(d)
+            nxt = self.layers[li + 1].input_norm if li + 1 < n else self.final_norm
+            x = ops.rmsnorm(d, nxt, cfg.norm_eps, residual=res)
+        if meta.logits_idx is not None:
+            x = x.index_select(0, meta.logits_idx)
+        return x
+
+    def logits(self, hidden: torch.Tensor, gather: bool = True, dtype=torch.float32) -> torch.Tensor:
+        lg = ops.linear(hidden, self.lm_head)
+        if self.tp.enabled and gather:
+            lg = self.tp.all_gather_cat(lg, dim=-1)
+        return lg.to(dtype) if dtype is not None else lg
+
+    # ------------------------------------------------------------------ HF checkpoint
+    @torch.no_grad()
+    def load_hf_state_dict(self, sd: dict):
+        """Load HuggingFace ``LlamaForCausalLM`` tensors (q/k/v/gate/up fused and
+        TP-sliced here)."""
+        cfg, tp, D = self.cfg, self.tp, self.D
+
+        def t(name):
+            return sd[name].to(self.dtype)
+
+        def rows(w, n_heads_total):
+            s, e = tp.shard(n_heads_total) if n_heads_total >= tp.size else (0, n_heads_total)
+            return w[s * D:e * D]
+
+        self.embed.copy_(t("model.embed_tokens.weight")[self.vocab_lo:self.vocab_hi])
+        for i, L in enumerate(self.layers):
+            p = f"model.layers.{i}."
+            q = rows(t(p + "self_attn.q_proj.weight"), cfg.num_heads)
+            k = rows(t(p + "self_attn.k_proj.weight"), cfg.num_kv_heads)
+            v = rows(t(p + "self_attn.v_proj.weight"), cfg.num_kv_heads)
+            L.qkv.copy_(torch.cat([q, k, v], 0))
+            o = t(p + "self_attn.o_proj.weight")
+            s, e = tp.shard(cfg.num_heads)
+            L.o.copy_(o[:, s * D:e * D])
+            s, e = tp.shard(cfg.intermediate)
+            g = t(p + "mlp.gate_proj.weight")[s:e]
+            u = t(p + "mlp.up_proj.weight")[s:e]
+            L.gate_up.copy_(torch.cat([g, u], 0))
+            L.down.copy_(t(p + "mlp.down_proj.weight")[:, s:e])
+            L.input_norm.copy_(t(p + "input_layernorm.weight"))
+            L.post_norm.copy_(t(p + "post_attention_layernorm.weight"))
+        self.final_norm.copy_(t("model.norm.weight"))
+        if not cfg.tie_word_embeddings:
+            key = "lm_head.weight" if "lm_head.weight" in sd else "model.embed_tokens.weight"
+            self.lm_head.copy_(t(key)[self.vocab_lo:self.vocab_hi])
+        return self
+
+    def kv_cache_shape(self, num_blocks: int, block_size: int):
+        return (num_blocks, self.hkv, block_size, self.D)
+
+    def kv_bytes_per_token(self) -> int:
+        return 2 * self.cfg.num_layers * self.hkv * self.D * torch.tensor([], dtype=self.dtype).element_size()

@@ -1,0 +1,159 @@
+"""Tokenizers.
+
+* A real checkpoint's ``tokenizer.json`` (HF ``tokenizers``) is used when a model
+  directory is given.
+* Otherwise a built-in **byte-level BPE** (reversible, any UTF-8 input) trained
+  deterministically on the synthetic runbook corpus is used, so random-init
+  benchmark runs see realistic ~4 chars/token prompt lengths and streamed output
+  decodes to text.  Trained once and cached next to this file.
+
+Special tokens follow the Llama-3 chat format (Ollama applies the model's template
+to ``/api/generate`` prompts).
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+from pathlib import Path
+from typing import Iterable, Optional
+
+SPECIALS = ["<|begin_of_text|>", "<|end_of_text|>", "<|start_header_id|>", "<|end_header_id|>",
+            "<|eot_id|>", "[CLS]", "[SEP]", "[PAD]", "[UNK]", "[MASK]"]
+_CACHE = Path(__file__).resolve().parent / "data" / "bpe_runbooks.json"
+_lock = threading.Lock()
+
+
+def _train_builtin(vocab_size: int = 16384):
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+
+    from ..rag.synthetic import training_text
+
+    tok = Tokenizer(models.BPE())
+    tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tok.decoder = decoders.ByteLevel()
+    trainer = trainers.BpeTrainer(vocab_size=vocab_size, special_tokens=SPECIALS,
+                                  initial_alphabet=pre_tokenizers.ByteLevel.alphabet(),
+                                  show_progress=False)
+    tok.train_from_iterator(training_text(), trainer=trainer)
+    return tok
+
+
+class Tokenizer:
+    """Thin wrapper with the few calls the engine needs."""
+
+    def __init__(self, hf_tok, kind: str = "builtin"):
+        self.tok = hf_tok
+        self.kind = kind
+        self.vocab_size = hf_tok.get_vocab_size()
+        v = hf_tok.get_vocab()
+        self.bos_id = v.get("<|begin_of_text|>", v.get("<s>", v.get("[CLS]", 0)))
+        self.eot_id = v.get("<|eot_id|>", v.get("</s>", v.get("[SEP]", 0)))
+        self.eos_ids = {i for i in (v.get("<|end_of_text|>"), v.get("<|eot_id|>"), v.get("</s>")) if i is not None}
+        self.cls_id = v.get("[CLS]", self.bos_id)
+        self.sep_id = v.get("[SEP]", self.eot_id)
+        self._piece_cache: Optional[list] = None
+
+    def encode(self, text: str, add_bos: bool = False) -> list[int]:
+        ids = self.tok.encode(text, add_special_tokens=False).ids
+        return ([self.bos_id] + ids) if add_bos else ids
+
+    def encode_batch(self, texts: Iterable[str]) -> list[list[int]]:
+        return [e.ids for e in self.tok.encode_batch(list(texts), add_special_tokens=False)]
+
+    def encode_for_embedding(self, texts: list[str], max_len: int = 512) -> list[list[int]]:
+        """[CLS] text [SEP], truncated (BERT-style)."""
+        out = []
+        for ids in self.encode_batch(texts):
+            ids = ids[: max_len - 2]
+            out.append([self.cls_id] + ids + [self.sep_id])
+        return out
+
+    def decode(self, ids: list[int], skip_special: bool = True) -> str:
+        ids = [i for i in ids if 0 <= i < self.vocab_size]
+        return self.tok.decode(ids, skip_special_tokens=skip_special)
+
+    def piece(self, i: int) -> str:
+        """Decoded text of a single token (for constrained decoding)."""
+        if self._piece_cache is None:
+            self._piece_cache = [self.tok.decode([j], skip_special_tokens=False) for j in range(self.vocab_size)]
+        return self._piece_cache[i] if 0 <= i < self.vocab_size else ""
+
+    def special(self, name: str) -> int:
+        return self.tok.token_to_id(name)
+
+    # ------------------------------------------------------------ chat formats
+    def chat_prompt(self, prompt: str, system: Optional[str] = None, style: str = "llama3") -> list[int]:
+        """Token ids of the model's chat template around a raw /api/generate prompt."""
+        if style == "raw":
+            return self.encode(prompt, add_bos=True)
+        sh, eh, eot = self.special("<|start_header_id|>"), self.special("<|end_header_id|>"), self.eot_id
+        ids = [self.bos_id]
+        if system:
+            ids += [sh] + self.encode("system") + [eh] + self.encode("\n\n" + system) + [eot]
+        ids += [sh] + self.encode("user") + [eh] + self.encode("\n\n" + prompt) + [eot]
+        ids += [sh] + self.encode("assistant") + [eh] + self.encode("\n\n")
+        return ids
+
+
+class IncrementalDetokenizer:
+    """Streams text for growing id lists without re-decoding emitted text and without
+    splitting multi-byte UTF-8 characters across chunks."""
+
+    def __init__(self, tok: Tokenizer):
+        self.tok = tok
+        self.ids: list[int] = []
+        self.sent = ""
+
+    def push(self, tid: int) -> str:
+        self.ids.append(tid)
+        text = self.tok.decode(self.ids)
+        if text.endswith("�"):
+            return ""
+        new = text[len(self.sent):]
+        self.sent = text
+        return new
+
+
+_builtin: Optional[Tokenizer] = None
+
+
+def builtin_tokenizer() -> Tokenizer:
+    global _builtin
+    with _lock:
+        if _builtin is None:
+            from tokenizers import Tokenizer as HFTok
+
+            if _CACHE.exists():
+                hf = HFTok.from_file(str(_CACHE))
+            else:
+                hf = _train_builtin()
+                try:
+                    _CACHE.parent.mkdir(parents=True, exist_ok=True)
+                    tmp = _CACHE.with_suffix(f".{os.getpid()}.tmp")
+                    hf.save(str(tmp))
+                    os.replace(tmp, _CACHE)
+                except OSError:
+                    pass
+            _builtin = Tokenizer(hf, "builtin")
+    return _builtin
+
+
+def load_tokenizer(path: Optional[str] = None) -> Tokenizer:
+    if path:
+        p = Path(path)
+        f = p / "tokenizer.json" if p.is_dir() else p
+        if f.exists():
+            from tokenizers import Tokenizer as HFTok
+
+            return Tokenizer(HFTok.from_file(str(f)), "hf")
+    return builtin_tokenizer()
+
+
+def describe(tok: Tokenizer) -> dict:
+    return {"kind": tok.kind, "vocab_size": tok.vocab_size, "bos": tok.bos_id, "eot": tok.eot_id}
+
+
+if __name__ == "__main__":  # pragma: no cover
+    t = builtin_tokenizer()
+    print(json.dumps(describe(t)))
