@@ -1,0 +1,105 @@
+"""Batched ``/agent_rag`` pipeline (retrieve -> gate -> augment -> generate -> gate ->
+act), the headline workload, running fully in-process on MI355X:
+
+  query embeddings (encoder kernels) -> cosine top-6 (HIP kNN, corpus in HBM)
+  -> citations ``score >= max(0.35, 0.6*best)`` -> evidence JSON (System.Text.Json
+  escaping) -> Llama-3 chat template -> continuous-batching engine (flash prefill
+  with the shared system-prompt prefix served from the prefix cache, hipGraph
+  decode) -> JSON extraction -> typed tool call -> RAG gating -> k8s action.
+
+The same per-request semantics as ``Minimal_RAG/Program.cs:106-316``; the HTTP app
+(`apps.rag_app`) serves single requests through it, the benchmark runs batches.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Any, Optional
+
+from .json_extract import extract_json_object
+from .policy import select_citations
+from .prompts import RAG_AGENT_SYSTEM, json_prompt, rag_agent_input
+from .tools import dispatch_rag_tool
+
+
+@dataclass
+class RagAgentResult:
+    prompt: str
+    status: int = 200
+    body: Any = None
+    citations: list = field(default_factory=list)
+    prompt_tokens: int = 0
+    output_tokens: int = 0
+    raw: str = ""
+    timings: dict = field(default_factory=dict)
+
+
+NO_EVIDENCE_NOTE = "Nessuna evidenza trovata nei runbook."
+
+
+class RagAgentPipeline:
+    def __init__(self, index, llm, tokenizer, k8s, cfg, chat_style: str = "llama3"):
+        self.index = index
+        self.llm = llm
+        self.tok = tokenizer
+        self.k8s = k8s
+        self.cfg = cfg
+        self.chat_style = chat_style
+
+    def plan(self, prompts: list[str]):
+        """Retrieval + gating + prompt construction for a batch of user prompts."""
+        t0 = time.perf_counter()
+        r = self.cfg.rag
+        embedder = self.index.embedder
+        if hasattr(embedder, "embed_tensor"):
+            qv = embedder.embed_tensor(prompts)
+        else:
+            qv = embedder.embed(prompts)
+        t1 = time.perf_counter()
+        res = self.index.search_vectors(qv, r.agent_topk)
+        t2 = time.perf_counter()
+        plans = []
+        texts = []
+        for p, rr in zip(prompts, res):
+            hits = self.index.hits(rr)
+            if not hits:
+                plans.append((p, None, [], []))
+                continue
+            citations, evidence = select_citations(hits, r.evidence_min_score, r.citation_best_ratio)
+            full = json_prompt(RAG_AGENT_SYSTEM, rag_agent_input(p, evidence, r.evidence_text_chars))
+            plans.append((p, full, citations, evidence))
+            texts.append(full)
+        ids = iter(self.tok.chat_prompt_batch(texts, style=self.chat_style)) if texts else iter(())
+        out = []
+        for p, full, cit, ev in plans:
+            out.append((p, next(ids) if full is not None else None, cit, ev))
+        t3 = time.perf_counter()
+        return out, {"embed_s": t1 - t0, "knn_s": t2 - t1, "prompt_s": t3 - t2}
+
+    def finish(self, prompt: str, out_ids: list, citations, evidence) -> RagAgentResult:
+        raw = self.tok.decode(out_ids)
+        tool_json = extract_json_object(raw)
+        status, body = dispatch_rag_tool(self.k8s, tool_json, citations, evidence, self.cfg)
+        return RagAgentResult(prompt, status, body, citations, 0, len(out_ids), raw)
+
+    def run_batch(self, prompts: list[str], params) -> list[RagAgentResult]:
+        """Synchronous batch through an in-process LLMEngine."""
+        plans, tim = self.plan(prompts)
+        todo = [(i, ids) for i, (_, ids, _, _) in enumerate(plans) if ids is not None]
+        seqs = {}
+        for i, ids in todo:
+            seqs[i] = self.llm.add_request(ids, params.__class__(**{**params.__dict__}))
+        t0 = time.perf_counter()
+        self.llm.run_until_done(list(seqs.values()))
+        tgen = time.perf_counter() - t0
+        results = []
+        for i, (p, ids, cit, ev) in enumerate(plans):
+            if ids is None:
+                results.append(RagAgentResult(p, 200, {"result": None, "citations": [], "note": NO_EVIDENCE_NOTE}))
+                continue
+            s = seqs[i]
+            r = self.finish(p, s.output_ids, cit, ev)
+            r.prompt_tokens = len(ids)
+            r.timings = {**tim, "generate_s": tgen, **s.metrics()}
+            results.append(r)
+        return results

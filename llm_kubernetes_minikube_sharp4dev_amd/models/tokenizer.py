@@ -95,6 +95,19 @@ class Tokenizer:
         ids += [sh] + self.encode("assistant") + [eh] + self.encode("\n\n")
         return ids
 
+    def chat_prompt_batch(self, prompts: list, system: Optional[str] = None, style: str = "llama3") -> list:
+        """Batched :meth:`chat_prompt` (one parallel encode of all bodies)."""
+        if style == "raw":
+            return [[self.bos_id] + ids for ids in self.encode_batch(prompts)]
+        sh, eh, eot = self.special("<|start_header_id|>"), self.special("<|end_header_id|>"), self.eot_id
+        head = [self.bos_id]
+        if system:
+            head += [sh] + self.encode("system") + [eh] + self.encode("\n\n" + system) + [eot]
+        head += [sh] + self.encode("user") + [eh]
+        tail = [eot, sh] + self.encode("assistant") + [eh] + self.encode("\n\n")
+        bodies = self.encode_batch(["\n\n" + p for p in prompts])
+        return [head + b + tail for b in bodies]
+
 
 class IncrementalDetokenizer:
     """Streams text for growing id lists without re-decoding emitted text and without

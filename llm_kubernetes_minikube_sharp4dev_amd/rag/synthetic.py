@@ -109,7 +109,10 @@ def iter_documents(n: int, seed: int = 0, min_chars: int = 400, max_chars: int =
         yield f"runbook_{slug}_{i:07d}.md", make_document(i, seed, rng.randint(min_chars, max_chars))
 
 
-def make_queries(n: int, seed: int = 0) -> list[str]:
+def make_queries(n: int, seed: int = 0, unique: bool = True) -> list[str]:
+    """Agent requests in the style of the demo videos (scale / list / logs / status).
+    ``unique`` appends a distinct ticket reference so no two requests of a benchmark
+    share a whole prompt (only the system-prompt prefix is shared)."""
     rng = random.Random(seed + 17)
     templates = [
         "Scala il deployment {d} nel namespace {ns} a {r} repliche",
@@ -122,9 +125,12 @@ def make_queries(n: int, seed: int = 0) -> list[str]:
     out = []
     for _ in range(n):
         t = rng.choice(templates)
-        out.append(t.format(d=rng.choice(["echoserver", "api", "web", "worker"]),
-                            ns=rng.choice(NAMESPACES), r=rng.randint(1, 10),
-                            h=f"{rng.randint(0, 0xfffff):05x}"))
+        q = t.format(d=rng.choice(["echoserver", "api", "web", "worker"]),
+                     ns=rng.choice(NAMESPACES), r=rng.randint(1, 10),
+                     h=f"{rng.randint(0, 0xfffff):05x}")
+        if unique:
+            q += f" (ticket INC-{seed & 0xffffff:06x}-{len(out):04d}, {_sentence(rng, 3, 9).lower()})"
+        out.append(q)
     return out
 
 
