@@ -1,0 +1,150 @@
+"""Model registry of the serving process: maps the model names the .NET clients send
+(``llama3.1:8b``, ``nomic-embed-text`` — ``Minimal_RAG/Program.cs:18,24``) to
+architecture presets, loads them lazily (random-init or a safetensors directory)
+onto this process's GPU, and owns one engine per model."""
+from __future__ import annotations
+
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+
+from ..config import Config
+from ..engine.embed_engine import EmbeddingEngine
+from ..engine.llm_engine import AsyncLLMEngine, LLMEngine
+from ..models import build_decoder, build_encoder
+from ..models.configs import DECODERS, ENCODERS, param_count
+from ..models.tokenizer import load_tokenizer
+from ..utils.logging import get_logger
+
+log = get_logger("serving.models")
+
+
+@dataclass
+class GeneratorHandle:
+    name: str
+    preset: str
+    engine: LLMEngine
+    async_engine: AsyncLLMEngine
+    tokenizer: object
+    chat_style: str
+    loaded_at: float = field(default_factory=time.time)
+    load_s: float = 0.0
+
+
+@dataclass
+class EmbedderHandle:
+    name: str
+    preset: str
+    engine: EmbeddingEngine
+    loaded_at: float = field(default_factory=time.time)
+    load_s: float = 0.0
+
+
+class ModelManager:
+    def __init__(self, cfg: Optional[Config] = None, device: Optional[str] = None,
+                 aliases: Optional[dict] = None, checkpoints: Optional[dict] = None,
+                 engine_overrides: Optional[dict] = None):
+        self.cfg = cfg or Config()
+        self.device = torch.device(device) if device else (
+            torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+        self.aliases = dict(aliases or {})
+        self.checkpoints = dict(checkpoints or {})
+        self.engine_overrides = dict(engine_overrides or {})
+        self.generators: dict[str, GeneratorHandle] = {}
+        self.embedders: dict[str, EmbedderHandle] = {}
+        self.lock = threading.RLock()
+
+    # ------------------------------------------------------------ resolution
+    def resolve(self, name: str) -> tuple[str, str]:
+        """-> (kind, preset) for a client-side model name."""
+        n = self.aliases.get(name, name)
+        base = n.split(":latest")[0]
+        gens, embs = self.cfg.models.generators, self.cfg.models.embedders
+        for cand in (n, base):
+            if cand in gens:
+                return "generate", gens[cand]
+            if cand in embs:
+                return "embed", embs[cand]
+            if cand in DECODERS:
+                return "generate", cand
+            if cand in ENCODERS:
+                return "embed", cand
+        raise KeyError(f"model '{name}' not found")
+
+    def known_models(self) -> list[tuple[str, str, str]]:
+        out = []
+        for n, p in self.cfg.models.generators.items():
+            out.append((n, "generate", self.aliases.get(n, p) if n in self.aliases else p))
+        for n, p in self.cfg.models.embedders.items():
+            out.append((n, "embed", p))
+        return out
+
+    # ------------------------------------------------------------ loading
+    def generator(self, name: str) -> GeneratorHandle:
+        with self.lock:
+            if name in self.generators:
+                return self.generators[name]
+            kind, preset = self.resolve(name)
+            if kind != "generate":
+                raise KeyError(f"model '{name}' does not support generate")
+            for h in self.generators.values():  # same preset under another name
+                if h.preset == preset:
+                    self.generators[name] = h
+                    return h
+            t0 = time.perf_counter()
+            e = self.cfg.engine
+            ck = self.checkpoints.get(name) or self.checkpoints.get(preset)
+            model = build_decoder(preset, device=self.device, seed=e.seed, checkpoint=ck)
+            tok = load_tokenizer(ck)
+            style = "llama3" if model.cfg.arch == "llama" else "raw"
+            kw = dict(block_size=e.kv_block_size, max_model_len=min(e.max_model_len, model.cfg.max_position),
+                      max_num_seqs=e.max_num_seqs, max_num_batched_tokens=e.max_num_batched_tokens,
+                      enable_prefix_caching=e.enable_prefix_caching, use_graphs=e.use_hip_graphs,
+                      gpu_memory_fraction=e.gpu_memory_fraction, seed=e.seed)
+            if self.device.type == "cpu":
+                kw["num_blocks"] = 2048
+            kw.update(self.engine_overrides)
+            eng = LLMEngine(model, tok, **kw)
+            h = GeneratorHandle(name, preset, eng, AsyncLLMEngine(eng), tok, style,
+                                load_s=time.perf_counter() - t0)
+            self.generators[name] = h
+            log.info("loaded generator %s (%s) in %.1fs", name, preset, h.load_s)
+            return h
+
+    def embedder(self, name: str) -> EmbedderHandle:
+        with self.lock:
+            if name in self.embedders:
+                return self.embedders[name]
+            kind, preset = self.resolve(name)
+            if kind != "embed":
+                raise KeyError(f"model '{name}' does not support embeddings")
+            t0 = time.perf_counter()
+            ck = self.checkpoints.get(name) or self.checkpoints.get(preset)
+            enc = build_encoder(preset, device=self.device, seed=self.cfg.engine.seed, checkpoint=ck)
+            h = EmbedderHandle(name, preset, EmbeddingEngine(enc, load_tokenizer(ck), name=name),
+                               load_s=time.perf_counter() - t0)
+            self.embedders[name] = h
+            log.info("loaded embedder %s (%s) in %.1fs", name, preset, h.load_s)
+            return h
+
+    def details(self, name: str) -> dict:
+        kind, preset = self.resolve(name)
+        if kind == "generate":
+            c = DECODERS[preset]
+            n = param_count(c)
+            fam = c.arch
+        else:
+            c = ENCODERS[preset]
+            n = c.num_layers * 12 * c.hidden * c.hidden + c.vocab_size * c.hidden
+            fam = "nomic-bert" if c.arch == "nomic_bert" else "bert"
+        size = f"{n / 1e9:.1f}B" if n >= 1e9 else f"{n / 1e6:.0f}M"
+        return {"format": "safetensors" if (self.checkpoints.get(name) or self.checkpoints.get(preset)) else "random-init",
+                "family": fam, "families": [fam], "parameter_size": size, "quantization_level": "BF16",
+                "params": n, "preset": preset, "kind": kind}
+
+    def shutdown(self):
+        for h in set(self.generators.values()):
+            h.async_engine.shutdown()

@@ -1,0 +1,55 @@
+"""Grammar-constrained decoding: every sampled continuation stays inside the grammar."""
+import json
+import random
+
+import pytest
+
+from llm_kubernetes_minikube_sharp4dev_amd.agent.dotnet_json import RAG_TOOL_CALL, parse_record
+from llm_kubernetes_minikube_sharp4dev_amd.engine.constrained import (JSON_START, JsonGrammar, ToolCallGrammar,
+                                                                      json_feed_text)
+from llm_kubernetes_minikube_sharp4dev_amd.models.tokenizer import builtin_tokenizer
+
+
+@pytest.mark.parametrize("text,ok", [('{"a": [1, -2.5e3, true, null, "x\\u00e8"]}', True), ('{"a" 1}', False),
+                                      ('[01]', False), ('"unterminated', True), ('{"a":1,}', False)])
+def test_json_pda(text, ok):
+    assert (json_feed_text(JSON_START, text) is not None) == ok
+
+
+def _walk(proc, tok, steps, seed):
+    rng = random.Random(seed)
+    ids = []
+    for _ in range(steps):
+        allowed = proc(ids)
+        assert allowed
+        t = rng.choice(allowed)
+        if t in tok.eos_ids:
+            return ids, True
+        ids.append(t)
+    return ids, False
+
+
+def test_tool_call_grammar_random_walks():
+    tok = builtin_tokenizer()
+    g = ToolCallGrammar(tok)
+    done = 0
+    for seed in range(30):
+        ids, fin = _walk(g, tok, 200, seed)
+        text = tok.decode(ids)
+        if fin:
+            done += 1
+            call = parse_record(text, RAG_TOOL_CALL)
+            assert call["action"] in ("list_pods", "get_logs", "scale_deployment", "cluster_context", "final_answer")
+            if call["action"] == "scale_deployment":
+                assert isinstance(call["replicas"], int) and call["name"] and call["namespace"]
+    assert done >= 25
+
+
+def test_json_grammar_random_walk_prefix_valid():
+    tok = builtin_tokenizer()
+    g = JsonGrammar(tok)
+    for seed in range(3):
+        ids, fin = _walk(g, tok, 40, seed)
+        assert json_feed_text(JSON_START, tok.decode(ids)) is not None
+        if fin:
+            json.loads(tok.decode(ids))
