@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""Per-kernel microbenchmarks on one MI355X vs. their rooflines.
+
+Each case is timed with HIP events (median over iterations, after warm-up) on
+random data, and reported as achieved GB/s (bandwidth-bound kernels) or TFLOP/s
+(MFMA-bound kernels).  Output: one JSON line per case (+ a markdown table with
+``--md``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from llm_kubernetes_minikube_sharp4dev_amd import ops  # noqa: E402
+
+DEV = "cuda"
+
+
+def timeit(fn, iters=20, warmup=5):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) * 1e-3)
+    return statistics.median(ts)
+
+
+def paged_setup(B, ctx, Hkv, D, BS=16):
+    nblk = (ctx + BS - 1) // BS
+    NB = B * nblk + 1
+    kc = torch.randn(NB, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.randperm(NB - 1, device=DEV)[: B * nblk].int().view(B, nblk)
+    return kc, vc, bt
+
+
+def case_decode(B=64, ctx=1000, Hq=32, Hkv=8, D=128):
+    kc, vc, bt = paged_setup(B, ctx, Hkv, D)
+    q = torch.randn(B, Hq, D, device=DEV, dtype=torch.bfloat16)
+    cl = torch.full((B,), ctx, dtype=torch.int32, device=DEV)
+    bt_full = torch.zeros(B, 8192 // 16, dtype=torch.int32, device=DEV)
+    bt_full[:, : bt.shape[1]] = bt
+    t = timeit(lambda: ops.paged_decode(q, kc, vc, bt_full, cl, 1 / math.sqrt(D)))
+    byts = B * ctx * Hkv * D * 2 * 2
+    return {"case": f"paged_decode B{B} ctx{ctx} Hq{Hq} Hkv{Hkv} D{D}", "us": t * 1e6, "GB/s": byts / t / 1e9}
+
+
+def case_prefill(B=32, L=1024, Hq=32, Hkv=8, D=128):
+    kc, vc, bt = paged_setup(B, L, Hkv, D)
+    T = B * L
+    q = torch.randn(T, Hq * D, device=DEV, dtype=torch.bfloat16)
+    cu = torch.arange(0, T + 1, L, dtype=torch.int32, device=DEV)
+    cl = torch.full((B,), L, dtype=torch.int32, device=DEV)
+    ts, tq = ops.prefill_tiles([L] * B, [L] * B, Hq // Hkv, True)
+    tiles = (torch.from_numpy(ts).to(DEV), torch.from_numpy(tq).to(DEV))
+    t = timeit(lambda: ops.flash_prefill(q, kc, vc, cu, Hq, Hkv, D, 1 / math.sqrt(D), True, block_tables=bt,
+                                         ctx_lens=cl, tiles=tiles))
+    flops = B * 4 * (L * L / 2) * D * Hq
+    return {"case": f"flash_prefill causal B{B} L{L} Hq{Hq} Hkv{Hkv} D{D}", "us": t * 1e6, "TFLOP/s": flops / t / 1e12}
+
+
+def case_encoder_attn(B=1600, L=80, H=12, D=64):
+    T = B * L
+    qkv = torch.randn(T, 3 * H * D, device=DEV, dtype=torch.bfloat16)
+    cu = torch.arange(0, T + 1, L, dtype=torch.int32, device=DEV)
+    ts, tq = ops.prefill_tiles([L] * B, [L] * B, 1, False)
+    tiles = (torch.from_numpy(ts).to(DEV), torch.from_numpy(tq).to(DEV))
+    t = timeit(lambda: ops.flash_prefill(qkv[:, : H * D], qkv[:, H * D: 2 * H * D], qkv[:, 2 * H * D:], cu, H, H, D,
+                                         1 / math.sqrt(D), False, tiles=tiles))
+    flops = B * 4 * L * L * D * H
+    return {"case": f"encoder_attn B{B} L{L} H{H} D{D}", "us": t * 1e6, "TFLOP/s": flops / t / 1e12}
+
+
+def case_rmsnorm(T=8192, H=4096):
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn_like(x)
+    w = torch.randn(H, device=DEV, dtype=torch.bfloat16)
+    t = timeit(lambda: ops.rmsnorm(x, w, 1e-5, residual=r))
+    return {"case": f"rmsnorm+res T{T} H{H}", "us": t * 1e6, "GB/s": T * H * 2 * 4 / t / 1e9}
+
+
+def case_silu(T=8192, I=14336):
+    x = torch.randn(T, 2 * I, device=DEV, dtype=torch.bfloat16)
+    t = timeit(lambda: ops.silu_mul(x))
+    return {"case": f"silu_mul T{T} I{I}", "us": t * 1e6, "GB/s": T * I * 2 * 3 / t / 1e9}
+
+
+def case_knn(N=485_000, D=768, nq=64):
+    c = torch.randn(N, D, device=DEV, dtype=torch.bfloat16)
+    q = torch.randn(nq, D, device=DEV, dtype=torch.bfloat16)
+    cn, qn = ops.row_norms(c), ops.row_norms(q)
+    t = timeit(lambda: ops.knn_topk(c, cn, q, qn, 6))
+    return {"case": f"knn_topk N{N} D{D} nq{nq} k6", "us": t * 1e6, "GB/s": N * D * 2 / t / 1e9}
+
+
+def case_gemm(M, N, K):
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+    t = timeit(lambda: torch.nn.functional.linear(a, b))
+    return {"case": f"hipBLASLt linear M{M} N{N} K{K}", "us": t * 1e6, "TFLOP/s": 2 * M * N * K / t / 1e12,
+            "GB/s": (M * K + N * K + M * N) * 2 / t / 1e9}
+
+
+CASES = {
+    "decode": lambda: [case_decode(), case_decode(B=128, ctx=1000), case_decode(B=8, ctx=3000)],
+    "prefill": lambda: [case_prefill(), case_prefill(B=8, L=4096)],
+    "encoder": lambda: [case_encoder_attn()],
+    "norm": lambda: [case_rmsnorm(), case_silu()],
+    "knn": lambda: [case_knn()],
+    "gemm": lambda: [case_gemm(64, 6144, 4096), case_gemm(64, 28672, 4096), case_gemm(64, 4096, 14336),
+                     case_gemm(32768, 6144, 4096), case_gemm(32768, 28672, 4096), case_gemm(32768, 4096, 14336)],
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cases", nargs="*", default=list(CASES))
+    ap.add_argument("--md", default=None)
+    a = ap.parse_args()
+    rows = []
+    for c in a.cases:
+        for r in CASES[c]():
+            r = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in r.items()}
+            print(json.dumps(r), flush=True)
+            rows.append(r)
+    if a.md:
+        with open(a.md, "w") as f:
+            f.write("| case | us | GB/s | TFLOP/s |\n|---|---|---|---|\n")
+            for r in rows:
+                f.write(f"| {r['case']} | {r['us']} | {r.get('GB/s', '')} | {r.get('TFLOP/s', '')} |\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -19,138 +19,201 @@
 
 namespace {
 
-constexpr int kSplit = 512;  // keys per workgroup
+constexpr int kMaxSplit = 2048;  // max keys per workgroup (LDS block-table slice)
+typedef short4_t __attribute__((address_space(3))) * lds_s4_ptr;
 
+// v3 (streaming): workgroup = (split, kv_head, seq), 4 waves; each wave walks 32-key
+// chunks (w, w+4, ...) of the split with its own online softmax, so there is no
+// workgroup barrier inside the key loop and the next chunk's K/V loads are always
+// in flight while the current chunk is computed.
+//   QK^T: 2 x v_mfma_f32_16x16x32_bf16 tiles, A = K rows straight from the paged
+//         cache, B = Q^T (G query heads of the GQA group padded to 16 columns).
+//   PV:   v_mfma_f32_16x16x32_bf16, A = P taken from the S^T accumulators (k order
+//         permuted to match), B = V^T via ds_read_b64_tr_b16 from a wave-private,
+//         XOR-swizzled LDS image of the chunk.
+// The 4 waves' (m, l, O) are merged through LDS at the end; splits > 1 emit
+// partials for lk_decode_reduce (flash-decoding).
 template <int D, int G>
-__global__ __launch_bounds__(256) void paged_decode_kernel(
+__global__ __launch_bounds__(256, 2) void paged_decode_kernel(
     const bf16_t* __restrict__ q, long qs, const bf16_t* __restrict__ kc,
     const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ctx_lens, bf16_t* __restrict__ out, long os,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int BS, int max_splits,
-    float scale) {
-  constexpr int P = kSplit;
-  constexpr int KK = D / 32;   // MFMA k-steps over the head dim
-  constexpr int LPR = D / 8;   // lanes per V row in the PV phase
-  constexpr int RPW = 64 / LPR;
-  const int s = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+    int split, float scale_log2) {
+  constexpr int KK = D / 32;     // QK k-steps (16x16x32)
+  constexpr int ND = D / 16;     // PV output tiles of 16 d
+  constexpr int CPR = D / 8;     // 16-B chunks per V row
+  constexpr int NVL = 32 * CPR / 64;  // V 16-B loads per lane per chunk
+  constexpr int RPL = 64 / CPR;  // V rows per load instruction
+  // grid (B*Hkv, max_splits): the flattened (seq, kv head) index varies fastest so the
+  // active split-0 workgroups are dealt round-robin over all 8 XCDs (split-fastest
+  // order put every active workgroup of a short-context batch on ONE XCD).
+  const int s = blockIdx.y, kvh = blockIdx.x % Hkv, b = blockIdx.x / Hkv;
   const int ctx = ctx_lens[b];
-  const int k_begin = s * P;
+  const int k_begin = s * split;
   if (k_begin >= ctx) return;  // uniform for the whole workgroup
-  const int nkeys = min(P, ctx - k_begin);
-  const int nsplit = min((ctx + P - 1) / P, max_splits);
+  const int nkeys = min(split, ctx - k_begin);
+  const int nsplit = min((ctx + split - 1) / split, max_splits);
   const int Hq = Hkv * G;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r16 = lane & 15, h4 = lane >> 4;
 
-  __shared__ float logits[G][P];
-  __shared__ float red[4][G][D];
-  __shared__ float stat[2][G];
-  __shared__ int blk[P / 16];
+  __shared__ int blk[kMaxSplit / 16];
+  __shared__ __attribute__((aligned(16))) bf16_t vlds[4][32 * D];
+  __shared__ float mrg_ml[4][2][16];
+  __shared__ float mrg_o[4][G][D];
 
   const int nblk = (nkeys + BS - 1) / BS;
   for (int i = threadIdx.x; i < nblk; i += 256)
     blk[i] = block_tables[(long)b * bt_stride + k_begin / BS + i];
+  __syncthreads();
 
-  // Q^T fragments (B operand): lane holds Q[q = lane&15][32kk + 8(lane>>4) + j]
-  const int qi = lane & 15, hq = lane >> 4;
+  auto row_ptr = [&](const bf16_t* cache, int rel) {
+    rel = min(rel, nkeys - 1);
+    const int abs_k = k_begin + rel;
+    return cache + (((long)blk[rel / BS] * Hkv + kvh) * BS + (abs_k % BS)) * D;
+  };
+
+  // Q^T fragments (B of QK): lane holds Q[q = r16][32kk + 8*h4 + j]
   short8 qf[KK];
 #pragma unroll
-  for (int kk = 0; kk < KK; ++kk) {
-    if (qi < G)
-      qf[kk] = *reinterpret_cast<const short8*>(q + (long)b * qs + (long)(kvh * G + qi) * D +
-                                                32 * kk + 8 * hq);
-    else
-      qf[kk] = short8{0, 0, 0, 0, 0, 0, 0, 0};
-  }
-  __syncthreads();
+  for (int kk = 0; kk < KK; ++kk)
+    qf[kk] = r16 < G ? *reinterpret_cast<const short8*>(q + (long)b * qs + (long)(kvh * G + r16) * D +
+                                                        32 * kk + 8 * h4)
+                     : short8{0, 0, 0, 0, 0, 0, 0, 0};
 
-  // ---- QK^T over 16-key tiles, round-robin over the 4 waves
-  const int ntile = (nkeys + 15) >> 4;
-  for (int t = w; t < ntile; t += 4) {
-    const int rel = min(16 * t + qi, nkeys - 1);  // clamp: rows past the end are masked below
-    const int abs_k = k_begin + rel;
-    const bf16_t* kp = kc + (((long)blk[rel / BS] * Hkv + kvh) * BS + (abs_k % BS)) * D + 8 * hq;
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int nch = (nkeys + 31) >> 5;
+  short8 kr[2][KK], vr[NVL];
+  auto load_chunk = [&](int c, short8 (&kd)[2][KK], short8 (&vd)[NVL]) {
+    const int base = 32 * c;
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      const short8 a = *reinterpret_cast<const short8*>(kp + 32 * kk);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[kk], acc, 0, 0, 0);
+    for (int t = 0; t < 2; ++t) {
+      const bf16_t* kp = row_ptr(kc, base + 16 * t + r16) + 8 * h4;
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) kd[t][kk] = *reinterpret_cast<const short8*>(kp + 32 * kk);
     }
-    if (qi < G) {
+#pragma unroll
+    for (int i = 0; i < NVL; ++i)
+      vd[i] = *reinterpret_cast<const short8*>(row_ptr(vc, base + i * RPL + lane / CPR) + (lane % CPR) * 8);
+  };
+
+  floatx4 o[ND];
+#pragma unroll
+  for (int n = 0; n < ND; ++n) o[n] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  bf16_t* vw = vlds[w];
+
+  int c = w;
+  if (c < nch) load_chunk(c, kr, vr);
+  for (; c < nch; c += 4) {
+    // stage this chunk's V into the wave-private LDS image (row-major, 16-B chunk
+    // index XOR ((row & 7) << 1) so the transposed reads below are conflict-free)
+#pragma unroll
+    for (int i = 0; i < NVL; ++i) {
+      const int row = i * RPL + lane / CPR, ch = lane % CPR;
+      *reinterpret_cast<short8*>(vw + row * D + ((ch ^ ((row & 7) << 1)) & (CPR - 1)) * 8) = vr[i];
+    }
+    short8 kcur[2][KK];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) kcur[t][kk] = kr[t][kk];
+    if (c + 4 < nch) load_chunk(c + 4, kr, vr);  // next chunk in flight under the math
+
+    // S^T tiles: lane (q = r16) holds keys 16t + 4*h4 + i
+    floatx4 sc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      sc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+        sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kcur[t][kk], qf[kk], sc[t], 0, 0, 0);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int kr = 16 * t + 4 * hq + i;
-        logits[qi][kr] = kr < nkeys ? acc[i] * scale : -INFINITY;
+        const int rel = 32 * c + 16 * t + 4 * h4 + i;
+        const float x = rel < nkeys ? sc[t][i] * scale_log2 : -INFINITY;
+        sc[t][i] = x;
+        mx = fmaxf(mx, x);
       }
-    }
-  }
-  __syncthreads();
-
-  // ---- softmax statistics per query row
-  for (int g = w; g < G; g += 4) {
-    float m = -INFINITY;
-    for (int j = lane; j < nkeys; j += 64) m = fmaxf(m, logits[g][j]);
-    m = wave_max(m);
-    float sum = 0.f;
-    for (int j = lane; j < nkeys; j += 64) {
-      const float e = __expf(logits[g][j] - m);
-      logits[g][j] = e;
-      sum += e;
-    }
-    sum = wave_sum(sum);
-    if (lane == 0) {
-      stat[0][g] = m;
-      stat[1][g] = sum;
-    }
-  }
-  __syncthreads();
-
-  // ---- P.V : lane owns d = (lane % LPR)*8 .. +7 of key row (lane / LPR)
-  float acc[G][8];
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);  // finite: every chunk has >= 1 valid key
+    const float alpha = exp2f(m_run - m_new);
+    float rs = 0.f;
+    short8 pa;
 #pragma unroll
-  for (int g = 0; g < G; ++g)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
-  const int dv = (lane % LPR) * 8;
-  for (int kb = w * RPW; kb < nkeys; kb += 4 * RPW) {
-    const int rel = kb + lane / LPR;
-    if (rel < nkeys) {
-      const int abs_k = k_begin + rel;
-      float v[8];
-      load8(vc + (((long)blk[rel / BS] * Hkv + kvh) * BS + (abs_k % BS)) * D + dv, v);
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const float p = logits[g][rel];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[g][j] += p * v[j];
+      for (int i = 0; i < 4; ++i) {
+        const float e = exp2f(sc[t][i] - m_new);
+        rs += e;
+        pa[4 * t + i] = (short)f2bf(e);
       }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l_run = l_run * alpha + rs;
+    m_run = m_new;
+    // O rows are q = 4*h4 + reg: fetch alpha of those query rows (lanes 0..15 hold q = lane)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const float a = __shfl(alpha, 4 * h4 + rr, 64);
+#pragma unroll
+      for (int n = 0; n < ND; ++n) o[n][rr] *= a;
+    }
+    // PV: B = V^T fragment of k-step = keys {4*h4 + j} u {16 + 4*h4 + j}, column 16n + r16
+    const int qq = r16 >> 2, pp = r16 & 3;
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+      const int col = 16 * n + 4 * pp;
+      const int r0 = 4 * h4 + qq, r1 = 16 + 4 * h4 + qq;
+      const bf16_t* a0 = vw + r0 * D + (((col >> 3) ^ ((r0 & 7) << 1)) & (CPR - 1)) * 8 + (col & 7);
+      const bf16_t* a1 = vw + r1 * D + (((col >> 3) ^ ((r1 & 7) << 1)) & (CPR - 1)) * 8 + (col & 7);
+      const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(a0));
+      const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(a1));
+      const short8 vb = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[n], 0, 0, 0);
     }
   }
+
+  // ---- merge the 4 waves: (m, l) per query row (lanes 0..15 hold q = lane), O rows
+  if (lane < 16) {
+    mrg_ml[w][0][lane] = m_run;
+    mrg_ml[w][1][lane] = l_run;
+  }
 #pragma unroll
-  for (int o = LPR; o < 64; o <<= 1)
+  for (int rr = 0; rr < 4; ++rr) {
+    const int qrow = 4 * h4 + rr;
+    if (qrow < G) {
 #pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[g][j] += __shfl_xor(acc[g][j], o, 64);
-  if (lane < LPR) {
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) red[w][g][dv + j] = acc[g][j];
+      for (int n = 0; n < ND; ++n) mrg_o[w][qrow][16 * n + r16] = o[n][rr];
+    }
   }
   __syncthreads();
-
   for (int i = threadIdx.x; i < G * D; i += 256) {
     const int g = i / D, d = i - g * D;
-    const float o = red[0][g][d] + red[1][g][d] + red[2][g][d] + red[3][g][d];
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, mrg_ml[ww][0][g]);
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const float f = mrg_ml[ww][0][g] == -INFINITY ? 0.f : exp2f(mrg_ml[ww][0][g] - M);
+      L += f * mrg_ml[ww][1][g];
+      O += f * mrg_o[ww][g][d];
+    }
     const int qh = kvh * G + g;
     if (nsplit == 1) {
-      out[(long)b * os + (long)qh * D + d] = f2bf(o / stat[1][g]);
+      out[(long)b * os + (long)qh * D + d] = f2bf(O / L);
     } else {
       const long pi = ((long)b * Hq + qh) * max_splits + s;
-      part_o[pi * D + d] = o;
+      part_o[pi * D + d] = O;
       if (d == 0) {
-        part_ml[pi * 2] = stat[0][g];
-        part_ml[pi * 2 + 1] = stat[1][g];
+        part_ml[pi * 2] = M;  // log2 domain
+        part_ml[pi * 2 + 1] = L;
       }
     }
   }
@@ -162,10 +225,10 @@ __global__ __launch_bounds__(D) void decode_reduce_kernel(const float* __restric
                                                           const float* __restrict__ part_ml,
                                                           const int* __restrict__ ctx_lens,
                                                           bf16_t* __restrict__ out, long os,
-                                                          int Hq, int max_splits) {
+                                                          int Hq, int max_splits, int split) {
   const int qh = blockIdx.x, b = blockIdx.y;
   const int ctx = ctx_lens[b];
-  const int nsplit = min((ctx + kSplit - 1) / kSplit, max_splits);
+  const int nsplit = min((ctx + split - 1) / split, max_splits);
   if (nsplit <= 1) return;  // written directly by the main kernel
   const long base = ((long)b * Hq + qh) * max_splits;
   float M = -INFINITY;
@@ -173,7 +236,7 @@ __global__ __launch_bounds__(D) void decode_reduce_kernel(const float* __restric
   float den = 0.f, num = 0.f;
   const int d = threadIdx.x;
   for (int s = 0; s < nsplit; ++s) {
-    const float f = __expf(part_ml[(base + s) * 2] - M);
+    const float f = exp2f(part_ml[(base + s) * 2] - M);
     den += f * part_ml[(base + s) * 2 + 1];
     num += f * part_o[(base + s) * D + d];
   }
@@ -182,27 +245,37 @@ __global__ __launch_bounds__(D) void decode_reduce_kernel(const float* __restric
 
 }  // namespace
 
-int lk_decode_splits(int max_context) { return (max_context + kSplit - 1) / kSplit; }
+// keys per workgroup: enough workgroups to fill 256 CUs at small batch, long splits
+// (few partials) at large batch; static per (B, Hkv) so hipGraph launches are fixed.
+int lk_decode_split_size(int B, int Hkv) {
+  const int bh = B * Hkv;
+  if (bh >= 512) return 1024;
+  if (bh >= 128) return 512;
+  if (bh >= 32) return 256;
+  return 128;
+}
+
+int lk_decode_splits(int max_context, int split) { return (max_context + split - 1) / split; }
 
 int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc,
                     const int* block_tables, int bt_stride, const int* ctx_lens, bf16_t* out,
                     long os, float* part_o, float* part_ml, int B, int Hq, int Hkv, int D, int BS,
-                    int max_splits, float scale, hipStream_t st) {
+                    int max_splits, int split, float scale, hipStream_t st) {
   if (B == 0) return 0;
-  if (Hq % Hkv || BS % 16 || kSplit % BS) return -1;
+  if (Hq % Hkv || BS % 16 || split % 32 || split > kMaxSplit || split % BS) return -1;
   const int G = Hq / Hkv;
-  dim3 grid(max_splits, Hkv, B);
+  const float scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid(B * Hkv, max_splits);
 #define LAUNCH(DD, GG)                                                                        \
   paged_decode_kernel<DD, GG><<<grid, 256, 0, st>>>(q, qs, kc, vc, block_tables, bt_stride,   \
                                                     ctx_lens, out, os, part_o, part_ml, Hkv, \
-                                                    BS, max_splits, scale)
+                                                    BS, max_splits, split, scale_log2)
 #define BY_G(DD)                          \
   switch (G) {                            \
     case 1: LAUNCH(DD, 1); break;         \
     case 2: LAUNCH(DD, 2); break;         \
     case 4: LAUNCH(DD, 4); break;         \
     case 8: LAUNCH(DD, 8); break;         \
-    case 16: LAUNCH(DD, 16); break;       \
     default: return -2;                   \
   }
   if (D == 128) { BY_G(128) }
@@ -213,10 +286,10 @@ int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc
   if (max_splits > 1) {
     if (D == 128)
       decode_reduce_kernel<128><<<dim3(Hq, B), 128, 0, st>>>(part_o, part_ml, ctx_lens, out, os, Hq,
-                                                             max_splits);
+                                                             max_splits, split);
     else
       decode_reduce_kernel<64><<<dim3(Hq, B), 64, 0, st>>>(part_o, part_ml, ctx_lens, out, os, Hq,
-                                                           max_splits);
+                                                           max_splits, split);
   }
   return 0;
 }

@@ -152,11 +152,12 @@ void kv_write(const at::Tensor& k, const at::Tensor& v, at::Tensor& k_cache, at:
   CHECK_RC(rc, "kv_write");
 }
 
-int64_t decode_splits(int64_t max_context) { return lk_decode_splits((int)max_context); }
+int64_t decode_splits(int64_t max_context, int64_t split) { return lk_decode_splits((int)max_context, (int)split); }
+int64_t decode_split_size(int64_t B, int64_t Hkv) { return lk_decode_split_size((int)B, (int)Hkv); }
 
 at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                         const at::Tensor& block_tables, const at::Tensor& ctx_lens, int64_t max_splits,
-                        double scale, const c10::optional<at::Tensor>& part_o,
+                        int64_t split, double scale, const c10::optional<at::Tensor>& part_o,
                         const c10::optional<at::Tensor>& part_ml, const c10::optional<at::Tensor>& out_) {
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
   CHECK_I32(block_tables); CHECK_I32(ctx_lens); CHECK_CONTIG(ctx_lens);
@@ -167,7 +168,8 @@ at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at
   TORCH_CHECK(k_cache.size(3) == D, "head dim mismatch");
   TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && block_tables.stride(1) == 1, "block_tables");
   TORCH_CHECK(ctx_lens.numel() >= B, "ctx_lens");
-  TORCH_CHECK(max_splits >= 1 && (long)max_splits * 512 <= (long)block_tables.size(1) * BS + 511, "max_splits exceeds block table capacity");
+  TORCH_CHECK(split >= 32 && split <= 2048 && split % 32 == 0 && split % BS == 0, "decode split must be a multiple of 32 and of the block size, <= 2048");
+  TORCH_CHECK(max_splits >= 1 && (long)(max_splits - 1) * split < (long)block_tables.size(1) * BS, "max_splits exceeds block table capacity");
   check_rows16(q, "q");
   at::Tensor out = out_ ? *out_ : at::empty({B, Hq, D}, q.options());
   TORCH_CHECK(out.size(0) == B && out.size(1) == Hq && out.size(2) == D && out.stride(2) == 1 && out.stride(1) == D, "out layout");
@@ -181,7 +183,7 @@ at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at
   int rc = lk_paged_decode(bp(q), q.stride(0), bp(k_cache), bp(v_cache), ip(block_tables), block_tables.stride(0),
                            ip(ctx_lens), bp(out), out.stride(0), max_splits > 1 ? po.data_ptr<float>() : nullptr,
                            max_splits > 1 ? pm.data_ptr<float>() : nullptr, B, Hq, Hkv, D, BS, (int)max_splits,
-                           (float)scale, cur_stream());
+                           (int)split, (float)scale, cur_stream());
   CHECK_RC(rc, "paged_decode");
   return out;
 }
@@ -323,7 +325,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_kv_", &rope_kv_);
   m.def("kv_write", &kv_write);
   m.def("decode_splits", &decode_splits);
-  m.def("paged_decode", &paged_decode, "", py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("max_splits"), py::arg("scale"), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("out") = py::none());
+  m.def("decode_split_size", &decode_split_size);
+  m.def("paged_decode", &paged_decode, "", py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("max_splits"), py::arg("split"), py::arg("scale"), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("out") = py::none());
   m.def("prefill_rows_per_tile", &prefill_rows_per_tile);
   m.def("flash_prefill", &flash_prefill, "", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("block_tables"), py::arg("cu_q"), py::arg("ctx_lens"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("out") = py::none());
   m.def("knn_topk", &knn_topk);

@@ -30,11 +30,12 @@ int lk_kv_write(const bf16_t* k, long ks, const bf16_t* v, long vs, bf16_t* kc, 
                 const int* slots, long T, int Hkv, int D, int BS, hipStream_t st);
 
 // attn_decode.hip
-int lk_decode_splits(int max_context);
+int lk_decode_split_size(int B, int Hkv);
+int lk_decode_splits(int max_context, int split);
 int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc,
                     const int* block_tables, int bt_stride, const int* ctx_lens, bf16_t* out,
                     long os, float* part_o, float* part_ml, int B, int Hq, int Hkv, int D, int BS,
-                    int max_splits, float scale, hipStream_t st);
+                    int max_splits, int split, float scale, hipStream_t st);
 
 // attn_prefill.hip
 int lk_prefill_rows_per_tile(int G);

@@ -67,6 +67,7 @@ class LLMEngine:
         return self.scheduler.has_work()
 
     # ------------------------------------------------------------------ step
+    @torch.inference_mode()
     def step(self) -> list:
         """One scheduler iteration.  Returns the sequences that produced a token."""
         with self.lock:

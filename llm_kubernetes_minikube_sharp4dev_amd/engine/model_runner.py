@@ -36,7 +36,6 @@ class ModelRunner:
         self.bs = block_size
         self.max_model_len = max_model_len
         self.max_blocks = (max_model_len + block_size - 1) // block_size
-        self.max_splits = ops.decode_splits(self.max_blocks * block_size)
         self.max_num_seqs = max_num_seqs
         cfg = model.cfg
         self.L = cfg.num_layers
@@ -68,13 +67,19 @@ class ModelRunner:
         self.vocab = None
 
     # ----------------------------------------------------------- workspaces
+    def decode_split(self, B: int):
+        split = max(ops.decode_split_size(B, self.hkv), self.bs)
+        return split, ops.decode_splits(self.max_blocks * self.bs, split)
+
     def _decode_ws(self, B: int):
-        need = max(B, self.graph_sizes[-1] if self.graph_sizes else B)
-        if self._ws is None or self._ws[0].shape[0] < need:
-            po = torch.empty((need, self.hq, self.max_splits, self.D), dtype=torch.float32, device=self.device)
-            pm = torch.empty((need, self.hq, self.max_splits, 2), dtype=torch.float32, device=self.device)
-            self._ws = (po, pm)
-        return self._ws[0][:B], self._ws[1][:B]
+        split, ms = self.decode_split(B)
+        n = B * self.hq * ms
+        if self._ws is None or self._ws[0].numel() < n * self.D:
+            self._ws = (torch.empty(max(n, 1) * self.D, dtype=torch.float32, device=self.device),
+                        torch.empty(max(n, 1) * 2, dtype=torch.float32, device=self.device))
+        po = self._ws[0][: n * self.D].view(B, self.hq, ms, self.D)
+        pm = self._ws[1][: n * 2].view(B, self.hq, ms, 2)
+        return po, pm
 
     def _slots(self, table, start, n):
         pos = np.arange(start, start + n, dtype=np.int64)
@@ -135,9 +140,8 @@ class ModelRunner:
             width = max(len(t) for t in dt)
             meta.block_tables_d = torch.from_numpy(self._bt(dt, width)).to(dev, non_blocking=True)
             meta.ctx_lens_d = torch.tensor([s.length for s, _, _ in dec], dtype=torch.int32).to(dev, non_blocking=True)
-            meta.max_splits = ops.decode_splits(width * self.bs)
-            if dev.type == "cuda":
-                meta.part_o, meta.part_ml = None, None  # sized by the op for this width
+            meta.decode_split = max(ops.decode_split_size(len(dec), self.hkv), self.bs)
+            meta.max_splits = ops.decode_splits(width * self.bs, meta.decode_split)
         meta.logits_idx = torch.tensor([row for _, row in rows], dtype=torch.long).to(dev, non_blocking=True)
         ids_t = torch.tensor(ids, dtype=torch.int32).to(dev, non_blocking=True)
         assert ids_t.shape[0] == T
@@ -172,9 +176,10 @@ class ModelRunner:
             "bt": torch.zeros((B, self.max_blocks), dtype=torch.int32, device=dev),
             "ctx": torch.ones(B, dtype=torch.int32, device=dev),
         }
+        split, ms = self.decode_split(B)
         st["meta"] = AttnMeta(positions=st["pos"], slots=st["slots"], num_decode=B,
-                              block_tables_d=st["bt"], ctx_lens_d=st["ctx"], max_splits=self.max_splits,
-                              part_o=po, part_ml=pm)
+                              block_tables_d=st["bt"], ctx_lens_d=st["ctx"], max_splits=ms,
+                              decode_split=split, part_o=po, part_ml=pm)
         return st
 
     def capture(self, B):

@@ -33,7 +33,8 @@ class AttnMeta:
     # decode part
     block_tables_d: Optional[torch.Tensor] = None
     ctx_lens_d: Optional[torch.Tensor] = None
-    max_splits: int = 1
+    max_splits: Optional[int] = None
+    decode_split: Optional[int] = None
     part_o: Optional[torch.Tensor] = None
     part_ml: Optional[torch.Tensor] = None
     # rows whose hidden state feeds the LM head (last token of each prefill + decode rows)
@@ -69,5 +70,5 @@ def paged_attention(qkv: torch.Tensor, k_cache, v_cache, meta: AttnMeta, Hq: int
         q = qkv[Tp:Tp + Bd, : Hq * D].view(Bd, Hq, D)
         o = out[Tp:Tp + Bd].view(Bd, Hq, D)
         ops.paged_decode(q, k_cache, v_cache, meta.block_tables_d, meta.ctx_lens_d, scale,
-                         meta.max_splits, meta.part_o, meta.part_ml, out=o)
+                         meta.max_splits, meta.part_o, meta.part_ml, out=o, split=meta.decode_split)
     return out

@@ -22,7 +22,7 @@ __all__ = [
 ]
 
 rope_cos_sin = ref.rope_cos_sin
-DECODE_SPLIT = 512  # keys per decode workgroup (csrc/attn_decode.hip kSplit)
+DECODE_MAX_SPLIT = 2048  # csrc/attn_decode.hip kMaxSplit
 
 
 def rmsnorm(x, w, eps: float, residual: Optional[torch.Tensor] = None, out=None):
@@ -90,16 +90,29 @@ def kv_write(k, v, k_cache, v_cache, slots):
     return ref.kv_write(k, v, k_cache, v_cache, slots)
 
 
-def decode_splits(max_context: int) -> int:
-    return max(1, (int(max_context) + DECODE_SPLIT - 1) // DECODE_SPLIT)
+def decode_split_size(B: int, Hkv: int) -> int:
+    """Keys per decode workgroup (mirrors lk_decode_split_size): small batches split the
+    context finer so 256 CUs stay busy; static per (B, Hkv) for hipGraph capture."""
+    bh = B * Hkv
+    return 1024 if bh >= 512 else 512 if bh >= 128 else 256 if bh >= 32 else 128
 
 
-def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_splits: int,
-                 part_o=None, part_ml=None, out=None):
-    """q [B, Hq, D] -> [B, Hq, D].  ``max_splits`` = decode_splits(max context the
-    block tables can hold) — static, so the launch is hipGraph-capturable."""
+def decode_splits(max_context: int, split: int) -> int:
+    return max(1, (int(max_context) + split - 1) // split)
+
+
+def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_splits: Optional[int] = None,
+                 part_o=None, part_ml=None, out=None, split: Optional[int] = None):
+    """q [B, Hq, D] -> [B, Hq, D].  ``split`` keys per workgroup (default from
+    :func:`decode_split_size`), ``max_splits`` = splits covering the block-table width —
+    both static, so the launch is hipGraph-capturable."""
     if use_hip(q):
-        return lib().paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, max_splits, scale,
+        BS = k_cache.shape[2]
+        if split is None:
+            split = max(decode_split_size(q.shape[0], k_cache.shape[1]), BS)
+        if max_splits is None:
+            max_splits = decode_splits(block_tables.shape[1] * BS, split)
+        return lib().paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, max_splits, split, scale,
                                   part_o, part_ml, out)
     y = ref.paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
     if out is not None:

@@ -146,5 +146,5 @@ class ModelManager:
                 "params": n, "preset": preset, "kind": kind}
 
     def shutdown(self):
-        for h in set(self.generators.values()):
+        for h in {id(h): h for h in self.generators.values()}.values():
             h.async_engine.shutdown()

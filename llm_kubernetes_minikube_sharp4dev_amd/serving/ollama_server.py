@@ -21,6 +21,8 @@ Routes (Ollama REST API):
 """
 from __future__ import annotations
 
+from fastapi import Request  # module level: FastAPI resolves string annotations here
+
 import asyncio
 import json
 import time

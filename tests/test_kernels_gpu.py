@@ -122,11 +122,12 @@ def test_paged_decode(hip, G, D):
     kc, vc, bt = _paged_setup(B, ctx, Hkv, D, BS)
     q = torch.randn(B, Hq, D, device=DEV, dtype=torch.bfloat16)
     cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
-    max_splits = ops.decode_splits(bt.shape[1] * BS)
     scale = 1 / math.sqrt(D)
-    y = hip.paged_decode(q, kc, vc, bt, cl, max_splits, scale, None, None, None)
     y_ref = ref.paged_decode(q, kc, vc, bt, cl, scale)
-    _close(y, y_ref, 0.02, 0.0, "paged decode")
+    for split in (128, 256, 2048):  # many partials / few partials / single pass
+        max_splits = ops.decode_splits(bt.shape[1] * BS, split)
+        y = hip.paged_decode(q, kc, vc, bt, cl, max_splits, split, scale, None, None, None)
+        _close(y, y_ref, 0.02, 0.0, f"paged decode split={split}")
 
 
 @pytest.mark.parametrize("G", [1, 2, 4, 8])
