@@ -1,9 +1,119 @@
-"""Placeholder until the C++ runtime is built (see native/__init__)."""
+"""Native (C++) runtime: build + load ``_runtime`` (csrc/runtime/*.cpp, pybind11).
+
+:class:`NativeBlockAllocator` is a drop-in for ``engine.block_manager.BlockAllocator``
+(the scheduler's per-step hot path); it raises the same ``NoFreeBlocks`` type.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+SRC = ROOT / "csrc" / "runtime"
+_mod = None
+
+
+def so_path() -> Path:
+    return Path(__file__).resolve().parent / f"_runtime{sysconfig.get_config_var('EXT_SUFFIX') or '.so'}"
+
+
+def build(verbose: bool = False) -> Path:
+    import pybind11
+
+    out = so_path()
+    srcs = sorted(SRC.glob("*.cpp"))
+    if out.exists() and all(s.stat().st_mtime <= out.stat().st_mtime for s in srcs):
+        return out
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-O3", "-shared", "-fPIC", "-std=c++17", "-Wall", f"-I{pybind11.get_include()}",
+           f"-I{sysconfig.get_paths()['include']}", *map(str, srcs), "-o", str(out)]
+    if verbose:
+        print(" ".join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"native runtime build failed:\n{r.stderr}")
+    print(f"[build] linked {out.relative_to(ROOT)}", flush=True)
+    return out
+
+
+def load():
+    global _mod
+    if _mod is None:
+        _mod = importlib.import_module("llm_kubernetes_minikube_sharp4dev_amd.native._runtime")
+    return _mod
 
 
 def available() -> bool:
-    return False
+    try:
+        load()
+        return True
+    except Exception:
+        return False
 
 
-def build():
-    raise NotImplementedError("native runtime not yet available")
+class NativeBlockAllocator:
+    """Thin adapter so the native allocator raises the engine's NoFreeBlocks type."""
+
+    def __init__(self, num_blocks: int, block_size: int, prefix_caching: bool = True):
+        m = load()
+        self._a = m.BlockAllocator(num_blocks, block_size, prefix_caching)
+        self._native_exc = m.NoFreeBlocks
+        self.num_blocks = num_blocks
+        self.block_size = block_size
+        self.prefix_caching = prefix_caching
+
+    def allocate(self) -> int:
+        from ..engine.block_manager import NoFreeBlocks
+
+        try:
+            return self._a.allocate()
+        except self._native_exc:
+            raise NoFreeBlocks() from None
+
+    def free_block(self, b: int):
+        self._a.free_block(b)
+
+    def free_all(self, blocks):
+        self._a.free_all(list(blocks))
+
+    def match_prefix(self, tokens):
+        blocks, parent = self._a.match_prefix([int(t) for t in tokens])
+        return list(blocks), parent
+
+    def register(self, block: int, parent: int, tokens) -> int:
+        return self._a.register(block, parent, [int(t) for t in tokens])
+
+    @property
+    def num_free(self) -> int:
+        return self._a.num_free
+
+    def usage(self) -> float:
+        return self._a.usage()
+
+    @property
+    def hits(self):
+        return self._a.hits
+
+    @property
+    def queries(self):
+        return self._a.queries
+
+    @property
+    def ref(self):
+        a = self._a
+
+        class _R:
+            def __getitem__(self, b):
+                return a.ref(b)
+
+        return _R()
+
+
+if __name__ == "__main__":  # pragma: no cover
+    build(verbose=True)
+    print("native runtime available:", available())
+    sys.exit(0)
