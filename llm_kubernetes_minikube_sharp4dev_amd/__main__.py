@@ -1,0 +1,231 @@
+"""Command line.
+
+  serve           Ollama-compatible server on :11434 (one GPU; ``--gpus N`` starts N
+                  replica processes + the DP router in front of them)
+  rag-app         Minimal_RAG port (:5103): /health, /rag/search, /agent_rag
+  agent-app       Minimal_Agent port (:5217): /health, /agent
+  all             server + both apps in one process sharing the engines (in-process
+                  LLM/embedding calls, no HTTP hop)
+  index           build / refresh the persisted RAG index of a knowledge folder
+  fake-apiserver  in-memory kube-apiserver (echoserver fixture) for demos/tests
+  router          DP router in front of existing replicas
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import os
+import subprocess
+import sys
+import time
+
+
+def _kv(items):
+    out = {}
+    for it in items or []:
+        k, _, v = it.partition("=")
+        out[k] = v
+    return out
+
+
+def _cfg(args):
+    from .config import load_config
+
+    cfg = load_config(getattr(args, "config", None))
+    if getattr(args, "knowledge", None):
+        cfg.rag.knowledge_dir = args.knowledge
+    if getattr(args, "kubeconfig", None):
+        cfg.agent.kubeconfig = args.kubeconfig
+        cfg.agent.fake_cluster = False
+    if getattr(args, "index_cache", None):
+        cfg.rag.cache_dir = args.index_cache
+    return cfg
+
+
+def _uvicorn(app, host, port):
+    import uvicorn
+
+    uvicorn.run(app, host=host, port=port, log_level="warning")
+
+
+def cmd_serve(args):
+    if args.gpus > 1:
+        return _serve_replicas(args)
+    from .serving.model_manager import ModelManager
+    from .serving.ollama_server import create_app
+
+    cfg = _cfg(args)
+    mgr = ModelManager(cfg, device=args.device, aliases=_kv(args.alias), checkpoints=_kv(args.checkpoint))
+    for m in args.preload or []:
+        kind, _ = mgr.resolve(m)
+        (mgr.generator if kind == "generate" else mgr.embedder)(m)
+    _uvicorn(create_app(mgr), args.host, args.port)
+
+
+def _serve_replicas(args):
+    """One process per GPU (HIP_VISIBLE_DEVICES) + router; this parent never touches
+    the GPU itself."""
+    procs, urls = [], []
+    base = args.port + 1
+    for g in range(args.gpus):
+        env = dict(os.environ, HIP_VISIBLE_DEVICES=str(g), CUDA_VISIBLE_DEVICES=str(g))
+        cmd = [sys.executable, "-m", "llm_kubernetes_minikube_sharp4dev_amd", "serve", "--host", "127.0.0.1",
+               "--port", str(base + g)] + sum([["--alias", a] for a in args.alias or []], []) + \
+            sum([["--checkpoint", c] for c in args.checkpoint or []], []) + \
+            sum([["--preload", p] for p in args.preload or []], [])
+        if args.config:
+            cmd += ["--config", args.config]
+        procs.append(subprocess.Popen(cmd, env=env))
+        urls.append(f"http://127.0.0.1:{base + g}")
+    try:
+        from .parallel.router import create_router_app
+
+        _uvicorn(create_router_app(urls), args.host, args.port)
+    finally:
+        for p in procs:
+            p.terminate()
+
+
+def _backends(args, cfg, mgr=None):
+    from .k8s.client import make_client
+    from .rag.embedder import LocalEmbedder, OllamaEmbedder
+    from .serving.backends import LocalGenerate, OllamaHTTPGenerate
+
+    k8s = make_client(cfg)
+    if mgr is not None:
+        emb = LocalEmbedder(mgr.embedder(cfg.rag.embed_model).engine)
+        llm = LocalGenerate(mgr, cfg.agent.gen_model)
+    else:
+        emb = OllamaEmbedder(cfg.agent.embedder_url, cfg.rag.embed_model)
+        llm = OllamaHTTPGenerate(cfg.agent.ollama_url, cfg.agent.gen_model)
+    return emb, llm, k8s
+
+
+def cmd_rag_app(args):
+    from .apps.rag_app import create_rag_app
+    from .rag.index import RagIndex
+
+    cfg = _cfg(args)
+    if args.ollama_url:
+        cfg.agent.ollama_url = cfg.agent.embedder_url = args.ollama_url
+    emb, llm, k8s = _backends(args, cfg)
+    idx = RagIndex(emb, backend=cfg.rag.index_backend)
+    _uvicorn(create_rag_app(cfg, idx, llm, k8s), args.host, args.port)
+
+
+def cmd_agent_app(args):
+    from .apps.agent_app import create_agent_app
+
+    cfg = _cfg(args)
+    if args.ollama_url:
+        cfg.agent.ollama_url = args.ollama_url
+    _, llm, k8s = _backends(args, cfg)
+    _uvicorn(create_agent_app(cfg, llm, k8s), args.host, args.port)
+
+
+def cmd_all(args):
+    import uvicorn
+
+    from .apps.agent_app import create_agent_app
+    from .apps.rag_app import create_rag_app
+    from .rag.index import RagIndex
+    from .serving.model_manager import ModelManager
+    from .serving.ollama_server import create_app
+
+    cfg = _cfg(args)
+    mgr = ModelManager(cfg, device=args.device, aliases=_kv(args.alias), checkpoints=_kv(args.checkpoint))
+    emb, llm, k8s = _backends(args, cfg, mgr)
+    idx = RagIndex(emb, backend=cfg.rag.index_backend)
+    apps = [(create_app(mgr), cfg.server.ollama_port), (create_rag_app(cfg, idx, llm, k8s), cfg.server.rag_port),
+            (create_agent_app(cfg, llm, k8s), cfg.server.agent_port)]
+
+    async def main():
+        servers = [uvicorn.Server(uvicorn.Config(a, host=args.host, port=p, log_level="warning")) for a, p in apps]
+        await asyncio.gather(*(s.serve() for s in servers))
+
+    asyncio.run(main())
+
+
+def cmd_index(args):
+    from .rag.embedder import OllamaEmbedder
+    from .rag.index import RagIndex
+
+    cfg = _cfg(args)
+    if args.local:
+        from .serving.model_manager import ModelManager
+        from .rag.embedder import LocalEmbedder
+
+        emb = LocalEmbedder(ModelManager(cfg).embedder(cfg.rag.embed_model).engine)
+    else:
+        emb = OllamaEmbedder(args.ollama_url or cfg.agent.embedder_url, cfg.rag.embed_model)
+    idx = RagIndex(emb, backend="exact")
+    t0 = time.time()
+    stats = idx.build_incremental(cfg.rag.knowledge_dir, args.index_cache or ".lk_index")
+    print({**stats, "seconds": round(time.time() - t0, 2)})
+
+
+def cmd_fake_apiserver(args):
+    from .k8s.fake import FakeCluster, make_apiserver_app
+
+    _uvicorn(make_apiserver_app(FakeCluster.default(fault_rate=args.fault_rate, latency_s=args.latency)),
+             args.host, args.port)
+
+
+def cmd_router(args):
+    from .parallel.router import create_router_app
+
+    _uvicorn(create_router_app(args.backends.split(",")), args.host, args.port)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="llm_kubernetes_minikube_sharp4dev_amd")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+
+    def common(p, port):
+        p.add_argument("--host", default="127.0.0.1")
+        p.add_argument("--port", type=int, default=port)
+        p.add_argument("--config", default=None)
+        return p
+
+    p = common(sub.add_parser("serve"), 11434)
+    p.add_argument("--device", default=None)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--alias", action="append", help="client-name=preset (e.g. llama3.1:8b=opt-125m)")
+    p.add_argument("--checkpoint", action="append", help="name-or-preset=safetensors dir")
+    p.add_argument("--preload", action="append")
+    p.set_defaults(fn=cmd_serve)
+    for name, port, fn in (("rag-app", 5103, cmd_rag_app), ("agent-app", 5217, cmd_agent_app)):
+        p = common(sub.add_parser(name), port)
+        p.add_argument("--ollama-url", default=None)
+        p.add_argument("--knowledge", default=None)
+        p.add_argument("--kubeconfig", default=None)
+        p.add_argument("--index-cache", default=None)
+        p.set_defaults(fn=fn)
+    p = common(sub.add_parser("all"), 0)
+    p.add_argument("--device", default=None)
+    p.add_argument("--alias", action="append")
+    p.add_argument("--checkpoint", action="append")
+    p.add_argument("--knowledge", default=None)
+    p.add_argument("--kubeconfig", default=None)
+    p.add_argument("--index-cache", default=None)
+    p.set_defaults(fn=cmd_all)
+    p = sub.add_parser("index")
+    p.add_argument("--config", default=None)
+    p.add_argument("--knowledge", default=None)
+    p.add_argument("--index-cache", default=None)
+    p.add_argument("--ollama-url", default=None)
+    p.add_argument("--local", action="store_true")
+    p.set_defaults(fn=cmd_index)
+    p = common(sub.add_parser("fake-apiserver"), 8001)
+    p.add_argument("--fault-rate", type=float, default=0.0)
+    p.add_argument("--latency", type=float, default=0.0)
+    p.set_defaults(fn=cmd_fake_apiserver)
+    p = common(sub.add_parser("router"), 11434)
+    p.add_argument("--backends", required=True)
+    p.set_defaults(fn=cmd_router)
+    args = ap.parse_args(argv)
+    return args.fn(args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

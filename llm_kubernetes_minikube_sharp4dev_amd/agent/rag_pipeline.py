@@ -103,3 +103,59 @@ class RagAgentPipeline:
             r.timings = {**tim, "generate_s": tgen, **s.metrics()}
             results.append(r)
         return results
+
+    def run_continuous(self, next_queries, params, concurrency: int, n_complete: int,
+                       admit_chunk: int = 16, on_done=None) -> list[RagAgentResult]:
+        """One-shot closed-loop run (see :class:`ContinuousLoad`); drains at the end."""
+        load = ContinuousLoad(self, next_queries, params, concurrency, admit_chunk)
+        out = load.run(n_complete, on_done)
+        load.drain()
+        return out
+
+
+class ContinuousLoad:
+    """Closed-loop serving load: keep ``concurrency`` requests in flight in the
+    continuous-batching engine; as requests finish, new ones are retrieved and
+    admitted (in chunks of ``admit_chunk`` so the query-encoder / kNN launches are
+    batched).  Decode tokens of running requests share every step with other
+    requests' chunked prefill, so the weights streamed for decode are amortised by
+    prefill compute.  ``run`` can be called repeatedly (warm-up, then the timed
+    window) without draining the in-flight requests in between; latency is measured
+    from admission to completion."""
+
+    def __init__(self, pipe: RagAgentPipeline, next_queries, params, concurrency: int, admit_chunk: int = 16):
+        self.pipe, self.next_queries, self.params = pipe, next_queries, params
+        self.concurrency, self.admit_chunk = concurrency, admit_chunk
+        self.inflight: dict = {}
+
+    def run(self, n_complete: int, on_done=None) -> list[RagAgentResult]:
+        pipe = self.pipe
+        done: list[RagAgentResult] = []
+        while len(done) < n_complete:
+            free = self.concurrency - len(self.inflight)
+            if free >= min(self.admit_chunk, self.concurrency) or not self.inflight:
+                qs = self.next_queries(free)
+                t_adm = time.perf_counter()
+                plans, tim = pipe.plan(qs)
+                for p, ids, cit, ev in plans:
+                    if ids is None:
+                        done.append(RagAgentResult(p, 200, {"result": None, "citations": [], "note": NO_EVIDENCE_NOTE}))
+                        continue
+                    seq = pipe.llm.add_request(ids, self.params.__class__(**{**self.params.__dict__}))
+                    seq.arrival = t_adm
+                    self.inflight[seq.req_id] = (seq, p, ids, cit, ev, tim)
+            pipe.llm.step()
+            for rid in [r for r, v in self.inflight.items() if v[0].finished]:
+                seq, p, ids, cit, ev, tim = self.inflight.pop(rid)
+                r = pipe.finish(p, seq.output_ids, cit, ev)
+                r.prompt_tokens = len(ids)
+                r.timings = {**tim, **seq.metrics(), "e2e_s": time.perf_counter() - seq.arrival}
+                done.append(r)
+                if on_done is not None:
+                    on_done(r)
+        return done
+
+    def drain(self):
+        for seq, *_ in self.inflight.values():
+            self.pipe.llm.abort(seq.req_id)
+        self.inflight.clear()

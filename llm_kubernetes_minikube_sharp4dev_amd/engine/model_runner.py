@@ -13,7 +13,7 @@ hipGraph-captured decode.
 from __future__ import annotations
 
 import bisect
-import math
+from dataclasses import dataclass, field
 from typing import Optional
 
 import numpy as np
@@ -41,19 +41,10 @@ class ModelRunner:
         self.L = cfg.num_layers
         self.hq, self.hkv, self.D = model.hq, model.hkv, model.D
         dt = model.dtype
-        esz = torch.tensor([], dtype=dt).element_size()
-        block_bytes = self.L * 2 * self.hkv * block_size * self.D * esz
+        block_bytes = self.block_bytes(model, block_size)
         if num_blocks is None:
-            if kv_cache_gb is not None:
-                num_blocks = int(kv_cache_gb * (1 << 30) // block_bytes)
-            elif self.device.type == "cuda":
-                free, total = torch.cuda.mem_get_info(self.device)
-                budget = free - (1 - gpu_memory_fraction) * total
-                num_blocks = int(max(budget, 0) // block_bytes)
-            else:
-                num_blocks = 512
-            cap = max_num_seqs * self.max_blocks + 64
-            num_blocks = max(16, min(num_blocks, cap))
+            num_blocks = self.plan_num_blocks(model, block_size, max_model_len, max_num_seqs, kv_cache_gb,
+                                              gpu_memory_fraction)
         self.num_blocks = num_blocks
         self.kv = torch.empty((self.L, 2, num_blocks, self.hkv, block_size, self.D), dtype=dt, device=self.device)
         self.kv_caches = [(self.kv[l, 0], self.kv[l, 1]) for l in range(self.L)]
@@ -64,7 +55,29 @@ class ModelRunner:
         self.graphs: dict = {}
         self._graph_pool = None
         self._ws = None
-        self.vocab = None
+        self.step_hook = None
+
+    @staticmethod
+    def block_bytes(model, block_size: int) -> int:
+        esz = torch.tensor([], dtype=model.dtype).element_size()
+        return model.cfg.num_layers * 2 * model.hkv * block_size * model.D * esz
+
+    @staticmethod
+    def plan_num_blocks(model, block_size=16, max_model_len=8192, max_num_seqs=256, kv_cache_gb=None,
+                        gpu_memory_fraction=0.85) -> int:
+        """KV blocks this rank can hold: an explicit GB budget, else the free HBM left
+        after weights minus the reserved fraction, capped at what max_num_seqs x
+        max_model_len could ever use."""
+        bb = ModelRunner.block_bytes(model, block_size)
+        if kv_cache_gb is not None:
+            n = int(kv_cache_gb * (1 << 30) // bb)
+        elif model.device.type == "cuda":
+            free, total = torch.cuda.mem_get_info(model.device)
+            n = int(max(free - (1 - gpu_memory_fraction) * total, 0) // bb)
+        else:
+            n = 512
+        cap = max_num_seqs * ((max_model_len + block_size - 1) // block_size) + 64
+        return max(16, min(n, cap))
 
     # ----------------------------------------------------------- workspaces
     def decode_split(self, B: int):
@@ -92,10 +105,12 @@ class ModelRunner:
             bt[i, : len(t)] = t
         return bt
 
-    # ----------------------------------------------------------- eager step
-    def build(self, items):
-        """items: [(seq, start, n)].  Returns (ids, meta, sample_rows) where
-        sample_rows lists (seq, row) of the rows that produce a next token."""
+    # ----------------------------------------------------------- step inputs (host)
+    def prepare(self, items):
+        """items [(seq, start, n)] -> (StepInputs of host arrays, rows [(seq, row)]).
+        Everything a rank needs to run the step; a TP driver broadcasts it."""
+        if self.use_graphs and items and all(s.is_decode for s, _, _ in items) and len(items) <= self.graph_sizes[-1]:
+            return self._prepare_graph(items)
         pre = [it for it in items if not it[0].is_decode]
         dec = [it for it in items if it[0].is_decode]
         ids, pos, slots = [], [], []
@@ -120,46 +135,81 @@ class ModelRunner:
             pos.append(p)
             rows.append((seq, r))
             r += 1
+        si = StepInputs(decode_graph=0, ids=np.asarray(ids, dtype=np.int32), positions=np.concatenate(pos),
+                        slots=np.concatenate(slots), q_lens=q_lens, ctx_lens=ctx,
+                        tables_p=self._bt(tables, max(len(t) for t in tables)) if pre else None,
+                        ctx_d=np.asarray([s.length for s, _, _ in dec], dtype=np.int32) if dec else None,
+                        tables_d=self._bt([s.block_table for s, _, _ in dec],
+                                          max(len(s.block_table) for s, _, _ in dec)) if dec else None,
+                        num_decode=len(dec), logits_rows=np.asarray([row for _, row in rows], dtype=np.int64))
+        return si, rows
+
+    def _prepare_graph(self, items):
+        B = len(items)
+        Bg = self._graph_bucket(B)
+        ids = np.zeros(Bg, dtype=np.int32)
+        pos = np.zeros(Bg, dtype=np.int32)
+        slots = np.full(Bg, -1, dtype=np.int32)
+        ctx = np.ones(Bg, dtype=np.int32)
+        bt = np.zeros((Bg, self.max_blocks), dtype=np.int32)
+        rows = []
+        for i, (seq, start, n) in enumerate(items):
+            ids[i] = seq.token_at(start)
+            pos[i] = start
+            slots[i] = seq.block_table[start // self.bs] * self.bs + start % self.bs
+            ctx[i] = seq.length
+            bt[i, : len(seq.block_table)] = seq.block_table
+            rows.append((seq, i))
+        si = StepInputs(decode_graph=Bg, ids=ids, positions=pos, slots=slots, ctx_d=ctx, tables_d=bt,
+                        num_decode=B, logits_rows=np.arange(B, dtype=np.int64))
+        return si, rows
+
+    # ----------------------------------------------------------- execution (device)
+    def _meta(self, si: "StepInputs"):
         dev = self.device
-        T = r
-        meta = AttnMeta(
-            positions=torch.from_numpy(np.concatenate(pos)).to(dev, non_blocking=True),
-            slots=torch.from_numpy(np.concatenate(slots)).to(dev, non_blocking=True),
-            num_prefill_tokens=sum(q_lens), num_prefill_seqs=len(pre), num_decode=len(dec),
-        )
-        if pre:
-            cu = np.zeros(len(pre) + 1, dtype=np.int32)
-            cu[1:] = np.cumsum(q_lens)
-            width = max(len(t) for t in tables)
-            meta.cu_q = torch.from_numpy(cu).to(dev, non_blocking=True)
-            meta.ctx_lens_p = torch.tensor(ctx, dtype=torch.int32).to(dev, non_blocking=True)
-            meta.block_tables_p = torch.from_numpy(self._bt(tables, width)).to(dev, non_blocking=True)
-            meta.q_lens_cpu, meta.ctx_lens_cpu = q_lens, ctx
-        if dec:
-            dt = [s.block_table for s, _, _ in dec]
-            width = max(len(t) for t in dt)
-            meta.block_tables_d = torch.from_numpy(self._bt(dt, width)).to(dev, non_blocking=True)
-            meta.ctx_lens_d = torch.tensor([s.length for s, _, _ in dec], dtype=torch.int32).to(dev, non_blocking=True)
-            meta.decode_split = max(ops.decode_split_size(len(dec), self.hkv), self.bs)
-            meta.max_splits = ops.decode_splits(width * self.bs, meta.decode_split)
-        meta.logits_idx = torch.tensor([row for _, row in rows], dtype=torch.long).to(dev, non_blocking=True)
-        ids_t = torch.tensor(ids, dtype=torch.int32).to(dev, non_blocking=True)
-        assert ids_t.shape[0] == T
-        return ids_t, meta, rows
+
+        def t(a, dt=None):
+            return torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)
+
+        Tp = int(sum(si.q_lens))
+        meta = AttnMeta(positions=t(si.positions), slots=t(si.slots), num_prefill_tokens=Tp,
+                        num_prefill_seqs=len(si.q_lens), num_decode=si.num_decode)
+        if si.q_lens:
+            cu = np.zeros(len(si.q_lens) + 1, dtype=np.int32)
+            cu[1:] = np.cumsum(si.q_lens)
+            meta.cu_q = t(cu)
+            meta.ctx_lens_p = t(np.asarray(si.ctx_lens, dtype=np.int32))
+            meta.block_tables_p = t(si.tables_p)
+            meta.q_lens_cpu, meta.ctx_lens_cpu = list(si.q_lens), list(si.ctx_lens)
+        if si.num_decode:
+            meta.block_tables_d = t(si.tables_d)
+            meta.ctx_lens_d = t(si.ctx_d)
+            meta.decode_split = max(ops.decode_split_size(si.num_decode, self.hkv), self.bs)
+            meta.max_splits = ops.decode_splits(si.tables_d.shape[1] * self.bs, meta.decode_split)
+        meta.logits_idx = t(si.logits_rows) if len(si.logits_rows) else None
+        return t(si.ids), meta
 
     @torch.inference_mode()
+    def execute(self, si: "StepInputs"):
+        """Run one step on this rank; returns logits [R, V] f32 (None if no rows)."""
+        if si.decode_graph:
+            return self._graph_execute(si)
+        ids, meta = self._meta(si)
+        if meta.logits_idx is None:
+            self.model(ids, meta, self.kv_caches)  # partial prefill chunks only: KV write, no logits
+            return None
+        h = self.model(ids, meta, self.kv_caches)
+        return self.model.logits(h)
+
     def forward_logits(self, items):
         """Run one step; returns (rows [(seq,row)], logits [R, V] f32)."""
         if not items:
             return [], None
-        if self.use_graphs and all(s.is_decode for s, _, _ in items) and len(items) <= self.graph_sizes[-1]:
-            return self._graph_step(items)
-        ids, meta, rows = self.build(items)
-        if not rows:
-            self.model(ids, meta, self.kv_caches)  # partial prefill chunks only: KV write, no logits
-            return [], None
-        h = self.model(ids, meta, self.kv_caches)
-        return rows, self.model.logits(h)
+        si, rows = self.prepare(items)
+        if self.step_hook is not None:
+            self.step_hook(si)  # e.g. TP driver broadcast to worker ranks
+        lg = self.execute(si)
+        return rows, (lg if rows else None)
 
     # ----------------------------------------------------------- hipGraph decode
     def _graph_bucket(self, B):
@@ -202,34 +252,37 @@ class ModelRunner:
         self.graphs[B] = st
         return st
 
+    @torch.inference_mode()
     def capture_all(self, max_batch: Optional[int] = None):
         for B in self.graph_sizes:
             if max_batch is None or B <= max_batch:
                 if B not in self.graphs:
                     self.capture(B)
 
-    def _graph_step(self, items):
-        B = len(items)
-        Bg = self._graph_bucket(B)
+    def _graph_execute(self, si):
+        Bg = si.decode_graph
         st = self.graphs.get(Bg) or self.capture(Bg)
-        ids = np.zeros(Bg, dtype=np.int32)
-        pos = np.zeros(Bg, dtype=np.int32)
-        slots = np.full(Bg, -1, dtype=np.int32)
-        ctx = np.ones(Bg, dtype=np.int32)
-        bt = np.zeros((Bg, self.max_blocks), dtype=np.int32)
-        rows = []
-        for i, (seq, start, n) in enumerate(items):
-            ids[i] = seq.token_at(start)
-            pos[i] = start
-            blk = seq.block_table[start // self.bs]
-            slots[i] = blk * self.bs + start % self.bs
-            ctx[i] = seq.length
-            bt[i, : len(seq.block_table)] = seq.block_table
-            rows.append((seq, i))
-        st["ids"].copy_(torch.from_numpy(ids), non_blocking=True)
-        st["pos"].copy_(torch.from_numpy(pos), non_blocking=True)
-        st["slots"].copy_(torch.from_numpy(slots), non_blocking=True)
-        st["ctx"].copy_(torch.from_numpy(ctx), non_blocking=True)
-        st["bt"].copy_(torch.from_numpy(bt), non_blocking=True)
+        st["ids"].copy_(torch.from_numpy(si.ids), non_blocking=True)
+        st["pos"].copy_(torch.from_numpy(si.positions), non_blocking=True)
+        st["slots"].copy_(torch.from_numpy(si.slots), non_blocking=True)
+        st["ctx"].copy_(torch.from_numpy(si.ctx_d), non_blocking=True)
+        st["bt"].copy_(torch.from_numpy(si.tables_d), non_blocking=True)
         st["graph"].replay()
-        return rows, st["logits"][:B]
+        return st["logits"][: si.num_decode]
+
+
+@dataclass
+class StepInputs:
+    """Host-side description of one engine step (broadcast to TP worker ranks)."""
+
+    ids: np.ndarray
+    positions: np.ndarray
+    slots: np.ndarray
+    num_decode: int = 0
+    decode_graph: int = 0                 # >0: replay the decode hipGraph of this bucket
+    q_lens: list = field(default_factory=list)
+    ctx_lens: list = field(default_factory=list)
+    tables_p: Optional[np.ndarray] = None
+    ctx_d: Optional[np.ndarray] = None
+    tables_d: Optional[np.ndarray] = None
+    logits_rows: np.ndarray = field(default_factory=lambda: np.zeros(0, dtype=np.int64))

@@ -1,0 +1,142 @@
+"""Multi-process (gloo, world_size 2) tests of the distributed paths: tensor-parallel
+Llama/OPT generation == single process, sharded kNN == unsharded, TP engine driver /
+worker lockstep, DP router over two replicas."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+transformers = pytest.importorskip("transformers")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _hf_llama(seed=0):
+    cfg = transformers.LlamaConfig(vocab_size=512, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+                                   num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=1024,
+                                   rope_theta=10000.0, tie_word_embeddings=False)
+    torch.manual_seed(seed)
+    return transformers.LlamaForCausalLM(cfg).eval()
+
+
+def _ours_cfg(arch):
+    from llm_kubernetes_minikube_sharp4dev_amd.models.configs import DecoderConfig
+
+    if arch == "llama":
+        return DecoderConfig("t", "llama", 2, 128, 4, 2, 32, 256, 512, max_position=1024, rope_theta=10000.0)
+    return DecoderConfig("t", "opt", 2, 64, 2, 2, 32, 128, 512, max_position=256, tie_word_embeddings=True,
+                         activation="relu", bias=True)
+
+
+def _hf(arch):
+    if arch == "llama":
+        return _hf_llama()
+    cfg = transformers.OPTConfig(vocab_size=512, hidden_size=64, ffn_dim=128, num_hidden_layers=2,
+                                 num_attention_heads=2, max_position_embeddings=256, word_embed_proj_dim=64)
+    torch.manual_seed(1)
+    return transformers.OPTForCausalLM(cfg).eval()
+
+
+PROMPTS = [[5, 17, 99, 3, 250, 7, 7, 1, 400, 33, 21, 8, 2, 9, 11, 60, 61, 62, 63], [7, 8, 9], list(range(10, 60))]
+
+
+def _tp_worker(rank, world, port, arch, out_path):
+    _init(rank, world, port)
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import SamplingParams
+    from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp import TPGroup
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp_engine import make_tp_engine, run_tp_worker, shutdown_tp
+
+    tp = TPGroup(rank, world, dist.group.WORLD)
+    m = build_decoder(_ours_cfg(arch), dtype=torch.float32, tp=tp)
+    m.load_hf_state_dict(_hf(arch).state_dict())
+    kw = dict(block_size=16, max_model_len=512, max_num_seqs=8, num_blocks=96)
+    if rank == 0:
+        eng = make_tp_engine(m, tp, None, engine_kw={"eos_ids": set(), "max_num_batched_tokens": 40}, **kw)
+        seqs = eng.generate(PROMPTS, SamplingParams.greedy(10))
+        shutdown_tp(eng)
+        torch.save([s.output_ids for s in seqs], out_path)
+    else:
+        run_tp_worker(m, tp, **kw)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("arch", ["llama", "opt"])
+def test_tp2_generation_matches_single_process(arch):
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.llm_engine import LLMEngine
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import SamplingParams
+    from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder
+
+    m = build_decoder(_ours_cfg(arch), dtype=torch.float32)
+    m.load_hf_state_dict(_hf(arch).state_dict())
+    eng = LLMEngine(m, None, max_model_len=512, max_num_seqs=8, num_blocks=96, eos_ids=set())
+    ref = [s.output_ids for s in eng.generate(PROMPTS, SamplingParams.greedy(10))]
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "out.pt")
+        mp.spawn(_tp_worker, args=(2, _free_port(), arch, out), nprocs=2, join=True)
+        got = torch.load(out, weights_only=True)
+    assert got == ref
+
+
+def _knn_worker(rank, world, port, out_path):
+    _init(rank, world, port)
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.sharded_index import ShardedKnnIndex
+
+    g = torch.Generator().manual_seed(0)
+    corpus = torch.randn(301, 32, generator=g)
+    corpus[200] = corpus[5]  # duplicate across shards -> tie resolved by global id
+    q = torch.randn(4, 32, generator=g)
+    q[0] = corpus[5]
+    idx = ShardedKnnIndex.from_full(corpus)
+    s, i = idx.search(q, 7)
+    if rank == 0:
+        torch.save((s, i), out_path)
+    dist.destroy_process_group()
+
+
+def test_sharded_knn_equals_single():
+    from llm_kubernetes_minikube_sharp4dev_amd import ops
+
+    g = torch.Generator().manual_seed(0)
+    corpus = torch.randn(301, 32, generator=g)
+    corpus[200] = corpus[5]
+    q = torch.randn(4, 32, generator=g)
+    q[0] = corpus[5]
+    rs, ri = ops.knn_topk(corpus, ops.row_norms(corpus), q, ops.row_norms(q), 7)
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "knn.pt")
+        mp.spawn(_knn_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+        s, i = torch.load(out, weights_only=True)
+    assert torch.equal(i.int(), ri.int())
+    assert torch.allclose(s.float(), rs.float(), atol=1e-6)
+    assert int(i[0, 0]) == 5 and int(i[0, 1]) == 200
+
+
+def test_router_balances_two_replicas():
+    from fastapi.testclient import TestClient
+
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.router import ReplicaPool
+
+    pool = ReplicaPool(["http://a", "http://b"])
+    a = pool.pick()
+    a.inflight += 1
+    b = pool.pick()
+    assert a.url != b.url
+    b.inflight += 1
+    pool.mark_failed(a)
+    assert pool.pick().url == b.url
