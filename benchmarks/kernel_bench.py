@@ -107,12 +107,21 @@ def case_knn(N=485_000, D=768, nq=64):
     return {"case": f"knn_topk N{N} D{D} nq{nq} k6", "us": t * 1e6, "GB/s": N * D * 2 / t / 1e9}
 
 
-def case_gemm(M, N, K):
+def case_gemm(M, N, K, layout="NT"):
+    """hipBLASLt via torch: NT = x @ W^T with W [N,K] (nn.Linear layout), NN = x @ W with W [K,N]."""
     a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
-    b = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
-    t = timeit(lambda: torch.nn.functional.linear(a, b))
-    return {"case": f"hipBLASLt linear M{M} N{N} K{K}", "us": t * 1e6, "TFLOP/s": 2 * M * N * K / t / 1e12,
+    if layout == "NT":
+        b = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+        fn = lambda: torch.nn.functional.linear(a, b)  # noqa: E731
+    else:
+        b = torch.randn(K, N, device=DEV, dtype=torch.bfloat16)
+        fn = lambda: a @ b  # noqa: E731
+    t = timeit(fn)
+    return {"case": f"hipBLASLt {layout} M{M} N{N} K{K}", "us": t * 1e6, "TFLOP/s": 2 * M * N * K / t / 1e12,
             "GB/s": (M * K + N * K + M * N) * 2 / t / 1e9}
+
+
+LLAMA8B_SHAPES = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]
 
 
 CASES = {
@@ -123,6 +132,8 @@ CASES = {
     "knn": lambda: [case_knn()],
     "gemm": lambda: [case_gemm(64, 6144, 4096), case_gemm(64, 28672, 4096), case_gemm(64, 4096, 14336),
                      case_gemm(32768, 6144, 4096), case_gemm(32768, 28672, 4096), case_gemm(32768, 4096, 14336)],
+    "gemm_sweep": lambda: [case_gemm(M, N, K, lay) for M in (128, 256, 1024, 4096, 8192, 16384)
+                           for (N, K) in LLAMA8B_SHAPES for lay in ("NT", "NN")],
 }
 
 
