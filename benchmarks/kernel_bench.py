@@ -121,6 +121,21 @@ def case_gemm(M, N, K, layout="NT"):
             "GB/s": (M * K + N * K + M * N) * 2 / t / 1e9}
 
 
+def case_skinny(M, N, K, swiglu=False):
+    """Hand-written decode-regime GEMM vs hipBLASLt (+ silu_mul when swiglu) at the same shape."""
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+    L = ops.lib()
+    t = timeit(lambda: L.skinny_linear(a, b, swiglu))
+    if swiglu:
+        tb = timeit(lambda: ops.silu_mul(torch.nn.functional.linear(a, b)))
+    else:
+        tb = timeit(lambda: torch.nn.functional.linear(a, b))
+    byts = (N * K + M * K + M * N) * 2
+    return {"case": f"skinny{'+swiglu' if swiglu else ''} M{M} N{N} K{K} S{L.skinny_splits(min(M, 128), N, K, swiglu)}",
+            "us": t * 1e6, "GB/s": byts / t / 1e9, "hipblaslt_us": tb * 1e6, "speedup": tb / t}
+
+
 LLAMA8B_SHAPES = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]
 
 
@@ -132,6 +147,8 @@ CASES = {
     "knn": lambda: [case_knn()],
     "gemm": lambda: [case_gemm(64, 6144, 4096), case_gemm(64, 28672, 4096), case_gemm(64, 4096, 14336),
                      case_gemm(32768, 6144, 4096), case_gemm(32768, 28672, 4096), case_gemm(32768, 4096, 14336)],
+    "skinny": lambda: [case_skinny(M, N, K, N == 28672) for M in (1, 16, 32, 64, 128, 256)
+                       for (N, K) in LLAMA8B_SHAPES + [(128256, 4096)]],
     "gemm_sweep": lambda: [case_gemm(M, N, K, lay) for M in (128, 256, 1024, 4096, 8192, 16384)
                            for (N, K) in LLAMA8B_SHAPES for lay in ("NT", "NN")],
 }
@@ -150,9 +167,10 @@ def main():
             rows.append(r)
     if a.md:
         with open(a.md, "w") as f:
-            f.write("| case | us | GB/s | TFLOP/s |\n|---|---|---|---|\n")
+            f.write("| case | us | GB/s | TFLOP/s | hipBLASLt us | speedup |\n|---|---|---|---|---|---|\n")
             for r in rows:
-                f.write(f"| {r['case']} | {r['us']} | {r.get('GB/s', '')} | {r.get('TFLOP/s', '')} |\n")
+                f.write(f"| {r['case']} | {r['us']} | {r.get('GB/s', '')} | {r.get('TFLOP/s', '')} "
+                        f"| {r.get('hipblaslt_us', '')} | {r.get('speedup', '')} |\n")
 
 
 if __name__ == "__main__":

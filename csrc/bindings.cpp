@@ -105,6 +105,38 @@ at::Tensor silu_mul(const at::Tensor& x, const c10::optional<at::Tensor>& out_) 
   return out;
 }
 
+// Decode-regime linear: x [M, K] (M <= 256, row-contiguous) . w[N, K]^T -> [M, N];
+// swiglu=true: w = [Wg; Wu] (2I rows) -> silu(x Wg^T) * (x Wu^T) [M, I].  Rows beyond
+// 128 are processed as a second launch (the weight stream is re-read; still far
+// below the library GEMM at these shapes).
+at::Tensor skinny_linear(const at::Tensor& x, const at::Tensor& w, bool swiglu, int64_t splits,
+                         const c10::optional<at::Tensor>& out_) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_LASTDIM(x); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "x [M,K], w [N,K]");
+  check_rows16(x, "x"); check_rows16(w, "w");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(M >= 1 && M <= 256, "skinny_linear: M must be in [1, 256]");
+  const int n_out = swiglu ? N / 2 : N;
+  at::Tensor out = out_ ? *out_ : at::empty({M, n_out}, x.options());
+  CHECK_BF16(out); CHECK_LASTDIM(out); check_rows16(out, "out");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == n_out, "out shape");
+  const int S = splits > 0 ? (int)splits : lk_skinny_splits(std::min(M, 128), N, K, swiglu);
+  at::Tensor part;
+  if (S > 1) part = at::empty({(long)S * std::min(M, 128) * N}, x.options().dtype(at::kFloat));
+  for (int m0 = 0; m0 < M; m0 += 128) {
+    const int mc = std::min(128, M - m0);
+    int rc = lk_skinny_gemm(bp(x) + (long)m0 * x.stride(0), x.stride(0), bp(w), mc, N, K, S, swiglu ? 1 : 0,
+                            bp(out) + (long)m0 * out.stride(0), out.stride(0),
+                            S > 1 ? part.data_ptr<float>() : nullptr, cur_stream());
+    CHECK_RC(rc, "skinny_linear");
+  }
+  return out;
+}
+
+int64_t skinny_splits(int64_t M, int64_t N, int64_t K, bool swiglu) {
+  return lk_skinny_splits((int)M, (int)N, (int)K, swiglu ? 1 : 0);
+}
+
 void activation_(at::Tensor& x, const c10::optional<at::Tensor>& bias, int64_t kind) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_LASTDIM(x);
   TORCH_CHECK(x.dim() == 2, "x must be 2-D");
@@ -320,6 +352,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rmsnorm", &rmsnorm, "", py::arg("x"), py::arg("w"), py::arg("eps"), py::arg("residual") = py::none(), py::arg("out") = py::none());
   m.def("layernorm", &layernorm, "", py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"), py::arg("residual") = py::none(), py::arg("write_residual") = false);
   m.def("embed_layernorm", &embed_layernorm);
+  m.def("skinny_linear", &skinny_linear, "", py::arg("x"), py::arg("w"), py::arg("swiglu") = false,
+        py::arg("splits") = 0, py::arg("out") = py::none());
+  m.def("skinny_splits", &skinny_splits);
   m.def("silu_mul", &silu_mul, "", py::arg("x"), py::arg("out") = py::none());
   m.def("activation_", &activation_);
   m.def("rope_kv_", &rope_kv_);

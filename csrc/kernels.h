@@ -22,6 +22,11 @@ int lk_silu_mul(bf16_t* out, const bf16_t* x, long rows, int I, long xs, long os
 int lk_activation(bf16_t* x, const bf16_t* bias, long rows, int N, long xs, int kind,
                   hipStream_t st);
 
+// skinny_gemm.hip (decode-regime linear, optional fused SwiGLU)
+int lk_skinny_splits(int M, int N, int K, int swiglu);
+int lk_skinny_gemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int S, int swiglu,
+                   bf16_t* out, long ldo, float* part, hipStream_t st);
+
 // rope_kv.hip
 int lk_rope_kv(bf16_t* qkv, long qs, const int* positions, const float* cos_sin, long T, int Hq,
                int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,

@@ -104,8 +104,7 @@ class LlamaModel(nn.Module):
             o = ops.linear(attn_out, L.o)
             self.tp.all_reduce_(o)
             x = ops.rmsnorm(o, L.post_norm, cfg.norm_eps, residual=res)
-            gu = ops.linear(x, L.gate_up)
-            a = ops.silu_mul(gu)
+            a = ops.linear_swiglu(x, L.gate_up)
             d = ops.linear(a, L.down)
             self.tp.all_reduce_(d)
             nxt = self.layers[li + 1].input_norm if li + 1 < n else self.final_norm

@@ -6,6 +6,7 @@ Layouts are documented in :mod:`.reference`.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Sequence
 
 import numpy as np
@@ -17,7 +18,7 @@ from ._ext import available, force_reference, lib, use_hip  # noqa: F401
 __all__ = [
     "rmsnorm", "layernorm", "embed_layernorm", "silu_mul", "gelu_", "relu_", "rope_kv_",
     "kv_write", "paged_decode", "flash_prefill", "prefill_tiles", "knn_topk", "knn_merge",
-    "pool_normalize", "row_norms", "select_tokens", "repeat_penalty_", "linear",
+    "pool_normalize", "row_norms", "select_tokens", "repeat_penalty_", "linear", "linear_swiglu",
     "decode_splits", "rope_cos_sin",
 ]
 
@@ -220,9 +221,50 @@ def repeat_penalty_(logits, window, penalty):
     return ref.repeat_penalty_(logits, window, penalty)
 
 
+# When the hand-written decode-regime GEMM (csrc/skinny_gemm.hip) replaces the library
+# GEMM.  Measured on MI355X (profiles/r1_skinny_gemm.md): it wins wherever N is too
+# small for hipBLASLt to fill the chip (QKV / O / down at 64-96 column tiles of 64:
+# 1.3-2.3x at M <= 64, O/down still 1.3x at M = 128) and loses on wide N (gate_up,
+# LM head) beyond a handful of rows, where its fragment-shaped loads cap the per-CU
+# load rate; there hipBLASLt keeps the job.
+SKINNY_MAX_M = int(os.environ.get("LK_SKINNY_MAX_M", "128"))
+
+
+def _skinny_wanted(M: int, N: int, swiglu: bool) -> bool:
+    tiles = (N // 2) // 32 if swiglu else N // 64
+    if M <= 8:
+        return True
+    if tiles >= 256:
+        return False
+    return M <= (128 if tiles <= 64 else 64)
+
+
+def _skinny_ok(x, w, swiglu: bool) -> bool:
+    if not (use_hip(x) and x.dim() == 2 and w.dim() == 2 and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and 1 <= x.shape[0] <= SKINNY_MAX_M):
+        return False
+    N, K = w.shape
+    if K % 256 or x.stride(1) != 1 or x.stride(0) % 8 or not w.is_contiguous():
+        return False
+    if not ((N % 2 == 0 and (N // 2) % 32 == 0) if swiglu else N % 64 == 0):
+        return False
+    return _skinny_wanted(x.shape[0], N, swiglu)
+
+
 def linear(x, w, b=None):
-    """Plain projection GEMM (hipBLASLt through torch on the GPU)."""
+    """Projection GEMM: decode-sized batches (M <= SKINNY_MAX_M) on the hand-written
+    weight-streaming MFMA kernel, everything else on hipBLASLt through torch."""
+    if b is None and _skinny_ok(x, w, False):
+        return lib().skinny_linear(x, w)
     return torch.nn.functional.linear(x, w, b)
+
+
+def linear_swiglu(x, w_gate_up):
+    """silu(x Wg^T) * (x Wu^T) for a fused [Wg; Wu] weight: one kernel (GEMM with the
+    SwiGLU epilogue) in the decode regime, hipBLASLt + silu_mul otherwise."""
+    if _skinny_ok(x, w_gate_up, True):
+        return lib().skinny_linear(x, w_gate_up, True)
+    return silu_mul(linear(x, w_gate_up))
 
 
 def softmax_scale(D: int) -> float:

@@ -268,3 +268,45 @@ def test_repeat_penalty(hip):
     hip.repeat_penalty_(a, win, pen)
     ref.repeat_penalty_(b, win.cpu(), pen.cpu())
     _close(a, b, 1e-6)
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64, 100, 128, 200, 256])
+@pytest.mark.parametrize("NK", [(6144, 4096), (4096, 4096), (4096, 14336), (1280, 8192), (768, 768)])
+def test_skinny_linear(hip, M, NK):
+    """Decode-regime GEMM (split-K + reduce where chosen) vs an fp32 matmul."""
+    N, K = NK
+    torch.manual_seed(M)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    y = hip.skinny_linear(x, w)
+    y_ref = x.float() @ w.float().t()
+    _close(y, y_ref, 0.02, 0.01, f"skinny M{M} N{N} K{K}")
+    for S in (1, 2):  # explicit split counts agree
+        if K % (S * 256) == 0:
+            _close(hip.skinny_linear(x, w, False, S), y_ref, 0.02, 0.01, f"skinny S{S}")
+
+
+@pytest.mark.parametrize("M", [1, 5, 64, 128, 130])
+@pytest.mark.parametrize("IK", [(14336, 4096), (3584, 8192), (1536, 512)])
+def test_skinny_swiglu_matches_unfused(hip, M, IK):
+    """GEMM with the fused SwiGLU epilogue == linear -> silu_mul, bit for bit modulo the
+    GEMM accumulation order."""
+    I, K = IK
+    torch.manual_seed(1)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(2 * I, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    a = hip.skinny_linear(x, w, True)
+    gu = (x.float() @ w.float().t()).to(torch.bfloat16)
+    a_ref = ref.silu_mul(gu)
+    _close(a, a_ref, 0.03, 0.01, f"swiglu M{M} I{I}")
+    if K % 512 == 0:
+        _close(hip.skinny_linear(x, w, True, 2), a_ref, 0.03, 0.01, "swiglu split 2")
+
+
+def test_linear_dispatch_uses_skinny(hip):
+    x = torch.randn(8, 4096, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(6144, 4096, device=DEV, dtype=torch.bfloat16) * 0.05
+    assert ops._skinny_ok(x, w, False)
+    _close(ops.linear(x, w), x.float() @ w.float().t(), 0.02, 0.01)
+    assert not ops._skinny_ok(torch.randn(512, 4096, device=DEV, dtype=torch.bfloat16), w, False)
+    assert not ops._skinny_wanted(64, 28672, True) and ops._skinny_wanted(4, 28672, True)
