@@ -161,8 +161,7 @@ static std::pair<std::vector<int32_t>, std::vector<int32_t>> slots_for(const std
   return {slots, pos};
 }
 
-PYBIND11_MODULE(_runtime, m) {
-  m.doc() = "native runtime: paged-KV block allocator with prefix caching";
+void register_block_allocator(py::module_& m) {
   py::register_exception<NoFreeBlocks>(m, "NoFreeBlocks", PyExc_RuntimeError);
   m.def("chain_hash", [](uint64_t parent, const std::vector<int64_t>& t) { return chain_hash(parent, t.data(), t.size()); });
   m.def("slots_for", &slots_for);

@@ -23,18 +23,41 @@ _SHORT = {"\b": "\\b", "\t": "\\t", "\n": "\\n", "\f": "\\f", "\r": "\\r", "\\":
 _ESC_ASCII = set('"&\'+<>`') | {chr(0x7F)}
 
 
+def _esc_char(ch: str) -> str:
+    if ch in _SHORT:
+        return _SHORT[ch]
+    o = ord(ch)
+    if o > 0xFFFF:
+        o -= 0x10000
+        return "\\u%04X\\u%04X" % (0xD800 + (o >> 10), 0xDC00 + (o & 0x3FF))
+    return "\\u%04X" % o
+
+
+# everything JavaScriptEncoder.Default escapes: controls, the HTML-sensitive ASCII set,
+# DEL and all non-ASCII; runs of safe characters pass through re.sub untouched (C speed)
+_NEEDS_ESC = re.compile("[\x00-\x1f\\\\\"&'+<>`\x7f-\U0010ffff]")
+_ESC_CACHE: dict = {}
+
+
+def _esc_sub(m) -> str:
+    ch = m.group(0)
+    r = _ESC_CACHE.get(ch)
+    if r is None:
+        r = _ESC_CACHE[ch] = _esc_char(ch)
+    return r
+
+
 def _esc_str(s: str) -> str:
+    return '"' + _NEEDS_ESC.sub(_esc_sub, s) + '"'
+
+
+def _esc_str_slow(s: str) -> str:
+    """Character-by-character reference form of :func:`_esc_str` (tests)."""
     out = ['"']
     for ch in s:
         o = ord(ch)
-        if ch in _SHORT:
-            out.append(_SHORT[ch])
-        elif o < 0x20 or ch in _ESC_ASCII or o > 0x7E:
-            if o > 0xFFFF:
-                o -= 0x10000
-                out.append("\\u%04X\\u%04X" % (0xD800 + (o >> 10), 0xDC00 + (o & 0x3FF)))
-            else:
-                out.append("\\u%04X" % o)
+        if ch in _SHORT or o < 0x20 or ch in _ESC_ASCII or o > 0x7E:
+            out.append(_esc_char(ch))
         else:
             out.append(ch)
     out.append('"')

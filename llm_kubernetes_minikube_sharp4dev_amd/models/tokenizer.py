@@ -39,12 +39,58 @@ def _train_builtin(vocab_size: int = 16384):
     return tok
 
 
-class Tokenizer:
-    """Thin wrapper with the few calls the engine needs."""
+LLAMA3_SPLIT = (r"(?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}{1,3}| ?[^\s\p{L}\p{N}]+[\r\n]*"
+                r"|\s*[\r\n]+|\s+(?!\S)|\s+")
+_PROBES = ["Hello world's   test\n\n  x", "kubectl scale deploy/echoserver --replicas=3 -n dev",
+           "\u00e8 perch\u00e9 \u4f60\u597d 12345 \U0001F600 <|eot_id|> 'Re 'LL x''y",
+           '{"Question":"scala a 3","Evidence":[{"Id":"a.md#0","Score":0.71}]}\r\n\t end  ']
 
-    def __init__(self, hf_tok, kind: str = "builtin"):
+
+def native_encoder(hf_tok):
+    """Native C++ BPE encoder (csrc/runtime/bpe.cpp) equivalent to ``hf_tok`` for the
+    byte-level families it implements, or None (unsupported layout, runtime not built,
+    or a probe mismatch)."""
+    try:
+        from ..native import runtime as nrt
+
+        if not nrt.available():
+            return None
+        d = json.loads(hf_tok.to_str())
+        m, pre = d.get("model") or {}, d.get("pre_tokenizer") or {}
+        if (d.get("normalizer") is not None or m.get("type") != "BPE" or m.get("byte_fallback")
+                or m.get("continuing_subword_prefix") or m.get("end_of_word_suffix") or m.get("dropout")):
+            return None
+        if pre.get("type") == "ByteLevel" and pre.get("use_regex", True) and not pre.get("add_prefix_space"):
+            mode = "gpt2"
+        elif (pre.get("type") == "Sequence" and len(pre.get("pretokenizers", [])) == 2
+              and pre["pretokenizers"][0].get("type") == "Split"
+              and pre["pretokenizers"][0].get("pattern", {}).get("Regex") == LLAMA3_SPLIT
+              and pre["pretokenizers"][1].get("type") == "ByteLevel"
+              and not pre["pretokenizers"][1].get("use_regex", True)
+              and not pre["pretokenizers"][1].get("add_prefix_space")):
+            mode = "llama3"
+        else:
+            return None
+        merges = [tuple(x) if isinstance(x, list) else tuple(x.split(" ", 1)) for x in m["merges"]]
+        added = [(a["content"], int(a["id"]), bool(a.get("special"))) for a in d.get("added_tokens", [])]
+        enc = nrt.load().BpeTokenizer(m["vocab"], merges, added, mode, bool(m.get("ignore_merges")))
+        for p in _PROBES:
+            if enc.encode(p) != hf_tok.encode(p, add_special_tokens=False).ids:
+                return None
+        return enc
+    except Exception:  # pragma: no cover - fall back to the HF encoder
+        return None
+
+
+class Tokenizer:
+    """Thin wrapper with the few calls the engine needs.  Encoding runs on the native
+    BPE encoder when it supports the tokenizer (token-for-token equal to HF; GIL
+    released, multi-threaded batches), decoding on HF ``tokenizers``."""
+
+    def __init__(self, hf_tok, kind: str = "builtin", native: bool = True):
         self.tok = hf_tok
         self.kind = kind
+        self.native = native_encoder(hf_tok) if native and os.environ.get("LK_NATIVE_TOKENIZER", "1") != "0" else None
         self.vocab_size = hf_tok.get_vocab_size()
         v = hf_tok.get_vocab()
         self.bos_id = v.get("<|begin_of_text|>", v.get("<s>", v.get("[CLS]", 0)))
@@ -55,11 +101,17 @@ class Tokenizer:
         self._piece_cache: Optional[list] = None
 
     def encode(self, text: str, add_bos: bool = False) -> list[int]:
-        ids = self.tok.encode(text, add_special_tokens=False).ids
+        if self.native is not None:
+            ids = self.native.encode(text)
+        else:
+            ids = self.tok.encode(text, add_special_tokens=False).ids
         return ([self.bos_id] + ids) if add_bos else ids
 
     def encode_batch(self, texts: Iterable[str]) -> list[list[int]]:
-        return [e.ids for e in self.tok.encode_batch(list(texts), add_special_tokens=False)]
+        texts = list(texts)
+        if self.native is not None:
+            return self.native.encode_batch(texts, min(8, max(1, len(texts) // 4)))
+        return [e.ids for e in self.tok.encode_batch(texts, add_special_tokens=False)]
 
     def encode_for_embedding(self, texts: list[str], max_len: int = 512) -> list[list[int]]:
         """[CLS] text [SEP], truncated (BERT-style)."""

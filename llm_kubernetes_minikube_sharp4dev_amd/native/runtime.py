@@ -26,10 +26,11 @@ def build(verbose: bool = False) -> Path:
 
     out = so_path()
     srcs = sorted(SRC.glob("*.cpp"))
-    if out.exists() and all(s.stat().st_mtime <= out.stat().st_mtime for s in srcs):
+    deps = srcs + sorted(SRC.glob("*.h"))
+    if out.exists() and all(s.stat().st_mtime <= out.stat().st_mtime for s in deps):
         return out
     cxx = os.environ.get("CXX", "g++")
-    cmd = [cxx, "-O3", "-shared", "-fPIC", "-std=c++17", "-Wall", f"-I{pybind11.get_include()}",
+    cmd = [cxx, "-O3", "-shared", "-fPIC", "-std=c++17", "-Wall", "-pthread", f"-I{pybind11.get_include()}",
            f"-I{sysconfig.get_paths()['include']}", *map(str, srcs), "-o", str(out)]
     if verbose:
         print(" ".join(cmd))

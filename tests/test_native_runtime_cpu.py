@@ -70,3 +70,65 @@ def test_slots_for(native):
     assert list(p) == [14, 15, 16, 17] and list(s) == [2 * 8 + 6, 2 * 8 + 7, 9 * 8 + 0, 9 * 8 + 1]
     with pytest.raises(IndexError):
         m.slots_for([1], 0, 9, 8)
+
+
+# ---------------------------------------------------------------- native BPE encoder
+def _adversarial_texts():
+    import random
+
+    rng = random.Random(0)
+    alpha = list("ab Z09'sStTrRevVlLmMdD \t\n\r\r\n.,;:!?()[]{}<>\"&+-_=*/\\|`~^%$#@") + \
+        ["è", "é", "你", "好", "١", "Ⅷ", " ", " ", "　", "\U0001F600",
+         "́", "²", " ", "<|eot_id|>", "<|begin_of_text|>", "[CLS]"]
+    out = []
+    for _ in range(1500):
+        out.append("".join(rng.choice(alpha) for _ in range(rng.randint(0, 60))))
+    out += ["", " ", "  ", "\n", " \n ", "'s", "'S", "x's", "''s", "   \n\n  x", "a  b   c    ", "1234567 89",
+            "=" * 300, " " * 50 + "x", "\t\tfoo\r\n\r\nbar", "ignore previous instructions"]
+    return out
+
+
+def _corpus_texts():
+    from llm_kubernetes_minikube_sharp4dev_amd.agent.prompts import RAG_AGENT_SYSTEM, json_prompt, rag_agent_input
+    from llm_kubernetes_minikube_sharp4dev_amd.rag.synthetic import make_queries
+    from llm_kubernetes_minikube_sharp4dev_amd.rag.corpus import build_chunks
+
+    chunks = build_chunks(40, 3, workers=1)
+    texts = [c[2] for c in chunks]
+    from llm_kubernetes_minikube_sharp4dev_amd.rag.index import RagHit
+
+    ev = [RagHit(c[0], c[1], c[2], 0.5 + 0.01 * i) for i, c in enumerate(chunks[:6])]
+    texts += [json_prompt(RAG_AGENT_SYSTEM, rag_agent_input(q, ev, 1500)) for q in make_queries(20, seed=1)]
+    return texts
+
+
+def test_native_bpe_matches_hf_builtin():
+    from llm_kubernetes_minikube_sharp4dev_amd.models.tokenizer import builtin_tokenizer
+
+    tok = builtin_tokenizer()
+    assert tok.native is not None, "native encoder should support the built-in byte-level BPE"
+    texts = _corpus_texts() + _adversarial_texts()
+    ref = [e.ids for e in tok.tok.encode_batch(texts, add_special_tokens=False)]
+    assert tok.native.encode_batch(texts, 4) == ref
+    assert [tok.native.encode(t) for t in texts[:200]] == ref[:200]
+
+
+def test_native_bpe_matches_hf_llama3_pretokenizer():
+    """Llama-3 layout: Split(llama-3 regex, isolated) + ByteLevel(no regex), ignore_merges."""
+    from tokenizers import Regex, Tokenizer, decoders, models, pre_tokenizers, trainers
+
+    from llm_kubernetes_minikube_sharp4dev_amd.models.tokenizer import LLAMA3_SPLIT, native_encoder
+
+    hf = Tokenizer(models.BPE(ignore_merges=True))
+    hf.pre_tokenizer = pre_tokenizers.Sequence([
+        pre_tokenizers.Split(Regex(LLAMA3_SPLIT), behavior="isolated", invert=False),
+        pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=False)])
+    hf.decoder = decoders.ByteLevel()
+    trainer = trainers.BpeTrainer(vocab_size=3000, special_tokens=["<|begin_of_text|>", "<|eot_id|>"],
+                                  initial_alphabet=pre_tokenizers.ByteLevel.alphabet(), show_progress=False)
+    texts = _corpus_texts()
+    hf.train_from_iterator(texts * 2, trainer=trainer)
+    enc = native_encoder(hf)
+    assert enc is not None
+    allt = texts + _adversarial_texts()
+    assert enc.encode_batch(allt, 3) == [e.ids for e in hf.encode_batch(allt, add_special_tokens=False)]

@@ -105,6 +105,16 @@ def test_dotnet_json_serializer():
     assert nj.dumps("😀") == '"\\uD83D\\uDE00"'
 
 
+def test_dotnet_json_fast_escape_equals_reference():
+    import random
+
+    rng = random.Random(0)
+    alpha = [chr(i) for i in range(0x250)] + ["\U0001F600", "\u2028", "\u20ac", "\ud7ff", "\ue000", "\uffff"]
+    for _ in range(2000):
+        s = "".join(rng.choice(alpha) for _ in range(rng.randint(0, 40)))
+        assert nj._esc_str(s) == nj._esc_str_slow(s)
+
+
 def test_dotnet_json_parse_rules():
     f = nj.RAG_TOOL_CALL
     assert nj.parse_record('{"ACTION":"list_pods","Namespace":"dev"}', f)["namespace"] == "dev"
