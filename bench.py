@@ -48,7 +48,9 @@ def parse():
     ap.add_argument("--embedder", default="bge-base")
     ap.add_argument("--kv-gb", type=float, default=48.0)
     ap.add_argument("--max-batched-tokens", type=int, default=None,
-                    help="token budget per engine step (default: 8192 continuous, 65536 batch)")
+                    help="token budget per engine step (default: 4096 continuous, 65536 batch)")
+    ap.add_argument("--admit-chunk", type=int, default=8,
+                    help="continuous mode: requests retrieved + admitted together (batched embed/kNN)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
@@ -130,7 +132,9 @@ def main():
     llm = build_decoder(args.model, device=dev, seed=args.seed)
     torch.cuda.synchronize()
     log(rank, f"{args.model} random-init in {time.perf_counter() - t0:.1f}s")
-    mbt = args.max_batched_tokens or (8192 if args.mode == "continuous" else 65536)
+    # continuous: ~4k-token steps keep most steps mixed (decode rows ride on the prefill
+    # GEMMs) without starving decode (profiles/r1_sched_sweep.md)
+    mbt = args.max_batched_tokens or (4096 if args.mode == "continuous" else 65536)
     engine = LLMEngine(llm, tok, block_size=16, max_model_len=8192, max_num_seqs=max(args.batch, 64),
                        max_num_batched_tokens=mbt,
                        enable_prefix_caching=not args.no_prefix_cache, use_graphs=not args.no_graphs,
@@ -157,7 +161,7 @@ def main():
 
         # warm-up fills the pipeline and reaches the steady prefill/decode mix; the timed
         # window continues the same stream (in-flight requests carry over)
-        load = ContinuousLoad(pipe, next_queries, params, args.batch)
+        load = ContinuousLoad(pipe, next_queries, params, args.batch, admit_chunk=args.admit_chunk)
 
         def run_steps(n):
             return load.run(n * args.batch)
@@ -171,6 +175,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    engine.step_trace = []
     t0 = time.perf_counter()
     results = []
     step_times = []
@@ -185,6 +190,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    trace, engine.step_trace = engine.step_trace, None
     if args.mode == "continuous":
         load.drain()
 
@@ -216,6 +222,15 @@ def main():
         statuses = {}
         for r in results:
             statuses[str(r.status)] = statuses.get(str(r.status), 0) + 1
+        dec_only = [t for t in trace if t[0] == 0]
+        mixed = [t for t in trace if t[0] > 0]
+        step_mix = {
+            "steps": len(trace),
+            "decode_only_steps": len(dec_only), "decode_only_s": round(sum(t[2] for t in dec_only), 3),
+            "mixed_steps": len(mixed), "mixed_s": round(sum(t[2] for t in mixed), 3),
+            "avg_prefill_tokens_mixed": round(statistics.mean(t[0] for t in mixed), 1) if mixed else 0,
+            "avg_decode_rows": round(statistics.mean(t[1] for t in trace), 1) if trace else 0,
+        }
         tim = {k: statistics.mean(r.timings.get(k, 0.0) for r in results) for k in ("embed_s", "knn_s", "prompt_s",
                                                                                    "generate_s")}
         out = {
@@ -249,6 +264,8 @@ def main():
                 "hip_graphs": not args.no_graphs,
                 "avg_cached_prefix_tokens": round(statistics.mean(pre), 1) if pre else 0,
                 "stage_means_s": {k: round(v, 4) for k, v in tim.items()},
+                "step_mix_rank0": step_mix,
+                "admit_chunk": args.admit_chunk if args.mode == "continuous" else None,
                 "index_build_s": round(t_index, 2),
                 "http_status_counts": statuses,
             },

@@ -41,6 +41,8 @@ class LLMEngine:
         self.eos_ids = set(eos_ids)
         self.lock = threading.RLock()
         self.steps = 0
+        # optional per-step trace: (prefill tokens, decode rows, wall seconds) -- bench.py
+        self.step_trace: Optional[list] = None
 
     # ------------------------------------------------------------------ API
     def add_request(self, prompt_ids: list, params: Optional[SamplingParams] = None,
@@ -90,6 +92,10 @@ class LLMEngine:
                     self._append(seq, int(tid), now)
                     out.append(seq)
             self.steps += 1
+            if self.step_trace is not None:
+                npre = sum(n for sq, st, n in batch.items if st < len(sq.prompt_ids))
+                self.step_trace.append((npre, len(batch.items) - sum(
+                    1 for sq, st, n in batch.items if st < len(sq.prompt_ids)), time.perf_counter() - t0))
             M.STEP_TOKENS.observe(batch.num_tokens)
             M.STEP_TIME.observe(time.perf_counter() - t0)
             M.KV_USAGE.set(self.allocator.usage())
