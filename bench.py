@@ -3,14 +3,22 @@
 Llama-3-8B (BASELINE.json config 2: bge-base embedder + Llama-3-8B bf16 TP=1 per
 MI355X, 100k-document synthetic corpus).
 
-One rank per GPU (DP replicas, weak scaling: per-GPU batch fixed as N grows).  A
-step = one batch of ``--batch`` concurrent ``/agent_rag`` requests per GPU through
-the full pipeline of ``Minimal_RAG/Program.cs:106-316``:
+One rank per GPU.  Default: DP replicas (TP=1, weak scaling: per-GPU concurrency
+fixed as N grows).  Each request is the full ``/agent_rag`` pipeline of
+``Minimal_RAG/Program.cs:106-316``:
 
   bge-base query embeddings -> cosine top-6 over the HBM-resident corpus (HIP kNN)
   -> citation gating -> evidence JSON prompt -> Llama-3-8B (flash prefill, prefix
   cache, hipGraph decode, greedy, ``--max-new-tokens`` per request) -> JSON
   extraction -> typed tool call -> RAG gating -> (fake) Kubernetes action.
+
+Default load is closed-loop continuous batching (``--batch`` requests in flight per
+replica; a step = ``--batch`` completions per replica).  Other BASELINE configs:
+  --workload agent        Minimal_Agent /agent tool-call loop (config 3)
+  --workload mixed        concurrent agent + RAG sessions on one engine (config 5)
+  --model llama-3-70b --tp 8 --docs 1000000   70B TP=8 over RCCL, 1M-doc kNN (config 4)
+With ``--tp T`` the world is split into TP groups of T ranks: the group's rank 0
+drives the engine (scheduler, retrieval, sampling) and the others follow in lockstep.
 
 Weights are random-init (no checkpoints offline), data synthetic; random weights
 never emit EOS on purpose, so every request generates exactly ``--max-new-tokens``
@@ -31,6 +39,13 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+METRICS = {
+    "rag": "RAG queries/sec (whole node) + p50 end-to-end latency, {model}",
+    "agent": "Agent tool-call requests/sec (whole node) + p50 end-to-end latency, {model}",
+    "mixed": "Mixed agent+RAG requests/sec (whole node) + p50 end-to-end latency, {model}",
+}
+MODEL_NAMES = {"llama-3-8b": "Llama-3-8B", "llama-3-70b": "Llama-3-70B", "opt-125m": "OPT-125m"}
+
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -38,14 +53,16 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=128,
-                    help="requests per GPU per step (= in-flight concurrency in continuous mode)")
+                    help="requests per replica per step (= in-flight concurrency in continuous mode)")
     ap.add_argument("--mode", choices=["continuous", "batch"], default="continuous",
                     help="continuous: closed-loop load, `batch` requests always in flight, a step = `batch` "
                          "completions; batch: a step = one synchronous batch of `batch` requests")
+    ap.add_argument("--workload", choices=sorted(METRICS), default="rag")
     ap.add_argument("--docs", type=int, default=100_000, help="synthetic runbook documents in the knowledge base")
     ap.add_argument("--max-new-tokens", type=int, default=48)
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--embedder", default="bge-base")
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (ranks per replica)")
     ap.add_argument("--kv-gb", type=float, default=48.0)
     ap.add_argument("--max-batched-tokens", type=int, default=None,
                     help="token budget per engine step (default: 4096 continuous, 65536 batch)")
@@ -68,6 +85,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world % args.tp:
+        raise SystemExit(f"--tp {args.tp} must divide the world size {world}")
     t_setup = time.perf_counter()
 
     # ---- corpus chunks (CPU, before any GPU init: the pool forks)
@@ -80,7 +99,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from llm_kubernetes_minikube_sharp4dev_amd.agent.rag_pipeline import RagAgentPipeline
+    from llm_kubernetes_minikube_sharp4dev_amd.agent.agent_pipeline import AgentPipeline, MixedPipeline
+    from llm_kubernetes_minikube_sharp4dev_amd.agent.rag_pipeline import ContinuousLoad, RagAgentPipeline
     from llm_kubernetes_minikube_sharp4dev_amd.config import Config
     from llm_kubernetes_minikube_sharp4dev_amd.engine.embed_engine import EmbeddingEngine
     from llm_kubernetes_minikube_sharp4dev_amd.engine.llm_engine import LLMEngine
@@ -89,6 +109,9 @@ def main():
     from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder, build_encoder
     from llm_kubernetes_minikube_sharp4dev_amd.models.tokenizer import builtin_tokenizer
     from llm_kubernetes_minikube_sharp4dev_amd.ops import _ext
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp import SINGLE, new_tp_groups
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp_engine import (make_tp_engine, run_tp_worker,
+                                                                          shutdown_tp, tp_barrier, tp_capture_all)
     from llm_kubernetes_minikube_sharp4dev_amd.rag.embedder import LocalEmbedder
     from llm_kubernetes_minikube_sharp4dev_amd.rag.index import RagChunk, RagIndex
     from llm_kubernetes_minikube_sharp4dev_amd.rag.synthetic import make_queries
@@ -99,11 +122,15 @@ def main():
     _ext.lib()  # fail loudly if the HIP library is not built
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    tpg = new_tp_groups(args.tp) if args.tp > 1 else SINGLE
+    leader = tpg.rank == 0
+    n_replicas = world // args.tp
 
     cfg = Config()
     tok = builtin_tokenizer()
 
-    # ---- embedder + index build (embedding work sharded over ranks, all-gather over RCCL)
+    # ---- embedder + index build (embedding work sharded over ALL ranks, all-gather over RCCL;
+    # every replica driver then holds the whole corpus in HBM: 1M x 768 bf16 = 1.5 GB)
     enc = build_encoder(args.embedder, device=dev, seed=args.seed)
     emb_engine = EmbeddingEngine(enc, tok, name=args.embedder, max_tokens_per_batch=131072)
     n = len(chunks)
@@ -119,6 +146,7 @@ def main():
     else:
         full = shard
     corpus = full[:n].contiguous()
+    del full, shard, mine
     torch.cuda.synchronize()
     t_index = time.perf_counter() - t0
     index = RagIndex(LocalEmbedder(emb_engine), backend="gpu", device=str(dev))
@@ -129,85 +157,105 @@ def main():
 
     # ---- generator + engine
     t0 = time.perf_counter()
-    llm = build_decoder(args.model, device=dev, seed=args.seed)
+    llm = build_decoder(args.model, device=dev, seed=args.seed, tp=tpg)
     torch.cuda.synchronize()
-    log(rank, f"{args.model} random-init in {time.perf_counter() - t0:.1f}s")
+    log(rank, f"{args.model} random-init (tp={args.tp}) in {time.perf_counter() - t0:.1f}s")
     # continuous: ~4k-token steps keep most steps mixed (decode rows ride on the prefill
     # GEMMs) without starving decode (profiles/r1_sched_sweep.md)
     mbt = args.max_batched_tokens or (4096 if args.mode == "continuous" else 65536)
-    engine = LLMEngine(llm, tok, block_size=16, max_model_len=8192, max_num_seqs=max(args.batch, 64),
-                       max_num_batched_tokens=mbt,
-                       enable_prefix_caching=not args.no_prefix_cache, use_graphs=not args.no_graphs,
-                       kv_cache_gb=args.kv_gb, eos_ids=set())
-    k8s = FakeCluster.default()
-    pipe = RagAgentPipeline(index, engine, tok, k8s, cfg)
+    runner_kw = dict(block_size=16, max_model_len=8192, max_num_seqs=max(args.batch, 64), kv_cache_gb=args.kv_gb,
+                     use_graphs=not args.no_graphs)
+    engine_kw = dict(max_num_batched_tokens=mbt, enable_prefix_caching=not args.no_prefix_cache, eos_ids=set())
     params = SamplingParams.greedy(args.max_new_tokens, ignore_eos=True)
-    if not args.no_graphs:
-        engine.runner.capture_all(max_batch=max(args.batch, 1))
+    results, trace, elapsed, tim_setup = [], [], 0.0, 0.0
 
-    qcount = [0]
-
-    def next_queries(n):
-        qcount[0] += 1
-        return make_queries(n, seed=args.seed * 100003 + rank * 7919 + qcount[0])
-
-    def step(i):
-        if args.mode == "batch":
-            return pipe.run_batch(next_queries(args.batch), params)
-        return pipe.run_continuous(next_queries, params, args.batch, args.batch)
-
-    if args.mode == "continuous":
-        from llm_kubernetes_minikube_sharp4dev_amd.agent.rag_pipeline import ContinuousLoad
-
-        # warm-up fills the pipeline and reaches the steady prefill/decode mix; the timed
-        # window continues the same stream (in-flight requests carry over)
-        load = ContinuousLoad(pipe, next_queries, params, args.batch, admit_chunk=args.admit_chunk)
-
-        def run_steps(n):
-            return load.run(n * args.batch)
-
-        run_steps(max(args.warmup, 1))
+    if not leader:
+        # TP follower: execute the driver's steps (and its barriers) until it says stop
+        run_tp_worker(llm, tpg, **runner_kw)
     else:
-        for w in range(args.warmup):
-            step(-1 - w)
-    log(rank, f"setup {time.perf_counter() - t_setup:.1f}s; timing {args.steps} steps x {args.batch} req/GPU")
+        if args.tp > 1:
+            engine = make_tp_engine(llm, tpg, tok, engine_kw=engine_kw, **runner_kw)
+            if not args.no_graphs:
+                tp_capture_all(engine, max_batch=max(args.batch, 1))
+        else:
+            engine = LLMEngine(llm, tok, **runner_kw, **engine_kw)
+            if not args.no_graphs:
+                engine.runner.capture_all(max_batch=max(args.batch, 1))
+        k8s = FakeCluster.default()
+        rag = RagAgentPipeline(index, engine, tok, k8s, cfg)
+        agent = AgentPipeline(engine, tok, k8s, cfg)
+        pipe = {"rag": rag, "agent": agent, "mixed": MixedPipeline(rag, agent)}[args.workload]
+        replica = rank // args.tp
+        qcount = [0]
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    engine.step_trace = []
-    t0 = time.perf_counter()
-    results = []
-    step_times = []
-    if args.mode == "continuous":
-        results.extend(run_steps(args.steps))
-    else:
-        for i in range(args.steps):
+        def next_queries(k):
+            qcount[0] += 1
+            return make_queries(k, seed=args.seed * 100003 + replica * 7919 + qcount[0])
+
+        def batch_step():
+            reqs, tim = pipe.plan_requests(next_queries(args.batch))
+            todo = {}
+            for i, (p, ids, ctx) in enumerate(reqs):
+                if ids is not None:
+                    todo[i] = engine.add_request(ids, params.__class__(**{**params.__dict__}))
             ts = time.perf_counter()
-            results.extend(step(i))
-            step_times.append(time.perf_counter() - ts)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    trace, engine.step_trace = engine.step_trace, None
-    if args.mode == "continuous":
-        load.drain()
+            engine.run_until_done(list(todo.values()))
+            out = []
+            for i, (p, ids, ctx) in enumerate(reqs):
+                if i not in todo:
+                    out.append(pipe.finish_request(p, [], None))
+                    continue
+                r = pipe.finish_request(p, todo[i].output_ids, ctx)
+                r.prompt_tokens = len(ids)
+                r.timings = {**tim, **todo[i].metrics(), "e2e_s": time.perf_counter() - ts}
+                out.append(r)
+            return out
 
-    lat = [r.timings.get("e2e_s", 0.0) for r in results]
+        load = None
+        if args.mode == "continuous":
+            # warm-up fills the pipeline and reaches the steady prefill/decode mix; the timed
+            # window continues the same stream (in-flight requests carry over)
+            load = ContinuousLoad(pipe, next_queries, params, args.batch, admit_chunk=args.admit_chunk)
+            load.run(max(args.warmup, 1) * args.batch)
+        else:
+            for _ in range(args.warmup):
+                batch_step()
+        tim_setup = time.perf_counter() - t_setup
+        log(rank, f"setup {tim_setup:.1f}s; timing {args.steps} steps x {args.batch} req/replica")
+
+        if world > 1:
+            tp_barrier(engine)
+        torch.cuda.synchronize()
+        engine.step_trace = []
+        t0 = time.perf_counter()
+        if load is not None:
+            results.extend(load.run(args.steps * args.batch))
+        else:
+            for _ in range(args.steps):
+                results.extend(batch_step())
+        torch.cuda.synchronize()
+        if world > 1:
+            tp_barrier(engine)
+        elapsed = time.perf_counter() - t0
+        trace, engine.step_trace = engine.step_trace, None
+        if load is not None:
+            load.drain()
+        if args.tp > 1:
+            shutdown_tp(engine)
+
+    # ---- aggregate (every rank; followers contribute zero requests)
+    lat = [r.timings.get("e2e_s", 0.0) for r in results if r.timings]
     ptok = [r.prompt_tokens for r in results if r.prompt_tokens]
     pre = [r.timings.get("cached_prefix_tokens", 0) for r in results if r.timings]
-    gen = [r.output_tokens for r in results]
-    stats = torch.tensor([elapsed, float(len(results)), float(sum(ptok)), float(len(ptok)), float(sum(gen))],
+    stats = torch.tensor([elapsed, float(len(results)), float(sum(ptok)), float(len(ptok))],
                          dtype=torch.float64, device=dev)
-    lat_t = torch.tensor(lat, dtype=torch.float64, device=dev)
     if world > 1:
         allst = [torch.zeros_like(stats) for _ in range(world)]
         dist.all_gather(allst, stats)
-        alll = [torch.zeros_like(lat_t) for _ in range(world)]
-        dist.all_gather(alll, lat_t)
         allst = torch.stack(allst).cpu()
-        lat_all = torch.cat(alll).cpu().tolist()
+        objs = [None] * world
+        dist.all_gather_object(objs, lat)
+        lat_all = [x for o in objs for x in o]
     else:
         allst = stats[None].cpu()
         lat_all = lat
@@ -231,12 +279,13 @@ def main():
             "avg_prefill_tokens_mixed": round(statistics.mean(t[0] for t in mixed), 1) if mixed else 0,
             "avg_decode_rows": round(statistics.mean(t[1] for t in trace), 1) if trace else 0,
         }
-        tim = {k: statistics.mean(r.timings.get(k, 0.0) for r in results) for k in ("embed_s", "knn_s", "prompt_s",
-                                                                                   "generate_s")}
+        tim = {k: statistics.mean(r.timings.get(k, 0.0) for r in results if r.timings)
+               for k in ("embed_s", "knn_s", "prompt_s")} if results else {}
+        par = f"dp{n_replicas}" if args.tp == 1 else f"tp{args.tp}" + (f"xdp{n_replicas}" if n_replicas > 1 else "")
         out = {
-            "metric": "RAG queries/sec (whole node) + p50 end-to-end latency, Llama-3-8B",
+            "metric": METRICS[args.workload].format(model=MODEL_NAMES.get(args.model, args.model)),
             "value": round(qps, 3),
-            "unit": "queries/s",
+            "unit": "queries/s" if args.workload == "rag" else "requests/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -249,14 +298,16 @@ def main():
             "p50_latency_ms": round(p50, 1) if p50 is not None else None,
             "p90_latency_ms": round(p90, 1) if p90 is not None else None,
             "config": {
-                "model": f"{args.model} (bf16, TP=1) + {args.embedder} embedder",
-                "global_batch": args.batch * world,
+                "model": f"{args.model} (bf16, TP={args.tp}) + {args.embedder} embedder",
+                "workload": args.workload,
+                "global_batch": args.batch * n_replicas,
                 "seq_len": round(avg_prompt, 1),
-                "parallelism": f"dp{world}",
-                "load": (f"continuous batching, closed loop, {args.batch} requests in flight per GPU, "
-                         f"step = {args.batch} completions" if args.mode == "continuous"
+                "parallelism": par,
+                "load": (f"continuous batching, closed loop, {args.batch} requests in flight per replica, "
+                         f"step = {args.batch} completions per replica" if args.mode == "continuous"
                          else f"synchronous batches of {args.batch}"),
                 "max_batched_tokens": mbt,
+                "admit_chunk": args.admit_chunk if args.mode == "continuous" else None,
                 "corpus_chunks": n,
                 "max_new_tokens": args.max_new_tokens,
                 "decoding": "greedy, ignore_eos",
@@ -265,9 +316,9 @@ def main():
                 "avg_cached_prefix_tokens": round(statistics.mean(pre), 1) if pre else 0,
                 "stage_means_s": {k: round(v, 4) for k, v in tim.items()},
                 "step_mix_rank0": step_mix,
-                "admit_chunk": args.admit_chunk if args.mode == "continuous" else None,
                 "index_build_s": round(t_index, 2),
-                "http_status_counts": statuses,
+                "setup_s": round(tim_setup, 1),
+                "http_status_counts_rank0": statuses,
             },
         }
         line = json.dumps(out)

@@ -76,6 +76,17 @@ class RagAgentPipeline:
         t3 = time.perf_counter()
         return out, {"embed_s": t1 - t0, "knn_s": t2 - t1, "prompt_s": t3 - t2}
 
+    # ---- request-level interface used by ContinuousLoad (shared with AgentPipeline)
+    def plan_requests(self, prompts: list[str]):
+        """[(prompt, token ids or None (no evidence -> answered without the LLM), ctx)], timings"""
+        plans, tim = self.plan(prompts)
+        return [(p, ids, (cit, ev)) for p, ids, cit, ev in plans], tim
+
+    def finish_request(self, prompt: str, out_ids: list, ctx) -> RagAgentResult:
+        if ctx is None:
+            return RagAgentResult(prompt, 200, {"result": None, "citations": [], "note": NO_EVIDENCE_NOTE})
+        return self.finish(prompt, out_ids, *ctx)
+
     def finish(self, prompt: str, out_ids: list, citations, evidence) -> RagAgentResult:
         raw = self.tok.decode(out_ids)
         tool_json = extract_json_object(raw)
@@ -136,18 +147,18 @@ class ContinuousLoad:
             if free >= min(self.admit_chunk, self.concurrency) or not self.inflight:
                 qs = self.next_queries(free)
                 t_adm = time.perf_counter()
-                plans, tim = pipe.plan(qs)
-                for p, ids, cit, ev in plans:
+                reqs, tim = pipe.plan_requests(qs)
+                for p, ids, ctx in reqs:
                     if ids is None:
-                        done.append(RagAgentResult(p, 200, {"result": None, "citations": [], "note": NO_EVIDENCE_NOTE}))
+                        done.append(pipe.finish_request(p, [], None))
                         continue
                     seq = pipe.llm.add_request(ids, self.params.__class__(**{**self.params.__dict__}))
                     seq.arrival = t_adm
-                    self.inflight[seq.req_id] = (seq, p, ids, cit, ev, tim)
+                    self.inflight[seq.req_id] = (seq, p, ids, ctx, tim)
             pipe.llm.step()
             for rid in [r for r, v in self.inflight.items() if v[0].finished]:
-                seq, p, ids, cit, ev, tim = self.inflight.pop(rid)
-                r = pipe.finish(p, seq.output_ids, cit, ev)
+                seq, p, ids, ctx, tim = self.inflight.pop(rid)
+                r = pipe.finish_request(p, seq.output_ids, ctx)
                 r.prompt_tokens = len(ids)
                 r.timings = {**tim, **seq.metrics(), "e2e_s": time.perf_counter() - seq.arrival}
                 done.append(r)

@@ -22,6 +22,10 @@ class TPGroup:
     rank: int = 0
     size: int = 1
     group: Optional[object] = None
+    # CPU (gloo) control group of the same ranks + their global ranks; created on ALL
+    # ranks by new_tp_groups (torch requires every rank to join every new_group call)
+    ctrl: Optional[object] = None
+    ranks: Optional[list] = None
 
     @property
     def enabled(self) -> bool:
@@ -67,8 +71,11 @@ def init_distributed(backend: Optional[str] = None) -> TPGroup:
     return TPGroup(dist.get_rank(), dist.get_world_size(), dist.group.WORLD)
 
 
-def new_tp_groups(tp_size: int) -> TPGroup:
-    """Split the world into contiguous TP groups of ``tp_size`` (DP across groups)."""
+def new_tp_groups(tp_size: int, with_ctrl: bool = True) -> TPGroup:
+    """Split the world into contiguous TP groups of ``tp_size`` (DP across groups).
+    Every rank creates every group (device group on the default backend -- RCCL on the
+    GPU -- and, with ``with_ctrl``, a gloo control group for the TP engine's step
+    broadcasts) in the same order."""
     ws, rank = dist.get_world_size(), dist.get_rank()
     if ws % tp_size:
         raise ValueError("world size must be a multiple of tp size")
@@ -76,6 +83,7 @@ def new_tp_groups(tp_size: int) -> TPGroup:
     for g in range(ws // tp_size):
         ranks = list(range(g * tp_size, (g + 1) * tp_size))
         grp = dist.new_group(ranks)
+        ctrl = dist.new_group(ranks, backend="gloo") if with_ctrl and tp_size > 1 else None
         if rank in ranks:
-            mine = TPGroup(ranks.index(rank), tp_size, grp)
+            mine = TPGroup(ranks.index(rank), tp_size, grp, ctrl, ranks)
     return mine

@@ -32,7 +32,9 @@ log = get_logger("tp")
 class _Ctrl:
     def __init__(self, tp: TPGroup):
         self.tp = tp
-        if tp.size > 1:
+        if tp.size > 1 and tp.ctrl is not None:
+            self.group, self.src = tp.ctrl, tp.ranks[0]
+        elif tp.size > 1:
             ranks = dist.get_process_group_ranks(tp.group) if tp.group is not None else list(range(tp.size))
             self.group = dist.new_group(ranks, backend="gloo")
             self.src = ranks[0]
@@ -96,6 +98,17 @@ def shutdown_tp(engine):
     engine.tp_ctrl.bcast(("stop", None))
 
 
+def tp_barrier(engine):
+    """World barrier (after a device sync) from the TP driver while its workers sit in
+    run_tp_worker: they receive a "barrier" command and join the same barrier."""
+    ctrl = getattr(engine, "tp_ctrl", None)
+    if ctrl is not None:
+        ctrl.bcast(("barrier", None))
+    if torch.cuda.is_available() and engine.model.device.type == "cuda":
+        torch.cuda.synchronize()
+    dist.barrier()
+
+
 @torch.inference_mode()
 def run_tp_worker(model, tp: TPGroup, **runner_kw):
     """Ranks > 0: execute whatever rank 0 schedules until it says stop."""
@@ -107,6 +120,10 @@ def run_tp_worker(model, tp: TPGroup, **runner_kw):
             break
         if cmd == "capture":
             runner.capture(arg)
+        elif cmd == "barrier":
+            if torch.cuda.is_available() and model.device.type == "cuda":
+                torch.cuda.synchronize()
+            dist.barrier()
         elif cmd == "step":
             runner.execute(arg)
             n += 1

@@ -140,3 +140,51 @@ def test_router_balances_two_replicas():
     b.inflight += 1
     pool.mark_failed(a)
     assert pool.pick().url == b.url
+
+
+def _tp_dp_worker(rank, world, port, out_path):
+    """world 4 = 2 replicas x TP 2: the bench.py protocol (leaders drive, followers run
+    run_tp_worker and join the driver's world barriers through the control group)."""
+    _init(rank, world, port)
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import SamplingParams
+    from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp import new_tp_groups
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp_engine import (make_tp_engine, run_tp_worker, shutdown_tp,
+                                                                          tp_barrier)
+
+    tpg = new_tp_groups(2)
+    m = build_decoder(_ours_cfg("llama"), dtype=torch.float32, tp=tpg)
+    m.load_hf_state_dict(_hf("llama").state_dict())
+    kw = dict(block_size=16, max_model_len=512, max_num_seqs=8, num_blocks=96)
+    got = None
+    if tpg.rank == 0:
+        eng = make_tp_engine(m, tpg, None, engine_kw={"eos_ids": set(), "max_num_batched_tokens": 40}, **kw)
+        tp_barrier(eng)
+        prompts = PROMPTS if rank == 0 else PROMPTS[::-1]
+        got = [s.output_ids for s in eng.generate(prompts, SamplingParams.greedy(6))]
+        tp_barrier(eng)
+        shutdown_tp(eng)
+    else:
+        run_tp_worker(m, tpg, **kw)
+    objs = [None] * world
+    dist.all_gather_object(objs, got)
+    if rank == 0:
+        torch.save(objs, out_path)
+    dist.destroy_process_group()
+
+
+def test_tp2_dp2_driver_worker_barrier_protocol():
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.llm_engine import LLMEngine
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import SamplingParams
+    from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder
+
+    m = build_decoder(_ours_cfg("llama"), dtype=torch.float32)
+    m.load_hf_state_dict(_hf("llama").state_dict())
+    eng = LLMEngine(m, None, max_model_len=512, max_num_seqs=8, num_blocks=96, eos_ids=set())
+    ref = [s.output_ids for s in eng.generate(PROMPTS, SamplingParams.greedy(6))]
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "out.pt")
+        mp.spawn(_tp_dp_worker, args=(4, _free_port(), out), nprocs=4, join=True)
+        objs = torch.load(out, weights_only=True)
+    assert objs[1] is None and objs[3] is None
+    assert objs[0] == ref and objs[2] == ref[::-1]

@@ -232,3 +232,55 @@ def test_dispatch_agent_tool():
     assert (st, b) == (400, {"error": "Azione non supportata"})
     with pytest.raises(UnhandledK8sError):
         dispatch_agent_tool(k8s, '{"action":"get_logs","namespace":"dev","pod":"missing"}', cfg)
+
+
+def _tiny_stack():
+    import numpy as np
+    import torch
+
+    from llm_kubernetes_minikube_sharp4dev_amd.config import Config
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.llm_engine import LLMEngine
+    from llm_kubernetes_minikube_sharp4dev_amd.k8s.fake import FakeCluster
+    from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder
+    from llm_kubernetes_minikube_sharp4dev_amd.models.tokenizer import builtin_tokenizer
+    from llm_kubernetes_minikube_sharp4dev_amd.rag.corpus import build_chunks
+    from llm_kubernetes_minikube_sharp4dev_amd.rag.embedder import HashEmbedder
+    from llm_kubernetes_minikube_sharp4dev_amd.rag.index import RagIndex
+
+    tok = builtin_tokenizer()
+    chunks = build_chunks(30, 0, workers=1)
+    idx = RagIndex(HashEmbedder(64), backend="exact")
+    idx.add([c[0] for c in chunks], [c[1] for c in chunks], [c[2] for c in chunks],
+            np.asarray(idx.embedder.embed([c[2] for c in chunks])))
+    llm = build_decoder("llama-tiny", dtype=torch.float32, seed=0)
+    eng = LLMEngine(llm, tok, max_model_len=4096, max_num_seqs=8, num_blocks=1200, max_num_batched_tokens=2048,
+                    use_graphs=False, eos_ids=set())
+    return tok, idx, eng, FakeCluster.default(), Config()
+
+
+def test_continuous_load_rag_agent_mixed():
+    """Closed-loop continuous batching over the three workloads of bench.py (configs 2/3/5)."""
+    from llm_kubernetes_minikube_sharp4dev_amd.agent.agent_pipeline import AgentPipeline, MixedPipeline
+    from llm_kubernetes_minikube_sharp4dev_amd.agent.rag_pipeline import ContinuousLoad, RagAgentPipeline
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import SamplingParams
+    from llm_kubernetes_minikube_sharp4dev_amd.rag.synthetic import make_queries
+
+    tok, idx, eng, k8s, cfg = _tiny_stack()
+    rag = RagAgentPipeline(idx, eng, tok, k8s, cfg)
+    agent = AgentPipeline(eng, tok, k8s, cfg)
+    counter = [0]
+
+    def nq(k):
+        counter[0] += 1
+        return make_queries(k, seed=counter[0])
+
+    params = SamplingParams.greedy(4, ignore_eos=True)
+    for pipe in (rag, agent, MixedPipeline(rag, agent)):
+        load = ContinuousLoad(pipe, nq, params, concurrency=4, admit_chunk=2)
+        out = load.run(6)
+        out += load.run(3)  # continues the same stream
+        load.drain()
+        assert len(out) >= 9
+        assert all(r.status in (200, 400, 404, 500) for r in out)
+        assert all(r.output_tokens in (0, 4) for r in out)
+        assert not eng.has_work()
