@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 kernel trace (run_kernel_trace.csv) over the last WINDOW
+seconds (the timed region of bench.py) as a markdown table: per-kernel time share,
+call count, mean duration, GPU busy fraction and the idle-gap histogram.
+
+    python scripts/summarize_trace.py gpurun_out/prof_c128/run_kernel_trace.csv 4.0 > profiles/x.md
+"""
+import collections
+import csv
+import sys
+
+
+def main(path, window_s, top=25):
+    rows = list(csv.DictReader(open(path)))
+    end = max(int(r["End_Timestamp"]) for r in rows)
+    t0 = end - window_s * 1e9
+    agg = collections.defaultdict(lambda: [0, 0])
+    ev = []
+    for r in rows:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if s < t0:
+            continue
+        ev.append((s, e))
+        a = agg[r["Kernel_Name"].replace("(anonymous namespace)", "anon").split("(")[0][:100]]
+        a[0] += e - s
+        a[1] += 1
+    ev.sort()
+    busy, gaps = 0, []
+    cs, ce = ev[0]
+    for s, e in ev[1:]:
+        if s > ce:
+            busy += ce - cs
+            gaps.append(s - ce)
+            cs, ce = s, e
+        else:
+            ce = max(ce, e)
+    busy += ce - cs
+    tot = sum(v[0] for v in agg.values())
+    print(f"Window: last {window_s:.1f} s of the trace; GPU busy {busy / 1e6:.0f} ms "
+          f"({100 * busy / (window_s * 1e9):.1f} %), {len(ev)} kernels\n")
+    print("| kernel | total ms | share | calls | mean us |\n|---|---|---|---|---|")
+    for k, (t, n) in sorted(agg.items(), key=lambda x: -x[1][0])[:top]:
+        print(f"| `{k}` | {t / 1e6:.1f} | {100 * t / tot:.1f} % | {n} | {t / n / 1e3:.1f} |")
+    b = collections.Counter()
+    bt = collections.Counter()
+    for g in gaps:
+        k = "<5us" if g < 5e3 else "5-20us" if g < 2e4 else "20-100us" if g < 1e5 else "0.1-1ms" if g < 1e6 else ">1ms"
+        b[k] += 1
+        bt[k] += g
+    print("\n| idle gap | count | total ms |\n|---|---|---|")
+    for k in ["<5us", "5-20us", "20-100us", "0.1-1ms", ">1ms"]:
+        print(f"| {k} | {b[k]} | {bt[k] / 1e6:.1f} |")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else 4.0)
