@@ -136,6 +136,56 @@ def case_skinny(M, N, K, swiglu=False):
             "us": t * 1e6, "GB/s": byts / t / 1e9, "hipblaslt_us": tb * 1e6, "speedup": tb / t}
 
 
+def case_ws(M, N, K, swiglu=False):
+    """LDS-DMA weight-streaming GEMM vs the fragment-load skinny kernel vs hipBLASLt."""
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+    L = ops.lib()
+    t = timeit(lambda: L.ws_linear(a, b, swiglu))
+    tsk = timeit(lambda: L.skinny_linear(a, b, swiglu))
+    if swiglu:
+        tb = timeit(lambda: ops.silu_mul(torch.nn.functional.linear(a, b)))
+    else:
+        tb = timeit(lambda: torch.nn.functional.linear(a, b))
+    byts = (N * K + M * K + M * N) * 2
+    bn, S = L.ws_plan(M, N, K, swiglu)
+    return {"case": f"ws{'+swiglu' if swiglu else ''} M{M} N{N} K{K} BN{bn} S{S}", "us": t * 1e6,
+            "GB/s": byts / t / 1e9, "TFLOP/s": 2 * M * N * K / t / 1e12, "skinny_us": tsk * 1e6,
+            "hipblaslt_us": tb * 1e6, "speedup": tb / t}
+
+
+def case_ws_sweep():
+    """Every (BN, split) plan of the weight-streaming GEMM per shape: the data the
+    planner (lk_wsgemm_plan) is calibrated on."""
+    L = ops.lib()
+    rows = []
+    shapes = LLAMA8B_SHAPES + [(10240, 8192), (8192, 8192), (57344, 8192), (8192, 28672)]
+    for M in (64, 128, 192, 256):
+        for N, K in shapes:
+            sw = N in (28672, 57344)
+            a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+            b = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+            res = {}
+            for bn in (64, 128):
+                per = bn // 2 if sw else bn
+                if (N // 2 if sw else N) % per:
+                    continue
+                for S in (1, 2, 4, 8):
+                    if K % (S * 64) or K // S < 256:
+                        continue
+                    res[(bn, S)] = timeit(lambda: L.ws_linear(a, b, sw, bn, S), iters=10, warmup=2)
+            tb = timeit(lambda: (ops.silu_mul(torch.nn.functional.linear(a, b)) if sw
+                                 else torch.nn.functional.linear(a, b)), iters=10, warmup=2)
+            best = min(res, key=res.get)
+            plan = tuple(L.ws_plan(M, N, K, sw))
+            rows.append({"case": f"ws-sweep M{M} N{N} K{K}{' swiglu' if sw else ''}",
+                         "us": res[best] * 1e6, "best": f"BN{best[0]} S{best[1]}",
+                         "plan": f"BN{plan[0]} S{plan[1]} {res.get(plan, float('nan')) * 1e6:.1f}us",
+                         "all": {f"{k[0]}/{k[1]}": round(v * 1e6, 1) for k, v in res.items()},
+                         "hipblaslt_us": tb * 1e6, "speedup": tb / res[best]})
+    return rows
+
+
 LLAMA8B_SHAPES = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]
 
 
@@ -149,6 +199,10 @@ CASES = {
                      case_gemm(32768, 6144, 4096), case_gemm(32768, 28672, 4096), case_gemm(32768, 4096, 14336)],
     "skinny": lambda: [case_skinny(M, N, K, N == 28672) for M in (1, 16, 32, 64, 128, 256)
                        for (N, K) in LLAMA8B_SHAPES + [(128256, 4096)]],
+    "ws": lambda: [case_ws(M, N, K, N in (28672, 57344)) for M in (64, 128, 192, 256)
+                   for (N, K) in LLAMA8B_SHAPES + [(128256, 4096), (10240, 8192), (8192, 8192), (57344, 8192),
+                                                   (8192, 28672)]],
+    "ws_sweep": lambda: case_ws_sweep(),
     "gemm_sweep": lambda: [case_gemm(M, N, K, lay) for M in (128, 256, 1024, 4096, 8192, 16384)
                            for (N, K) in LLAMA8B_SHAPES for lay in ("NT", "NN")],
 }
@@ -167,10 +221,11 @@ def main():
             rows.append(r)
     if a.md:
         with open(a.md, "w") as f:
-            f.write("| case | us | GB/s | TFLOP/s | hipBLASLt us | speedup |\n|---|---|---|---|---|---|\n")
+            f.write("| case | us | GB/s | TFLOP/s | skinny us | hipBLASLt us | speedup vs hipBLASLt |\n"
+                    "|---|---|---|---|---|---|---|\n")
             for r in rows:
                 f.write(f"| {r['case']} | {r['us']} | {r.get('GB/s', '')} | {r.get('TFLOP/s', '')} "
-                        f"| {r.get('hipblaslt_us', '')} | {r.get('speedup', '')} |\n")
+                        f"| {r.get('skinny_us', '')} | {r.get('hipblaslt_us', '')} | {r.get('speedup', '')} |\n")
 
 
 if __name__ == "__main__":

@@ -133,6 +133,39 @@ at::Tensor skinny_linear(const at::Tensor& x, const at::Tensor& w, bool swiglu, 
   return out;
 }
 
+// Weight-streaming GEMM for 64 < M <= 256 (LDS-DMA staged, csrc/skinny_gemm.hip wsgemm)
+at::Tensor ws_linear(const at::Tensor& x, const at::Tensor& w, bool swiglu, int64_t bn, int64_t splits,
+                     const c10::optional<at::Tensor>& out_) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_LASTDIM(x); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "x [M,K], w [N,K]");
+  check_rows16(x, "x"); check_rows16(w, "w");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(M >= 1 && M <= 256, "ws_linear: M must be in [1, 256]");
+  const int n_out = swiglu ? N / 2 : N;
+  at::Tensor out = out_ ? *out_ : at::empty({M, n_out}, x.options());
+  CHECK_BF16(out); CHECK_LASTDIM(out);
+  TORCH_CHECK(out.size(0) == M && out.size(1) == n_out, "out shape");
+  int BN = (int)bn, S = (int)splits;
+  if (BN <= 0 || S <= 0) {
+    int pb = 64, ps = 1;
+    lk_wsgemm_plan(M, N, K, swiglu ? 1 : 0, &pb, &ps);
+    if (BN <= 0) BN = pb;
+    if (S <= 0) S = ps;
+  }
+  at::Tensor part;
+  if (S > 1) part = at::empty({(long)S * M * N}, x.options().dtype(at::kFloat));
+  int rc = lk_wsgemm(bp(x), x.stride(0), bp(w), M, N, K, BN, S, swiglu ? 1 : 0, bp(out), out.stride(0),
+                     S > 1 ? part.data_ptr<float>() : nullptr, cur_stream());
+  CHECK_RC(rc, "ws_linear");
+  return out;
+}
+
+std::vector<int64_t> ws_plan(int64_t M, int64_t N, int64_t K, bool swiglu) {
+  int bn = 64, s = 1;
+  lk_wsgemm_plan((int)M, (int)N, (int)K, swiglu ? 1 : 0, &bn, &s);
+  return {bn, s};
+}
+
 int64_t skinny_splits(int64_t M, int64_t N, int64_t K, bool swiglu) {
   return lk_skinny_splits((int)M, (int)N, (int)K, swiglu ? 1 : 0);
 }
@@ -355,6 +388,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("skinny_linear", &skinny_linear, "", py::arg("x"), py::arg("w"), py::arg("swiglu") = false,
         py::arg("splits") = 0, py::arg("out") = py::none());
   m.def("skinny_splits", &skinny_splits);
+  m.def("ws_linear", &ws_linear, "", py::arg("x"), py::arg("w"), py::arg("swiglu") = false, py::arg("bn") = 0,
+        py::arg("splits") = 0, py::arg("out") = py::none());
+  m.def("ws_plan", &ws_plan);
   m.def("silu_mul", &silu_mul, "", py::arg("x"), py::arg("out") = py::none());
   m.def("activation_", &activation_);
   m.def("rope_kv_", &rope_kv_);

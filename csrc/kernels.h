@@ -27,6 +27,10 @@ int lk_skinny_splits(int M, int N, int K, int swiglu);
 int lk_skinny_gemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int S, int swiglu,
                    bf16_t* out, long ldo, float* part, hipStream_t st);
 
+void lk_wsgemm_plan(int M, int N, int K, int swiglu, int* bn_out, int* s_out);
+int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, int swiglu,
+              bf16_t* out, long ldo, float* part, hipStream_t st);
+
 // rope_kv.hip
 int lk_rope_kv(bf16_t* qkv, long qs, const int* positions, const float* cos_sin, long T, int Hq,
                int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,

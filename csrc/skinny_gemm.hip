@@ -25,6 +25,8 @@
 // SwiGLU fusion: block t owns gate columns [t*BN/2, (t+1)*BN/2) and the matching
 // up columns I + [...]; out[m][j] = bf16(silu(bf16(g)) ) * bf16(u), rounded like
 // the unfused linear -> silu_mul path (bit-identical to it).
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -207,6 +209,207 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Weight-streaming GEMM for 64 < M <= 256 rows ("wsgemm").  The fragment-shaped loads
+// of skinny_gemm_kernel touch 16 rows x 64 B per wave instruction, which caps the
+// per-CU load rate once X (re-read by every column block) grows with M.  Here both
+// operands are staged through LDS with 16-B global_load_lds (LDS-DMA): every wave
+// instruction moves 8 rows x one full 128-B line, lane-linear into LDS, with the
+// (row>>1)&7 XOR chunk swizzle applied on the SOURCE address so the MFMA fragment
+// reads (ds_read_b128, 16 rows x 16 B per lane group) are bank-conflict free.
+//   * block = 4 waves, tile = all M rows (16*MT) x BN columns, BK = 64 per stage,
+//     3-stage LDS ring, ONE raw s_barrier per stage, counted vmcnt (the DMA of the
+//     next stage stays in flight across the barrier and under the MFMAs);
+//   * waves split M (each 4*MT rows x BN columns: acc = MT/4 x BN/16 tiles);
+//   * W rows are streamed once with the non-temporal policy (aux = 2);
+//   * split-K over blocks (S) when N/BN leaves CUs idle; partial slabs -> the same
+//     reduce / SwiGLU kernel as skinny_gemm; S = 1 writes bf16 (or SwiGLU) directly.
+template <int N>
+LK_DEVICE void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+typedef const __attribute__((address_space(1))) void* gbl_void_ptr;
+
+LK_DEVICE int wsz(int row) { return (row >> 1) & 7; }
+
+// ring depth: the in-flight DMA bytes per CU set the per-CU load rate (latency-bound
+// at one block per CU), so fill the 160 KB LDS
+constexpr int ws_stages(int MT, int BN) {
+  const int sb = (16 * MT + BN) * 128;
+  const int n = 163840 / sb;
+  return n > 8 ? 8 : (n < 3 ? 3 : n);
+}
+
+template <int L, int NS>
+LK_DEVICE void wait_ahead(int ahead) {  // vmcnt(ahead * L), ahead in [0, NS-2]
+  if constexpr (NS > 2) {
+    if (ahead >= NS - 2) {
+      wait_vmcnt<L * (NS - 2)>();
+      return;
+    }
+    wait_ahead<L, NS - 1>(ahead);
+  } else {
+    wait_vmcnt<0>();
+  }
+}
+
+template <int MT, int BN, bool SWIGLU>
+__global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict__ X, long ldx,
+                                                        const bf16_t* __restrict__ W, int M, int K, int ks,
+                                                        int n_tiles, int swiglu_I, bf16_t* __restrict__ out,
+                                                        long ldo, float* __restrict__ part, long part_ld) {
+  constexpr int ROWS = 16 * MT;          // padded M
+  constexpr int MTW = MT / 4;            // row tiles per wave
+  constexpr int NT = BN / 16;            // column tiles per wave
+  constexpr int XB = ROWS * 128;         // X stage bytes
+  constexpr int WB = BN * 128;           // W stage bytes
+  constexpr int SB = XB + WB;            // stage bytes
+  constexpr int NS = ws_stages(MT, BN);  // ring depth: as many stages as 160 KB of LDS holds
+  constexpr int LX = ROWS / 32;          // X glds per wave per stage (8 rows each, 4 waves)
+  constexpr int LW = BN / 32;            // W glds per wave per stage
+  constexpr int L = LX + LW;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int t = blockIdx.x % n_tiles, s = blockIdx.x / n_tiles;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const long kbase = (long)s * ks;
+  const int nst = ks / 64;
+
+  auto wrow = [&](int row) -> long {  // tile row -> global W row (output column)
+    if constexpr (SWIGLU) {
+      return row < BN / 2 ? (long)t * (BN / 2) + row : (long)swiglu_I + (long)t * (BN / 2) + row - BN / 2;
+    } else {
+      return (long)t * BN + row;
+    }
+  };
+
+  // per-lane source pointers of this wave's glds instructions (k offset added per stage)
+  const bf16_t* xsrc[LX];
+  const bf16_t* wsrc[LW];
+  const int lrow = lane >> 3, lch = lane & 7;
+#pragma unroll
+  for (int i = 0; i < LX; ++i) {
+    const int row = (w * LX + i) * 8 + lrow;
+    xsrc[i] = X + (long)min(row, M - 1) * ldx + kbase + ((lch ^ wsz(row)) * 8);
+  }
+#pragma unroll
+  for (int i = 0; i < LW; ++i) {
+    const int row = (w * LW + i) * 8 + lrow;
+    wsrc[i] = W + wrow(row) * K + kbase + ((lch ^ wsz(row)) * 8);
+  }
+  auto issue = [&](int st) {
+    unsigned char* base = smem + (st % NS) * SB;
+    const int k = st * 64;
+#pragma unroll
+    for (int i = 0; i < LX; ++i)
+      __builtin_amdgcn_global_load_lds((gbl_void_ptr)(xsrc[i] + k),
+                                       (lds_void_ptr)(base + (w * LX + i) * 8 * 128), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < LW; ++i)
+      __builtin_amdgcn_global_load_lds((gbl_void_ptr)(wsrc[i] + k),
+                                       (lds_void_ptr)(base + XB + (w * LW + i) * 8 * 128), 16, 0, 2);
+  };
+
+  floatx4 acc[MTW][NT];
+#pragma unroll
+  for (int m = 0; m < MTW; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int st) {
+    const unsigned char* base = smem + (st % NS) * SB;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = 4 * h + g;
+      short8 a[MTW], b[NT];
+#pragma unroll
+      for (int m = 0; m < MTW; ++m) {
+        const int row = w * (4 * MT) + 16 * m + r;
+        a[m] = *reinterpret_cast<const short8*>(base + row * 128 + ((c ^ wsz(row)) << 4));
+      }
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const int row = 16 * n + r;
+        b[n] = *reinterpret_cast<const short8*>(base + XB + row * 128 + ((c ^ wsz(row)) << 4));
+      }
+#pragma unroll
+      for (int m = 0; m < MTW; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], b[n], acc[m][n], 0, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nst) issue(p);
+  for (int st = 0; st < nst; ++st) {
+    // stage st landed (this wave's DMAs); later stages may stay in flight
+    wait_ahead<L, NS>(min(NS - 2, nst - 1 - st));
+    __builtin_amdgcn_s_barrier();  // ... for every wave; and buffer (st-1)%NS is free
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + NS - 1 < nst) issue(st + NS - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(st);
+  }
+
+  // ---- epilogue straight from the accumulators: lane holds rows 4g+i, column r of each tile
+  const bool split = part != nullptr;
+#pragma unroll
+  for (int m = 0; m < MTW; ++m) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = w * (4 * MT) + 16 * m + 4 * g + i;
+      if (row >= M) continue;
+      if (SWIGLU && !split) {
+#pragma unroll
+        for (int n = 0; n < NT / 2; ++n) {
+          const float y = rbf(silu_f(rbf(acc[m][n][i]))) * rbf(acc[m][n + NT / 2][i]);
+          out[(long)row * ldo + (long)t * (BN / 2) + 16 * n + r] = f2bf(y);
+        }
+      } else if (split) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+          part[(long)s * M * part_ld + (long)row * part_ld + wrow(16 * n + r)] = acc[m][n][i];
+      } else {
+#pragma unroll
+        for (int n = 0; n < NT; ++n) out[(long)row * ldo + (long)t * BN + 16 * n + r] = f2bf(acc[m][n][i]);
+      }
+    }
+  }
+}
+
+template <int MT, int BN, bool SWIGLU>
+void launch_ws(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks, int S, int n_tiles, int I,
+               bf16_t* out, long ldo, float* part, long part_ld, hipStream_t st) {
+  constexpr size_t lds = (size_t)ws_stages(MT, BN) * (16 * MT * 128 + BN * 128);
+  auto kern = wsgemm_kernel<MT, BN, SWIGLU>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    attr = true;
+  }
+  kern<<<n_tiles * S, 256, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld);
+}
+
+template <bool SWIGLU>
+int dispatch_ws(int MT, int BN, const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks, int S,
+                int n_tiles, int I, bf16_t* out, long ldo, float* part, long part_ld, hipStream_t st) {
+#define LK_WS(mt, bn)                                                                               \
+  if (MT == mt && BN == bn) {                                                                       \
+    launch_ws<mt, bn, SWIGLU>(x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, part, part_ld, st);     \
+    return 0;                                                                                       \
+  }
+  LK_WS(4, 64) LK_WS(4, 128) LK_WS(8, 64) LK_WS(8, 128) LK_WS(16, 64) LK_WS(16, 128)
+#undef LK_WS
+  return -2;
+}
+
 template <int MT, int NTW, bool SWIGLU>
 void launch_skinny(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks, int S, int n_tiles,
                    int I, bf16_t* out, long ldo, float* part, long part_ld, hipStream_t st) {
@@ -235,6 +438,63 @@ int dispatch_mt(int MT, const bf16_t* x, long ldx, const bf16_t* w, int M, int K
 }
 
 }  // namespace
+
+// wsgemm launch plan for (M, N, K): BN (64/128) and split S maximising CU occupancy
+// (1 block per CU: its LDS ring is 72-144 KB), fewest partial slabs on ties.
+void lk_wsgemm_plan(int M, int N, int K, int swiglu, int* bn_out, int* s_out) {
+  // Rule fitted to the exhaustive (BN, S) sweep on MI355X (profiles/r1_ws_sweep.md):
+  // one block per CU, so fill <= 256 CUs in ONE round; prefer BN = 128 (half the X
+  // re-reads through L2) and split K only while every block keeps >= 16 stages;
+  // fall back to BN = 64 when BN = 128 leaves more than 30 % of the CUs idle.
+  (void)M;
+  auto plan = [&](int BN, int* S_out) -> double {
+    const int cols = swiglu ? N / 2 : N, per = swiglu ? BN / 2 : BN;
+    if (cols % per) return -1.0;
+    const int tiles = cols / per;
+    int S = 1;
+    while (tiles * S * 2 <= 256 && K % (S * 2 * 64) == 0 && K / (S * 2) >= 1024) S *= 2;
+    *S_out = S;
+    const int blocks = tiles * S, rounds = (blocks + 255) / 256;
+    return (double)blocks / (rounds * 256.0);
+  };
+  int s128 = 1, s64 = 1;
+  const double o128 = plan(128, &s128), o64 = plan(64, &s64);
+  if (o128 >= 0.7 || (o128 >= 0 && o64 <= o128)) {
+    *bn_out = 128;
+    *s_out = s128;
+  } else {
+    *bn_out = 64;
+    *s_out = o64 >= 0 ? s64 : 1;
+  }
+}
+
+int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, int swiglu,
+              bf16_t* out, long ldo, float* part, hipStream_t st) {
+  if (M < 1 || M > 256 || S < 1 || K % (S * 64) || (BN != 64 && BN != 128)) return -1;
+  const int per = swiglu ? BN / 2 : BN;
+  if (swiglu ? (N % 2 || (N / 2) % per) : N % BN) return -1;
+  if (S > 1 && part == nullptr) return -1;
+  const int I = swiglu ? N / 2 : 0;
+  const int n_tiles = (swiglu ? I : N) / per;
+  const int MT = M <= 64 ? 4 : M <= 128 ? 8 : 16;
+  const int ks = K / S;
+  float* p = S > 1 ? part : nullptr;
+  const int rc = swiglu ? dispatch_ws<true>(MT, BN, x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, p, N, st)
+                        : dispatch_ws<false>(MT, BN, x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, p, N, st);
+  if (rc) return rc;
+  if (S > 1) {
+    const int n_out = swiglu ? I : N;
+    const long work = (long)M * (n_out / 4);
+    int grid = (int)((work + 255) / 256);
+    if (grid > 2048) grid = 2048;
+    if (swiglu)
+      splitk_reduce_kernel<true><<<grid, 256, 0, st>>>(part, S, M, N, n_out, I, out, ldo);
+    else
+      splitk_reduce_kernel<false><<<grid, 256, 0, st>>>(part, S, M, N, n_out, 0, out, ldo);
+  }
+  LK_CHECK_LAUNCH();
+  return 0;
+}
 
 int lk_skinny_splits(int M, int N, int K, int swiglu) {
   (void)M;

@@ -221,49 +221,67 @@ def repeat_penalty_(logits, window, penalty):
     return ref.repeat_penalty_(logits, window, penalty)
 
 
-# When the hand-written decode-regime GEMM (csrc/skinny_gemm.hip) replaces the library
-# GEMM.  Measured on MI355X (profiles/r1_skinny_gemm.md): it wins wherever N is too
-# small for hipBLASLt to fill the chip (QKV / O / down at 64-96 column tiles of 64:
-# 1.3-2.3x at M <= 64, O/down still 1.3x at M = 128) and loses on wide N (gate_up,
-# LM head) beyond a handful of rows, where its fragment-shaped loads cap the per-CU
-# load rate; there hipBLASLt keeps the job.
-SKINNY_MAX_M = int(os.environ.get("LK_SKINNY_MAX_M", "128"))
+# Decode-regime GEMMs (csrc/skinny_gemm.hip) vs the library GEMM, from the MI355X
+# sweeps in profiles/r1_skinny_gemm.md and profiles/r1_ws_sweep.md:
+#  * M <= 16: the fragment-load kernel (weights straight to VGPRs, split-K);
+#  * 16 < M <= 256: the LDS-DMA weight-streaming kernel: 1.2-2.3x hipBLASLt on every
+#    Llama projection (QKV / O / down; gate_up+SwiGLU fused up to M = 160);
+#  * hipBLASLt keeps the LM head (N = 128256 fills the chip by itself) and anything larger.
+SKINNY_MAX_M = int(os.environ.get("LK_SKINNY_MAX_M", "16"))
+WS_MAX_M = int(os.environ.get("LK_WS_MAX_M", "256"))
+WS_SWIGLU_MAX_M = 160
 
 
-def _skinny_wanted(M: int, N: int, swiglu: bool) -> bool:
-    tiles = (N // 2) // 32 if swiglu else N // 64
-    if M <= 8:
-        return True
-    if tiles >= 256:
-        return False
-    return M <= (128 if tiles <= 64 else 64)
+def _decode_gemm_kind(x, w, swiglu: bool) -> Optional[str]:
+    if not (use_hip(x) and x.dim() == 2 and w.dim() == 2 and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16):
+        return None
+    M = x.shape[0]
+    N, K = w.shape
+    if M < 1 or K % 256 or x.stride(1) != 1 or x.stride(0) % 8 or not w.is_contiguous():
+        return None
+    if swiglu:
+        if N % 2 or (N // 2) % 64:
+            return None
+    elif N % 128:
+        return None
+    if M <= SKINNY_MAX_M:
+        return "skinny"
+    if N >= 65536 and not swiglu:
+        return None
+    if M <= (WS_SWIGLU_MAX_M if swiglu else WS_MAX_M):
+        return "ws"
+    return None
+
+
+def _skinny_wanted(M: int, N: int, swiglu: bool) -> bool:  # kept for tests / tooling
+    return M <= SKINNY_MAX_M
 
 
 def _skinny_ok(x, w, swiglu: bool) -> bool:
-    if not (use_hip(x) and x.dim() == 2 and w.dim() == 2 and x.dtype == torch.bfloat16
-            and w.dtype == torch.bfloat16 and 1 <= x.shape[0] <= SKINNY_MAX_M):
-        return False
-    N, K = w.shape
-    if K % 256 or x.stride(1) != 1 or x.stride(0) % 8 or not w.is_contiguous():
-        return False
-    if not ((N % 2 == 0 and (N // 2) % 32 == 0) if swiglu else N % 64 == 0):
-        return False
-    return _skinny_wanted(x.shape[0], N, swiglu)
+    return _decode_gemm_kind(x, w, swiglu) is not None
 
 
 def linear(x, w, b=None):
     """Projection GEMM: decode-sized batches (M <= SKINNY_MAX_M) on the hand-written
     weight-streaming MFMA kernel, everything else on hipBLASLt through torch."""
-    if b is None and _skinny_ok(x, w, False):
-        return lib().skinny_linear(x, w)
+    if b is None:
+        kind = _decode_gemm_kind(x, w, False)
+        if kind == "skinny":
+            return lib().skinny_linear(x, w)
+        if kind == "ws":
+            return lib().ws_linear(x, w)
     return torch.nn.functional.linear(x, w, b)
 
 
 def linear_swiglu(x, w_gate_up):
     """silu(x Wg^T) * (x Wu^T) for a fused [Wg; Wu] weight: one kernel (GEMM with the
     SwiGLU epilogue) in the decode regime, hipBLASLt + silu_mul otherwise."""
-    if _skinny_ok(x, w_gate_up, True):
+    kind = _decode_gemm_kind(x, w_gate_up, True)
+    if kind == "skinny":
         return lib().skinny_linear(x, w_gate_up, True)
+    if kind == "ws":
+        return lib().ws_linear(x, w_gate_up, True)
     return silu_mul(linear(x, w_gate_up))
 
 

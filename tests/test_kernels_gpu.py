@@ -309,4 +309,34 @@ def test_linear_dispatch_uses_skinny(hip):
     assert ops._skinny_ok(x, w, False)
     _close(ops.linear(x, w), x.float() @ w.float().t(), 0.02, 0.01)
     assert not ops._skinny_ok(torch.randn(512, 4096, device=DEV, dtype=torch.bfloat16), w, False)
-    assert not ops._skinny_wanted(64, 28672, True) and ops._skinny_wanted(4, 28672, True)
+    x128 = torch.randn(128, 4096, device=DEV, dtype=torch.bfloat16)
+    assert ops._decode_gemm_kind(x128, w, False) == "ws"
+    _close(ops.linear(x128, w), x128.float() @ w.float().t(), 0.02, 0.01)
+
+
+@pytest.mark.parametrize("M", [33, 64, 65, 100, 128, 129, 200, 256])
+@pytest.mark.parametrize("NK", [(6144, 4096), (4096, 4096), (4096, 14336), (1280, 8192), (128256, 4096)])
+def test_ws_linear(hip, M, NK):
+    """LDS-DMA staged weight-streaming GEMM (every BN / split plan) vs an fp32 matmul."""
+    N, K = NK
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    y_ref = x.float() @ w.float().t()
+    _close(hip.ws_linear(x, w), y_ref, 0.02, 0.01, f"ws M{M} N{N} K{K}")
+    if N <= 6144:
+        for bn, S in ((64, 1), (128, 2), (64, 4)):
+            if N % bn == 0 and K % (S * 64) == 0:
+                _close(hip.ws_linear(x, w, False, bn, S), y_ref, 0.02, 0.01, f"ws bn{bn} S{S}")
+
+
+@pytest.mark.parametrize("M", [64, 128, 256])
+@pytest.mark.parametrize("IK", [(14336, 4096), (3584, 8192)])
+def test_ws_swiglu(hip, M, IK):
+    I, K = IK
+    torch.manual_seed(2)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(2 * I, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    a_ref = ref.silu_mul((x.float() @ w.float().t()).to(torch.bfloat16))
+    _close(hip.ws_linear(x, w, True), a_ref, 0.03, 0.01, f"ws swiglu M{M} I{I}")
+    _close(hip.ws_linear(x, w, True, 64, 2), a_ref, 0.03, 0.01, "ws swiglu bn64 S2")
