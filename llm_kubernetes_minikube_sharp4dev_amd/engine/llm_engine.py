@@ -22,6 +22,10 @@ from .sequence import Sequence, Status
 log = get_logger("engine")
 
 
+def _plain_greedy(p: SamplingParams) -> bool:
+    return p.is_greedy and p.logits_processor is None and (p.repeat_penalty == 1.0 or p.repeat_last_n == 0)
+
+
 class LLMEngine:
     def __init__(self, model, tokenizer=None, block_size: int = 16, max_model_len: int = 8192,
                  max_num_seqs: int = 256, max_num_batched_tokens: int = 65536,
@@ -78,15 +82,20 @@ class LLMEngine:
             if batch.empty:
                 return []
             t0 = time.perf_counter()
-            rows, logits = self.runner.forward_logits(batch.items)
+            # plain greedy steps get token ids straight from the model (no fp32 logits;
+            # under TP an all-gather of (max, argmax) pairs instead of the vocab)
+            greedy = all(_plain_greedy(sq.params) for sq, _, _ in batch.items)
+            rows, logits = self.runner.forward_logits(batch.items, greedy)
             for seq, start, n in batch.items:
                 seq.num_computed = start + n
                 self.scheduler.publish_blocks(seq)
             out = []
             if rows:
                 seqs = [s for s, _ in rows]
-                ids = self.sampler(logits, [s.params for s in seqs], [s.output_ids for s in seqs])
-                ids = ids.tolist()
+                if greedy:
+                    ids = logits.tolist()
+                else:
+                    ids = self.sampler(logits, [s.params for s in seqs], [s.output_ids for s in seqs]).tolist()
                 now = time.perf_counter()
                 for seq, tid in zip(seqs, ids):
                     self._append(seq, int(tid), now)

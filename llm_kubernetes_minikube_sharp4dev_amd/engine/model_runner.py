@@ -106,9 +106,15 @@ class ModelRunner:
         return bt
 
     # ----------------------------------------------------------- step inputs (host)
-    def prepare(self, items):
+    def prepare(self, items, greedy: bool = False):
         """items [(seq, start, n)] -> (StepInputs of host arrays, rows [(seq, row)]).
-        Everything a rank needs to run the step; a TP driver broadcasts it."""
+        Everything a rank needs to run the step; a TP driver broadcasts it.  ``greedy``:
+        the step returns token ids (distributed argmax under TP) instead of logits."""
+        si, rows = self._prepare(items)
+        si.greedy = bool(greedy)
+        return si, rows
+
+    def _prepare(self, items):
         if self.use_graphs and items and all(s.is_decode for s, _, _ in items) and len(items) <= self.graph_sizes[-1]:
             return self._prepare_graph(items)
         pre = [it for it in items if not it[0].is_decode]
@@ -191,7 +197,8 @@ class ModelRunner:
 
     @torch.inference_mode()
     def execute(self, si: "StepInputs"):
-        """Run one step on this rank; returns logits [R, V] f32 (None if no rows)."""
+        """Run one step on this rank; returns logits [R, V] f32, or int32 token ids [R]
+        for a greedy step (None if no rows)."""
         if si.decode_graph:
             return self._graph_execute(si)
         ids, meta = self._meta(si)
@@ -199,13 +206,14 @@ class ModelRunner:
             self.model(ids, meta, self.kv_caches)  # partial prefill chunks only: KV write, no logits
             return None
         h = self.model(ids, meta, self.kv_caches)
-        return self.model.logits(h)
+        return self.model.greedy(h) if si.greedy else self.model.logits(h)
 
-    def forward_logits(self, items):
-        """Run one step; returns (rows [(seq,row)], logits [R, V] f32)."""
+    def forward_logits(self, items, greedy: bool = False):
+        """Run one step; returns (rows [(seq,row)], logits [R, V] f32 -- or int32 token
+        ids [R] when ``greedy``)."""
         if not items:
             return [], None
-        si, rows = self.prepare(items)
+        si, rows = self.prepare(items, greedy)
         if self.step_hook is not None:
             self.step_hook(si)  # e.g. TP driver broadcast to worker ranks
         lg = self.execute(si)
@@ -232,14 +240,14 @@ class ModelRunner:
                               decode_split=split, part_o=po, part_ml=pm)
         return st
 
-    def capture(self, B):
+    def capture(self, B, greedy: bool = False):
         st = self._static(B)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for _ in range(2):  # warm-up (allocator + lazy library init) outside capture
                 h = self.model(st["ids"], st["meta"], self.kv_caches)
-                self.model.logits(h)
+                self.model.greedy(h) if greedy else self.model.logits(h)
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         if self._graph_pool is None:
@@ -247,21 +255,24 @@ class ModelRunner:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=self._graph_pool):
             h = self.model(st["ids"], st["meta"], self.kv_caches)
-            st["logits"] = self.model.logits(h)
+            st["logits"] = self.model.greedy(h) if greedy else self.model.logits(h)
         st["graph"] = g
-        self.graphs[B] = st
+        self.graphs[(B, greedy)] = st
         return st
 
     @torch.inference_mode()
-    def capture_all(self, max_batch: Optional[int] = None):
+    def capture_all(self, max_batch: Optional[int] = None, variants=(False, True)):
+        """Capture the decode graphs of every batch bucket (<= max_batch), for the
+        sampled-logits and/or the greedy-ids output variant."""
         for B in self.graph_sizes:
             if max_batch is None or B <= max_batch:
-                if B not in self.graphs:
-                    self.capture(B)
+                for v in variants:
+                    if (B, v) not in self.graphs:
+                        self.capture(B, v)
 
     def _graph_execute(self, si):
         Bg = si.decode_graph
-        st = self.graphs.get(Bg) or self.capture(Bg)
+        st = self.graphs.get((Bg, si.greedy)) or self.capture(Bg, si.greedy)
         st["ids"].copy_(torch.from_numpy(si.ids), non_blocking=True)
         st["pos"].copy_(torch.from_numpy(si.positions), non_blocking=True)
         st["slots"].copy_(torch.from_numpy(si.slots), non_blocking=True)
@@ -286,3 +297,4 @@ class StepInputs:
     ctx_d: Optional[np.ndarray] = None
     tables_d: Optional[np.ndarray] = None
     logits_rows: np.ndarray = field(default_factory=lambda: np.zeros(0, dtype=np.int64))
+    greedy: bool = False                  # return token ids (argmax) instead of logits

@@ -119,6 +119,10 @@ class LlamaModel(nn.Module):
             lg = self.tp.all_gather_cat(lg, dim=-1)
         return lg.to(dtype) if dtype is not None else lg
 
+    def greedy(self, hidden: torch.Tensor) -> torch.Tensor:
+        """Greedy next tokens [R] int32 without materialising gathered fp32 logits."""
+        return self.tp.greedy_ids(ops.linear(hidden, self.lm_head), self.vocab_lo)
+
     # ------------------------------------------------------------------ HF checkpoint
     @torch.no_grad()
     def load_hf_state_dict(self, sd: dict):

@@ -105,6 +105,9 @@ class OPTModel(nn.Module):
         lg = ops.linear(hidden, self.lm_head)
         return lg.to(dtype) if dtype is not None else lg
 
+    def greedy(self, hidden):
+        return ops.linear(hidden, self.lm_head).float().argmax(dim=-1).int()
+
     @torch.no_grad()
     def load_hf_state_dict(self, sd: dict):
         """HuggingFace ``OPTForCausalLM`` names (``model.decoder.*``)."""

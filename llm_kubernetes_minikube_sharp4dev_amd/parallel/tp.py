@@ -43,6 +43,19 @@ class TPGroup:
         dist.all_gather(parts, t.contiguous(), group=self.group)
         return torch.cat(parts, dim=dim)
 
+    def greedy_ids(self, local_logits: torch.Tensor, vocab_lo: int = 0) -> torch.Tensor:
+        """Greedy token ids from vocab-parallel logits [R, V/tp]: local (max, argmax),
+        all-gather of R (value, id) pairs per rank instead of the [R, V] logits, pick the
+        max (first rank on ties = lowest id, the single-GPU argmax order)."""
+        vals, idx = local_logits.float().max(dim=-1)
+        idx = idx + vocab_lo
+        if self.size == 1:
+            return idx.int()
+        v = self.all_gather_cat(vals[None], dim=0)
+        i = self.all_gather_cat(idx[None], dim=0)
+        k = v.argmax(dim=0)
+        return i.gather(0, k[None]).squeeze(0).int()
+
     def shard(self, n: int) -> tuple[int, int]:
         """[start, end) of this rank's slice of a dimension of size n (n % size == 0)."""
         if n % self.size:

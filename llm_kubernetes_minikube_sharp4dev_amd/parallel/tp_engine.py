@@ -85,13 +85,14 @@ def make_tp_engine(model, tp: TPGroup, tokenizer=None, engine_kw: Optional[dict]
     return eng
 
 
-def tp_capture_all(engine, max_batch: Optional[int] = None):
+def tp_capture_all(engine, max_batch: Optional[int] = None, variants=(False, True)):
     """Capture decode graphs on every rank in lockstep."""
     r = engine.runner
     for B in r.graph_sizes:
-        if (max_batch is None or B <= max_batch) and B not in r.graphs:
-            engine.tp_ctrl.bcast(("capture", B))
-            r.capture(B)
+        for v in variants:
+            if (max_batch is None or B <= max_batch) and (B, v) not in r.graphs:
+                engine.tp_ctrl.bcast(("capture", (B, v)))
+                r.capture(B, v)
 
 
 def shutdown_tp(engine):
@@ -119,7 +120,7 @@ def run_tp_worker(model, tp: TPGroup, **runner_kw):
         if cmd == "stop":
             break
         if cmd == "capture":
-            runner.capture(arg)
+            runner.capture(*arg)
         elif cmd == "barrier":
             if torch.cuda.is_available() and model.device.type == "cuda":
                 torch.cuda.synchronize()
