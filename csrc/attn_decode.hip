@@ -66,6 +66,7 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(
   const int nblk = (nkeys + BS - 1) / BS;
   for (int i = threadIdx.x; i < nblk; i += 256)
     blk[i] = block_tables[(long)b * bt_stride + k_begin / BS + i];
+    LK_DASSERT(blk[i] >= 0);
   __syncthreads();
 
   auto row_ptr = [&](const bf16_t* cache, int rel) {

@@ -52,7 +52,10 @@ def _newer(src: Path, obj: Path, headers: list[Path]) -> bool:
     return src.stat().st_mtime > t or any(h.stat().st_mtime > t for h in headers)
 
 
-def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
+def build(clean: bool = False, jobs: int | None = None, verbose: bool = False, debug: bool = False) -> Path:
+    global BUILD
+    if debug:  # device asserts (LK_DASSERT) on, separate object cache
+        BUILD = ROOT / "build" / "csrc-debug"
     if clean and BUILD.exists():
         shutil.rmtree(BUILD)
     BUILD.mkdir(parents=True, exist_ok=True)
@@ -61,6 +64,8 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
     py_inc = sysconfig.get_paths()["include"]
     headers = sorted(CSRC.glob("*.h"))
     common = ["-O3", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-I{CSRC}"]
+    if debug:
+        common += ["-DLK_DEBUG", "-g"]
     kern_flags = common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-ffp-contract=fast"]
     bind_flags = common + [
         f"--offload-arch={ARCH}",
@@ -121,8 +126,9 @@ def main(argv=None):
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--debug", action="store_true", help="device bounds checks (LK_DASSERT), -g")
     a = ap.parse_args(argv)
-    build(a.clean, a.jobs, a.verbose)
+    build(a.clean, a.jobs, a.verbose, a.debug)
 
 
 if __name__ == "__main__":

@@ -83,3 +83,13 @@ LK_DEVICE int xcd_remap(int bid, int nwg) {
 }
 
 #define LK_CHECK_LAUNCH() (void)hipGetLastError()
+
+// Device-side bounds checks for debug builds (`python csrc/build.py --debug`, objects
+// under build/csrc-debug): a failing check traps the wave with the kernel's file/line
+// instead of silently reading or writing out of range.  Compiled out otherwise.
+#ifdef LK_DEBUG
+#include <cassert>
+#define LK_DASSERT(cond) assert(cond)
+#else
+#define LK_DASSERT(cond) ((void)0)
+#endif

@@ -22,6 +22,7 @@ __global__ __launch_bounds__(128) void rope_kv_kernel(
   const float* cs = cos_sin + (long)pos * D;  // [cos(D/2) | sin(D/2)]
   bf16_t* row = qkv + t * qs;
   const int slot = slots ? slots[t] : -1;
+  LK_DASSERT(slot >= -1);
   const long blk = slot >= 0 ? slot / BS : 0;
   const int off = slot >= 0 ? slot % BS : 0;
   const int ipr = NEOX ? (D >> 4) : (D >> 3);  // items per head

@@ -155,12 +155,29 @@ class LLMEngine:
 class AsyncLLMEngine:
     """Background step loop + asyncio streaming for the HTTP front-end."""
 
-    def __init__(self, engine: LLMEngine):
+    def __init__(self, engine: LLMEngine, request_timeout_s: Optional[float] = None, stall_s: float = 120.0):
+        from ..utils.watchdog import StepWatchdog
+
         self.engine = engine
+        self.request_timeout_s = request_timeout_s
         self._wake = threading.Event()
         self._stop = False
+        self.watchdog = StepWatchdog("engine", stall_s=stall_s, on_stall=lambda dt: self._fail_all("stalled"))
         self._thread = threading.Thread(target=self._loop, name="lk-engine", daemon=True)
         self._thread.start()
+
+    @property
+    def healthy(self) -> bool:
+        return self.watchdog.healthy and self._thread.is_alive()
+
+    def _fail_all(self, why: str):
+        """Finish every in-flight request with an error token (-1) so no client hangs."""
+        with self.engine.lock:
+            for s in list(self.engine.scheduler.running) + list(self.engine.scheduler.waiting):
+                self.engine.scheduler.abort(s.req_id)
+                s.error = why
+                if s.on_token:
+                    s.on_token(s, -1, True)
 
     def _loop(self):
         while not self._stop:
@@ -169,23 +186,28 @@ class AsyncLLMEngine:
                 self._wake.clear()
                 continue
             try:
-                self.engine.step()
+                with self.watchdog.busy():
+                    self.engine.step()
+                self.watchdog.beat()
             except Exception:  # pragma: no cover
                 log.exception("engine step failed; aborting in-flight requests")
-                with self.engine.lock:
-                    for s in list(self.engine.scheduler.running) + list(self.engine.scheduler.waiting):
-                        self.engine.scheduler.abort(s.req_id)
-                        if s.on_token:
-                            s.on_token(s, -1, True)
+                self._fail_all("engine step failed")
 
     def shutdown(self):
         self._stop = True
         self._wake.set()
+        self.watchdog.stop()
 
-    async def stream(self, prompt_ids: list, params: SamplingParams, req_id: Optional[str] = None):
-        """Async generator of (token_id, finished, seq)."""
+    async def stream(self, prompt_ids: list, params: SamplingParams, req_id: Optional[str] = None,
+                     timeout_s: Optional[float] = None):
+        """Async generator of (token_id, finished, seq).  A request still running after
+        ``timeout_s`` (default: the engine's ``request_timeout_s``) is aborted and
+        ``asyncio.TimeoutError`` raised; a client that stops iterating (HTTP disconnect)
+        aborts its request."""
         loop = asyncio.get_running_loop()
         q: asyncio.Queue = asyncio.Queue()
+        timeout_s = timeout_s if timeout_s is not None else self.request_timeout_s
+        deadline = loop.time() + timeout_s if timeout_s else None
 
         def cb(seq, tid, fin):
             loop.call_soon_threadsafe(q.put_nowait, (tid, fin, seq))
@@ -194,7 +216,10 @@ class AsyncLLMEngine:
         self._wake.set()
         try:
             while True:
-                tid, fin, s = await q.get()
+                if deadline is None:
+                    tid, fin, s = await q.get()
+                else:
+                    tid, fin, s = await asyncio.wait_for(q.get(), max(0.0, deadline - loop.time()))
                 yield tid, fin, s
                 if fin:
                     break
@@ -202,8 +227,9 @@ class AsyncLLMEngine:
             if not seq.finished:
                 self.engine.abort(seq.req_id)
 
-    async def generate(self, prompt_ids: list, params: SamplingParams, req_id: Optional[str] = None):
+    async def generate(self, prompt_ids: list, params: SamplingParams, req_id: Optional[str] = None,
+                       timeout_s: Optional[float] = None):
         last = None
-        async for _, fin, s in self.stream(prompt_ids, params, req_id):
+        async for _, fin, s in self.stream(prompt_ids, params, req_id, timeout_s):
             last = s
         return last

@@ -80,7 +80,11 @@ def init_distributed(backend: Optional[str] = None) -> TPGroup:
         os.environ.setdefault("MASTER_PORT", "29500")
         if backend == "nccl":
             torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-        dist.init_process_group(backend=backend)
+        # collectives on a dead / hung rank fail after this instead of blocking forever
+        from datetime import timedelta
+
+        dist.init_process_group(backend=backend,
+                                timeout=timedelta(seconds=float(os.environ.get("LK_DIST_TIMEOUT_S", "600"))))
     return TPGroup(dist.get_rank(), dist.get_world_size(), dist.group.WORLD)
 
 

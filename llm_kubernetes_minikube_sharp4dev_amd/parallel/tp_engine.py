@@ -113,10 +113,15 @@ def tp_barrier(engine):
 @torch.inference_mode()
 def run_tp_worker(model, tp: TPGroup, **runner_kw):
     """Ranks > 0: execute whatever rank 0 schedules until it says stop."""
+    from ..utils.watchdog import StepWatchdog
+
+    stall_s = float(runner_kw.pop("stall_s", 600.0)) if "stall_s" in runner_kw else 600.0
     runner, ctrl = make_tp_runner(model, tp, **runner_kw)
+    wd = StepWatchdog(f"tp-worker-{tp.rank}", stall_s=stall_s)
     n = 0
     while True:
-        cmd, arg = ctrl.bcast(None)
+        cmd, arg = ctrl.bcast(None)  # idle wait for the driver: not a stall
+        wd.beat()
         if cmd == "stop":
             break
         if cmd == "capture":
@@ -126,7 +131,11 @@ def run_tp_worker(model, tp: TPGroup, **runner_kw):
                 torch.cuda.synchronize()
             dist.barrier()
         elif cmd == "step":
-            runner.execute(arg)
+            with wd.busy():  # a step that never returns (dead peer in an all-reduce) is a stall
+                runner.execute(arg)
+                if torch.cuda.is_available() and model.device.type == "cuda":
+                    torch.cuda.synchronize()
             n += 1
+    wd.stop()
     log.info("tp worker rank %d done after %d steps", tp.rank, n)
     return n

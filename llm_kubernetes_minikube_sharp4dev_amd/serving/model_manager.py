@@ -108,7 +108,8 @@ class ModelManager:
                 kw["num_blocks"] = 2048
             kw.update(self.engine_overrides)
             eng = LLMEngine(model, tok, **kw)
-            h = GeneratorHandle(name, preset, eng, AsyncLLMEngine(eng), tok, style,
+            h = GeneratorHandle(name, preset, eng, AsyncLLMEngine(eng, request_timeout_s=self.cfg.agent.request_timeout_s),
+                                tok, style,
                                 load_s=time.perf_counter() - t0)
             self.generators[name] = h
             log.info("loaded generator %s (%s) in %.1fs", name, preset, h.load_s)

@@ -101,20 +101,27 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
             seq = None
             first_ns = None
             emitted = 0
-            async for tid, fin, s in h.async_engine.stream(ids, sp):
-                seq = s
-                if first_ns is None:
-                    first_ns = time.perf_counter_ns()
-                piece = detok.push(tid) if tid >= 0 and not (fin and tid in h.engine.eos_ids) else ""
-                text += piece
-                if stop_strs:
-                    cut = min((text.find(st) for st in stop_strs if st in text), default=-1)
-                    if cut >= 0:
-                        piece = piece[: max(0, len(piece) - (len(text) - cut))]
-                        text = text[:cut]
-                if piece and stream:
-                    yield json.dumps(mk_chunk(piece), ensure_ascii=False) + "\n"
-                emitted += 1
+            try:
+                async for tid, fin, s in h.async_engine.stream(ids, sp):
+                    seq = s
+                    if tid < 0 and getattr(s, "error", None):  # engine failure / watchdog stall
+                        yield json.dumps({"error": f"generation failed: {s.error}"}) + ("\n" if stream else "")
+                        return
+                    if first_ns is None:
+                        first_ns = time.perf_counter_ns()
+                    piece = detok.push(tid) if tid >= 0 and not (fin and tid in h.engine.eos_ids) else ""
+                    text += piece
+                    if stop_strs:
+                        cut = min((text.find(st) for st in stop_strs if st in text), default=-1)
+                        if cut >= 0:
+                            piece = piece[: max(0, len(piece) - (len(text) - cut))]
+                            text = text[:cut]
+                    if piece and stream:
+                        yield json.dumps(mk_chunk(piece), ensure_ascii=False) + "\n"
+                    emitted += 1
+            except asyncio.TimeoutError:
+                yield json.dumps({"error": "request timed out"}) + ("\n" if stream else "")
+                return
             end = time.perf_counter_ns()
             first_ns = first_ns or end
             stats = {
@@ -138,7 +145,8 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
         out = ""
         async for part in gen():
             out = part
-        return Response(out, media_type="application/json; charset=utf-8")
+        status = 500 if out.startswith('{"error"') else 200
+        return Response(out, status_code=status, media_type="application/json; charset=utf-8")
 
     # ------------------------------------------------------------------ generate
     @app.post("/api/generate")
@@ -288,6 +296,14 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
                 "details": {k: d[k] for k in ("format", "family", "families", "parameter_size", "quantization_level")},
                 "model_info": {"general.architecture": d["family"], "general.parameter_count": d["params"]},
                 "capabilities": caps}
+
+    @app.get("/health")
+    async def health():
+        """Engine health (watchdog): 503 while a loaded generator's step loop is stalled."""
+        eng = {n: {"healthy": h.async_engine.healthy, "steps": h.async_engine.watchdog.steps,
+                   "stalls": h.async_engine.watchdog.stalls} for n, h in list(mgr.generators.items())}
+        ok = all(v["healthy"] for v in eng.values())
+        return JSONResponse({"status": "ok" if ok else "degraded", "generators": eng}, status_code=200 if ok else 503)
 
     @app.get("/api/ps")
     async def ps():

@@ -207,3 +207,64 @@ def test_rest_k8s_client_against_fake_apiserver():
     with pytest.raises(K8sApiError) as e:
         client.read_namespaced_deployment_scale("nope", "default")
     assert "NotFound" in str(e.value)
+
+
+def test_ollama_concurrent_clients_share_one_engine(ollama):
+    """16 simultaneous streaming clients on one continuous-batching engine (the engine
+    loop is the single writer of scheduler state; requests interleave per step)."""
+    _, app = ollama
+
+    async def one(client, i):
+        async with client.stream("POST", "/api/generate", json={
+                "model": "llama3.1:8b", "prompt": f"richiesta {i} " * (1 + i % 5),
+                "options": {"num_predict": 4 + i % 3, "temperature": 0}}) as r:
+            lines = [json.loads(l) async for l in r.aiter_lines() if l.strip()]
+        return i, lines
+
+    async def main():
+        transport = httpx.ASGITransport(app=app)
+        async with httpx.AsyncClient(transport=transport, base_url="http://t") as client:
+            return await asyncio.gather(*(one(client, i) for i in range(16)))
+
+    res = asyncio.run(main())
+    assert len(res) == 16
+    for i, lines in res:
+        assert lines[-1]["done"] and lines[-1]["eval_count"] == 4 + i % 3
+    r = TestClient(app).get("/health")
+    assert r.status_code == 200 and r.json()["status"] == "ok"
+
+
+def test_request_timeout_aborts_and_watchdog_flags_stall():
+    import time as _t
+
+    import torch
+
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.llm_engine import AsyncLLMEngine, LLMEngine
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import SamplingParams
+    from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder
+    from llm_kubernetes_minikube_sharp4dev_amd.utils.watchdog import StepWatchdog
+
+    stalls = []
+    wd = StepWatchdog("t", stall_s=0.2, on_stall=stalls.append, poll_s=0.02)
+    with wd.busy():
+        _t.sleep(0.5)
+    assert stalls and not wd.healthy
+    wd.beat()
+    assert wd.healthy
+    wd.stop()
+
+    m = build_decoder("llama-tiny", dtype=torch.float32)
+    eng = LLMEngine(m, None, max_model_len=512, max_num_seqs=4, num_blocks=64, use_graphs=False, eos_ids=set())
+    aeng = AsyncLLMEngine(eng, request_timeout_s=1e-4)
+
+    async def go():
+        with pytest.raises(asyncio.TimeoutError):
+            await aeng.generate(list(range(5, 60)), SamplingParams.greedy(10_000))
+
+    asyncio.run(go())
+    for _ in range(100):
+        if not eng.has_work():
+            break
+        _t.sleep(0.01)
+    assert not eng.has_work()  # the timed-out request was aborted
+    aeng.shutdown()
