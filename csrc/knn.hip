@@ -47,8 +47,13 @@ __global__ __launch_bounds__(256) void knn_partial_kernel(
     float* __restrict__ part_s, int* __restrict__ part_i, int nblocks) {
   constexpr int CPR = D / 8;  // 16-B chunks per row
   constexpr int NG = D / 64;  // groups of 4 k-steps
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[QT * D];
-  __shared__ float sc[QT][ROWS + 1];
+  // one LDS buffer: the Q tile during the MFMA phase, then (after a barrier) the score
+  // tile for the top-k phase -- max(QT*D*2, QT*(ROWS+1)*4) bytes instead of the sum,
+  // so 2-3 workgroups fit per CU
+  constexpr int QBYTES = QT * D * 2, SBYTES = QT * (ROWS + 1) * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[QBYTES > SBYTES ? QBYTES : SBYTES];
+  bf16_t* Qs = reinterpret_cast<bf16_t*>(smem);
+  float(*sc)[ROWS + 1] = reinterpret_cast<float(*)[ROWS + 1]>(smem);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int qbase = blockIdx.y * QT;
@@ -64,6 +69,7 @@ __global__ __launch_bounds__(256) void knn_partial_kernel(
   __syncthreads();
 
   // k-step (4g+u), element j  <->  d = 64g + 32h + 8u + j
+  floatx16 acc2[2];
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     const long doc = row0 + w * 64 + m * 32 + r;
@@ -84,13 +90,18 @@ __global__ __launch_bounds__(256) void knn_partial_kernel(
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u], bq, acc, 0, 0, 0);
       }
     }
-    // C[row = doc (i&3)+8(i>>2)+4h][col = query r]
-    const float qn = (qbase + r < nq) ? qnorm[qbase + r] : 1.f;
+    acc2[m] = acc;
+  }
+  __syncthreads();  // every wave done with Qs: the buffer becomes the score tile
+  // C[row = doc (i&3)+8(i>>2)+4h][col = query r]
+  const float qn = (qbase + r < nq) ? qnorm[qbase + r] : 1.f;
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int lr = w * 64 + m * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
       const long d = row0 + lr;
-      sc[r][lr] = d < N ? acc[i] / (qn * cnorm[d] + 1e-9f) : -INFINITY;
+      sc[r][lr] = d < N ? acc2[m][i] / (qn * cnorm[d] + 1e-9f) : -INFINITY;
     }
   }
   __syncthreads();
@@ -192,6 +203,9 @@ int lk_knn_partial(const bf16_t* corpus, const float* cnorm, long N, int D, cons
   const int nb = lk_knn_nblocks(N);
   dim3 grid(nb, (nq + QT - 1) / QT);
   switch (D) {
+    case 128: knn_partial_kernel<128><<<grid, 256, 0, st>>>(corpus, cnorm, N, queries, qnorm, nq, K, part_s, part_i, nb); break;
+    case 256: knn_partial_kernel<256><<<grid, 256, 0, st>>>(corpus, cnorm, N, queries, qnorm, nq, K, part_s, part_i, nb); break;
+    case 512: knn_partial_kernel<512><<<grid, 256, 0, st>>>(corpus, cnorm, N, queries, qnorm, nq, K, part_s, part_i, nb); break;
     case 384: knn_partial_kernel<384><<<grid, 256, 0, st>>>(corpus, cnorm, N, queries, qnorm, nq, K, part_s, part_i, nb); break;
     case 768: knn_partial_kernel<768><<<grid, 256, 0, st>>>(corpus, cnorm, N, queries, qnorm, nq, K, part_s, part_i, nb); break;
     case 1024: knn_partial_kernel<1024><<<grid, 256, 0, st>>>(corpus, cnorm, N, queries, qnorm, nq, K, part_s, part_i, nb); break;

@@ -197,7 +197,7 @@ def test_flash_softmax_spike():
     _close(y, y_ref, 0.03, 0.0, "spike")
 
 
-@pytest.mark.parametrize("N,D", [(1, 384), (1000, 768), (70000, 768), (5000, 1024)])
+@pytest.mark.parametrize("N,D", [(1, 384), (1000, 768), (70000, 768), (5000, 1024), (3000, 128), (777, 256), (2000, 512)])
 def test_knn_topk(hip, N, D):
     torch.manual_seed(11)
     corpus = torch.randn(N, D, device=DEV).to(torch.bfloat16)
