@@ -104,7 +104,9 @@ def case_knn(N=485_000, D=768, nq=64):
     q = torch.randn(nq, D, device=DEV, dtype=torch.bfloat16)
     cn, qn = ops.row_norms(c), ops.row_norms(q)
     t = timeit(lambda: ops.knn_topk(c, cn, q, qn, 6))
-    return {"case": f"knn_topk N{N} D{D} nq{nq} k6", "us": t * 1e6, "GB/s": N * D * 2 / t / 1e9}
+    tf = timeit(lambda: ops.lib().knn_topk(c, cn, q, qn, 6, True))
+    return {"case": f"knn_topk N{N} D{D} nq{nq} k6 (fused single-pass kernel: {tf * 1e6:.0f} us)", "us": t * 1e6,
+            "GB/s": N * D * 2 / t / 1e9}
 
 
 def case_gemm(M, N, K, layout="NT"):
@@ -194,7 +196,7 @@ CASES = {
     "prefill": lambda: [case_prefill(), case_prefill(B=8, L=4096)],
     "encoder": lambda: [case_encoder_attn()],
     "norm": lambda: [case_rmsnorm(), case_silu()],
-    "knn": lambda: [case_knn()],
+    "knn": lambda: [case_knn(), case_knn(nq=8), case_knn(N=1_000_000, nq=8), case_knn(N=1_000_000, nq=128)],
     "gemm": lambda: [case_gemm(64, 6144, 4096), case_gemm(64, 28672, 4096), case_gemm(64, 4096, 14336),
                      case_gemm(32768, 6144, 4096), case_gemm(32768, 28672, 4096), case_gemm(32768, 4096, 14336)],
     "skinny": lambda: [case_skinny(M, N, K, N == 28672) for M in (1, 16, 32, 64, 128, 256)

@@ -294,7 +294,7 @@ at::Tensor flash_prefill(const at::Tensor& q, const at::Tensor& k, const at::Ten
 }
 
 std::vector<at::Tensor> knn_topk(const at::Tensor& corpus, const at::Tensor& cnorm, const at::Tensor& queries,
-                                 const at::Tensor& qnorm, int64_t K) {
+                                 const at::Tensor& qnorm, int64_t K, bool force_fused) {
   CHECK_CUDA(corpus); CHECK_BF16(corpus); CHECK_CONTIG(corpus); CHECK_F32(cnorm); CHECK_CONTIG(cnorm);
   CHECK_BF16(queries); CHECK_CONTIG(queries); CHECK_F32(qnorm); CHECK_CONTIG(qnorm);
   TORCH_CHECK(corpus.dim() == 2 && queries.dim() == 2 && corpus.size(1) == queries.size(1), "dimension mismatch");
@@ -308,6 +308,23 @@ std::vector<at::Tensor> knn_topk(const at::Tensor& corpus, const at::Tensor& cno
   at::Tensor out_s = at::full({nq, (long)K}, -INFINITY, fo);
   at::Tensor out_i = at::full({nq, (long)K}, -1, io);
   if (N == 0 || nq == 0) return {out_s, out_i};
+  if (D % 64 == 0 && nq <= 256 && !force_fused) {
+    // corpus streamed once by the LDS-DMA weight-streaming GEMM (dots in f32), then a
+    // normalise + chunked top-k pass and the shared merge
+    at::Tensor scores = at::empty({nq, N}, fo);
+    int rc = lk_ws_scores_f32(bp(queries), D, bp(corpus), nq, N, D, scores.data_ptr<float>(), N, cur_stream());
+    CHECK_RC(rc, "knn scores");
+    const int nc = lk_knn_score_chunks(N);
+    at::Tensor ps = at::empty({nq, nc, kk}, fo);
+    at::Tensor pi = at::empty({nq, nc, kk}, io);
+    rc = lk_knn_score_topk(scores.data_ptr<float>(), N, cnorm.data_ptr<float>(), qnorm.data_ptr<float>(), N, nq, kk,
+                           ps.data_ptr<float>(), pi.data_ptr<int>(), cur_stream());
+    CHECK_RC(rc, "knn score_topk");
+    rc = lk_knn_merge(ps.data_ptr<float>(), pi.data_ptr<int>(), nq, nc * kk, (int)K, out_s.data_ptr<float>(),
+                      out_i.data_ptr<int>(), cur_stream());
+    CHECK_RC(rc, "knn_merge");
+    return {out_s, out_i};
+  }
   const int nb = lk_knn_nblocks(N);
   at::Tensor ps = at::empty({nq, nb, kk}, fo);
   at::Tensor pi = at::empty({nq, nb, kk}, io);
@@ -400,7 +417,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("paged_decode", &paged_decode, "", py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("max_splits"), py::arg("split"), py::arg("scale"), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("out") = py::none());
   m.def("prefill_rows_per_tile", &prefill_rows_per_tile);
   m.def("flash_prefill", &flash_prefill, "", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("block_tables"), py::arg("cu_q"), py::arg("ctx_lens"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("out") = py::none());
-  m.def("knn_topk", &knn_topk);
+  m.def("knn_topk", &knn_topk, "", py::arg("corpus"), py::arg("cnorm"), py::arg("queries"), py::arg("qnorm"),
+        py::arg("K"), py::arg("force_fused") = false);
   m.def("knn_merge", &knn_merge);
   m.def("pool_normalize", &pool_normalize);
   m.def("row_norms", &row_norms);

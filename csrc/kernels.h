@@ -31,6 +31,9 @@ void lk_wsgemm_plan(int M, int N, int K, int swiglu, int* bn_out, int* s_out);
 int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, int swiglu,
               bf16_t* out, long ldo, float* part, hipStream_t st);
 
+int lk_ws_scores_f32(const bf16_t* x, long ldx, const bf16_t* w, int M, long N, int K, float* out, long ldo,
+                     hipStream_t st);
+
 // rope_kv.hip
 int lk_rope_kv(bf16_t* qkv, long qs, const int* positions, const float* cos_sin, long T, int Hq,
                int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,
@@ -58,6 +61,9 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
 int lk_knn_nblocks(long N);
 int lk_knn_partial(const bf16_t* corpus, const float* cnorm, long N, int D, const bf16_t* queries,
                    const float* qnorm, int nq, int K, float* part_s, int* part_i, hipStream_t st);
+int lk_knn_score_chunks(long N);
+int lk_knn_score_topk(const float* scores, long ld, const float* cnorm, const float* qnorm, long N, int nq, int K,
+                      float* part_s, int* part_i, hipStream_t st);
 int lk_knn_merge(const float* cand_s, const int* cand_i, int nq, int ncand, int K, float* out_s,
                  int* out_i, hipStream_t st);
 

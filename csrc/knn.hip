@@ -137,6 +137,67 @@ __global__ __launch_bounds__(256) void knn_partial_kernel(
   }
 }
 
+// Top-k over precomputed dot products (scores [nq, ld] from the weight-streaming GEMM,
+// csrc/skinny_gemm.hip lk_ws_scores_f32): one workgroup per (chunk of 4096 rows, query)
+// normalises dot / (|q| |c| + 1e-9) and extracts the chunk's top-k (score desc, index
+// asc) by k rounds of block-wide argmax.
+constexpr int SCH = 4096;
+
+__global__ __launch_bounds__(256) void score_topk_kernel(const float* __restrict__ scores, long ld,
+                                                         const float* __restrict__ cnorm,
+                                                         const float* __restrict__ qnorm, long N, int K,
+                                                         float* __restrict__ part_s, int* __restrict__ part_i,
+                                                         int nchunks) {
+  __shared__ float rs[4];
+  __shared__ int ri[4];
+  const int q = blockIdx.y, c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int PER = SCH / 256;
+  const long base = (long)c * SCH;
+  const float qn = qnorm[q];
+  float v[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const long d = base + j * 256 + tid;
+    v[j] = d < N ? scores[(long)q * ld + d] / (qn * cnorm[d] + 1e-9f) : -INFINITY;
+  }
+  float* ps = part_s + ((long)q * nchunks + c) * K;
+  int* pi = part_i + ((long)q * nchunks + c) * K;
+  for (int kk = 0; kk < K; ++kk) {
+    float bs = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int idx = (int)(base + j * 256 + tid);
+      if (better(v[j], idx, bs, bi)) {
+        bs = v[j];
+        bi = idx;
+      }
+    }
+    wave_argmax(bs, bi);
+    if (lane == 0) {
+      rs[w] = bs;
+      ri[w] = bi;
+    }
+    __syncthreads();
+    float fs = rs[0];
+    int fi = ri[0];
+#pragma unroll
+    for (int j = 1; j < 4; ++j)
+      if (better(rs[j], ri[j], fs, fi)) {
+        fs = rs[j];
+        fi = ri[j];
+      }
+    if (tid == 0) {
+      ps[kk] = fs;
+      pi[kk] = fs == -INFINITY ? -1 : fi;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      if ((int)(base + j * 256 + tid) == fi) v[j] = -INFINITY;
+    __syncthreads();
+  }
+}
+
 // merge: one workgroup per query over `ncand` (score, idx) candidates
 __global__ __launch_bounds__(256) void knn_merge_kernel(const float* __restrict__ cs,
                                                         const int* __restrict__ ci, int ncand,
@@ -211,6 +272,17 @@ int lk_knn_partial(const bf16_t* corpus, const float* cnorm, long N, int D, cons
     case 1024: knn_partial_kernel<1024><<<grid, 256, 0, st>>>(corpus, cnorm, N, queries, qnorm, nq, K, part_s, part_i, nb); break;
     default: return -2;
   }
+  return 0;
+}
+
+int lk_knn_score_chunks(long N) { return (int)((N + SCH - 1) / SCH); }
+
+int lk_knn_score_topk(const float* scores, long ld, const float* cnorm, const float* qnorm, long N, int nq, int K,
+                      float* part_s, int* part_i, hipStream_t st) {
+  if (N <= 0 || nq <= 0) return 0;
+  if (K < 1 || K > 64) return -1;
+  const int nc = lk_knn_score_chunks(N);
+  score_topk_kernel<<<dim3(nc, nq), 256, 0, st>>>(scores, ld, cnorm, qnorm, N, K, part_s, part_i, nc);
   return 0;
 }
 

@@ -260,7 +260,10 @@ template <int MT, int BN, bool SWIGLU>
 __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict__ X, long ldx,
                                                         const bf16_t* __restrict__ W, int M, int K, int ks,
                                                         int n_tiles, int swiglu_I, bf16_t* __restrict__ out,
-                                                        long ldo, float* __restrict__ part, long part_ld) {
+                                                        long ldo, float* __restrict__ part, long part_ld,
+                                                        long n_rows) {
+  // n_rows: valid W rows (the last column tile may be partial: kNN over a corpus of
+  // any size); loads clamp to the last row, stores are masked
   constexpr int ROWS = 16 * MT;          // padded M
   constexpr int MTW = MT / 4;            // row tiles per wave
   constexpr int NT = BN / 16;            // column tiles per wave
@@ -299,7 +302,7 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
 #pragma unroll
   for (int i = 0; i < LW; ++i) {
     const int row = (w * LW + i) * 8 + lrow;
-    wsrc[i] = W + wrow(row) * K + kbase + ((lch ^ wsz(row)) * 8);
+    wsrc[i] = W + min(wrow(row), n_rows - 1) * K + kbase + ((lch ^ wsz(row)) * 8);
   }
   auto issue = [&](int st) {
     unsigned char* base = smem + (st % NS) * SB;
@@ -373,11 +376,16 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
         }
       } else if (split) {
 #pragma unroll
-        for (int n = 0; n < NT; ++n)
-          part[(long)s * M * part_ld + (long)row * part_ld + wrow(16 * n + r)] = acc[m][n][i];
+        for (int n = 0; n < NT; ++n) {
+          const long col = wrow(16 * n + r);
+          if (col < n_rows) part[(long)s * M * part_ld + (long)row * part_ld + col] = acc[m][n][i];
+        }
       } else {
 #pragma unroll
-        for (int n = 0; n < NT; ++n) out[(long)row * ldo + (long)t * BN + 16 * n + r] = f2bf(acc[m][n][i]);
+        for (int n = 0; n < NT; ++n) {
+          const long col = (long)t * BN + 16 * n + r;
+          if (col < n_rows) out[(long)row * ldo + col] = f2bf(acc[m][n][i]);
+        }
       }
     }
   }
@@ -385,7 +393,7 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
 
 template <int MT, int BN, bool SWIGLU>
 void launch_ws(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks, int S, int n_tiles, int I,
-               bf16_t* out, long ldo, float* part, long part_ld, hipStream_t st) {
+               bf16_t* out, long ldo, float* part, long part_ld, long n_rows, hipStream_t st) {
   constexpr size_t lds = (size_t)ws_stages(MT, BN) * (16 * MT * 128 + BN * 128);
   auto kern = wsgemm_kernel<MT, BN, SWIGLU>;
   static bool attr = false;
@@ -394,16 +402,17 @@ void launch_ws(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks,
                               (int)lds);
     attr = true;
   }
-  kern<<<n_tiles * S, 256, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld);
+  kern<<<n_tiles * S, 256, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows);
 }
 
 template <bool SWIGLU>
 int dispatch_ws(int MT, int BN, const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks, int S,
-                int n_tiles, int I, bf16_t* out, long ldo, float* part, long part_ld, hipStream_t st) {
-#define LK_WS(mt, bn)                                                                               \
-  if (MT == mt && BN == bn) {                                                                       \
-    launch_ws<mt, bn, SWIGLU>(x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, part, part_ld, st);     \
-    return 0;                                                                                       \
+                int n_tiles, int I, bf16_t* out, long ldo, float* part, long part_ld, hipStream_t st,
+                long n_rows = 1L << 40) {
+#define LK_WS(mt, bn)                                                                                   \
+  if (MT == mt && BN == bn) {                                                                           \
+    launch_ws<mt, bn, SWIGLU>(x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, part, part_ld, n_rows, st); \
+    return 0;                                                                                           \
   }
   LK_WS(4, 64) LK_WS(4, 128) LK_WS(8, 64) LK_WS(8, 128) LK_WS(16, 64) LK_WS(16, 128)
 #undef LK_WS
@@ -494,6 +503,20 @@ int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, i
   }
   LK_CHECK_LAUNCH();
   return 0;
+}
+
+// f32 X W^T for a W of any row count (kNN scores: X = queries, W = corpus rows):
+// out[M, N] with row stride ldo; one pass over W, no split-K.
+int lk_ws_scores_f32(const bf16_t* x, long ldx, const bf16_t* w, int M, long N, int K, float* out, long ldo,
+                     hipStream_t st) {
+  if (M < 1 || M > 256 || N < 1 || K % 64 || K < 64) return -1;
+  const int BN = 128;
+  const long tiles = (N + BN - 1) / BN;
+  if (tiles > (1L << 30)) return -1;
+  const int MT = M <= 64 ? 4 : M <= 128 ? 8 : 16;
+  const int rc = dispatch_ws<false>(MT, BN, x, ldx, w, M, K, K, 1, (int)tiles, 0, nullptr, 0, out, ldo, st, N);
+  LK_CHECK_LAUNCH();
+  return rc;
 }
 
 int lk_skinny_splits(int M, int N, int K, int swiglu) {

@@ -198,7 +198,10 @@ def test_flash_softmax_spike():
 
 
 @pytest.mark.parametrize("N,D", [(1, 384), (1000, 768), (70000, 768), (5000, 1024), (3000, 128), (777, 256), (2000, 512)])
-def test_knn_topk(hip, N, D):
+@pytest.mark.parametrize("fused", [False, True])
+def test_knn_topk(hip, N, D, fused):
+    """fused=False: the GEMM-scores path (weight-streaming kernel + chunked top-k);
+    fused=True: the single-pass MFMA kernel with in-LDS top-k."""
     torch.manual_seed(11)
     corpus = torch.randn(N, D, device=DEV).to(torch.bfloat16)
     if N > 10:
@@ -210,7 +213,7 @@ def test_knn_topk(hip, N, D):
     qn = hip.row_norms(qs)
     _close(cn, corpus.float().norm(dim=-1), 1e-2, 1e-3, "row norms")
     K = 10
-    s, i = hip.knn_topk(corpus, cn, qs, qn, K)
+    s, i = hip.knn_topk(corpus, cn, qs, qn, K, fused)
     sc = ref.cosine_scores(corpus.float().cpu(), cn.cpu(), qs.float().cpu(), qn.cpu())
     rs, ri = ref.stable_topk(sc, K)
     kk = min(K, N)
