@@ -47,10 +47,13 @@ class TPGroup:
         """Greedy token ids from vocab-parallel logits [R, V/tp]: local (max, argmax),
         all-gather of R (value, id) pairs per rank instead of the [R, V] logits, pick the
         max (first rank on ties = lowest id, the single-GPU argmax order)."""
-        vals, idx = local_logits.float().max(dim=-1)
-        idx = idx + vocab_lo
+        from .. import ops
+
+        idx = ops.select_tokens(local_logits).long()  # HIP argmax on the bf16 logits (first max)
         if self.size == 1:
-            return idx.int()
+            return (idx + vocab_lo).int()
+        vals = local_logits.gather(1, idx[:, None]).squeeze(1).float()
+        idx = idx + vocab_lo
         v = self.all_gather_cat(vals[None], dim=0)
         i = self.all_gather_cat(idx[None], dim=0)
         k = v.argmax(dim=0)
