@@ -8,12 +8,25 @@ once per step by the model runner, then shared by every layer.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Optional
 
 import torch
 
 from .. import ops
+
+# Mixed (chunked-prefill + decode) steps: run the memory-bound paged-decode kernel on a
+# side HIP stream concurrently with the MFMA-bound flash prefill of the same layer.
+OVERLAP_ATTN = os.environ.get("LK_OVERLAP_ATTN", "0") == "1"  # measured neutral on MI355X (off)
+_side: dict = {}
+
+
+def _side_stream(device):
+    s = _side.get(device)
+    if s is None:
+        s = _side[device] = torch.cuda.Stream(device)
+    return s
 
 
 @dataclass
@@ -59,16 +72,31 @@ def paged_attention(qkv: torch.Tensor, k_cache, v_cache, meta: AttnMeta, Hq: int
     if out is None:
         out = torch.empty(T, Hq * D, dtype=qkv.dtype, device=qkv.device)
     Tp = meta.num_prefill_tokens
+    Bd = meta.num_decode
+
+    def decode():
+        q = qkv[Tp:Tp + Bd, : Hq * D].view(Bd, Hq, D)
+        o = out[Tp:Tp + Bd].view(Bd, Hq, D)
+        ops.paged_decode(q, k_cache, v_cache, meta.block_tables_d, meta.ctx_lens_d, scale,
+                         meta.max_splits, meta.part_o, meta.part_ml, out=o, split=meta.decode_split)
+
+    side = None
+    if (Tp and Bd and OVERLAP_ATTN and qkv.is_cuda and not torch.cuda.is_current_stream_capturing()):
+        cur = torch.cuda.current_stream(qkv.device)
+        side = _side_stream(qkv.device)
+        side.wait_stream(cur)  # Q and the freshly written K/V are ready
+        with torch.cuda.stream(side):
+            decode()
+        qkv.record_stream(side)
+        out.record_stream(side)
     if Tp:
         meta.ensure_tiles(Hq, Hkv, qkv.device)
         ops.flash_prefill(qkv[:Tp, : Hq * D], k_cache, v_cache, meta.cu_q, Hq, Hkv, D, scale, True,
                           block_tables=meta.block_tables_p, ctx_lens=meta.ctx_lens_p,
                           q_lens_cpu=meta.q_lens_cpu, ctx_lens_cpu=meta.ctx_lens_cpu,
                           tiles=meta.tiles, out=out[:Tp])
-    Bd = meta.num_decode
-    if Bd:
-        q = qkv[Tp:Tp + Bd, : Hq * D].view(Bd, Hq, D)
-        o = out[Tp:Tp + Bd].view(Bd, Hq, D)
-        ops.paged_decode(q, k_cache, v_cache, meta.block_tables_d, meta.ctx_lens_d, scale,
-                         meta.max_splits, meta.part_o, meta.part_ml, out=o, split=meta.decode_split)
+    if side is not None:
+        torch.cuda.current_stream(qkv.device).wait_stream(side)
+    elif Bd:
+        decode()
     return out
