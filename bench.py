@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: BASELINE config 1 plumbing run (fp32 torch reference ops, gloo), e.g. "
+                         "--device cpu --model opt-125m --embedder minilm-l6 --docs 1000")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -116,12 +119,24 @@ def main():
     from llm_kubernetes_minikube_sharp4dev_amd.rag.index import RagChunk, RagIndex
     from llm_kubernetes_minikube_sharp4dev_amd.rag.synthetic import make_queries
 
-    assert torch.cuda.is_available(), "bench.py needs an MI355X"
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    _ext.lib()  # fail loudly if the HIP library is not built
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    on_gpu = args.device == "cuda"
+    if on_gpu:
+        assert torch.cuda.is_available(), "bench.py needs an MI355X (or --device cpu)"
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        _ext.lib()  # fail loudly if the HIP library is not built
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
+    else:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
+    wdtype = torch.bfloat16 if on_gpu else torch.float32
     tpg = new_tp_groups(args.tp) if args.tp > 1 else SINGLE
     leader = tpg.rank == 0
     n_replicas = world // args.tp
@@ -131,23 +146,23 @@ def main():
 
     # ---- embedder + index build (embedding work sharded over ALL ranks, all-gather over RCCL;
     # every replica driver then holds the whole corpus in HBM: 1M x 768 bf16 = 1.5 GB)
-    enc = build_encoder(args.embedder, device=dev, seed=args.seed)
+    enc = build_encoder(args.embedder, device=dev, seed=args.seed, dtype=wdtype)
     emb_engine = EmbeddingEngine(enc, tok, name=args.embedder, max_tokens_per_batch=131072)
     n = len(chunks)
     per = (n + world - 1) // world
     lo, hi = min(n, rank * per), min(n, (rank + 1) * per)
     t0 = time.perf_counter()
     mine = emb_engine.embed([c[2] for c in chunks[lo:hi]])
-    full = torch.zeros((per * world, enc.cfg.hidden), dtype=torch.bfloat16, device=dev)
-    shard = torch.zeros((per, enc.cfg.hidden), dtype=torch.bfloat16, device=dev)
-    shard[: hi - lo] = mine.to(torch.bfloat16)
+    full = torch.zeros((per * world, enc.cfg.hidden), dtype=wdtype, device=dev)
+    shard = torch.zeros((per, enc.cfg.hidden), dtype=wdtype, device=dev)
+    shard[: hi - lo] = mine.to(wdtype)
     if world > 1:
         dist.all_gather_into_tensor(full, shard)
     else:
         full = shard
     corpus = full[:n].contiguous()
     del full, shard, mine
-    torch.cuda.synchronize()
+    sync()
     t_index = time.perf_counter() - t0
     index = RagIndex(LocalEmbedder(emb_engine), backend="gpu", device=str(dev))
     index.chunks = [RagChunk(i, s, t) for i, s, t in chunks]
@@ -157,14 +172,17 @@ def main():
 
     # ---- generator + engine
     t0 = time.perf_counter()
-    llm = build_decoder(args.model, device=dev, seed=args.seed, tp=tpg)
-    torch.cuda.synchronize()
+    llm = build_decoder(args.model, device=dev, seed=args.seed, tp=tpg, dtype=wdtype)
+    sync()
     log(rank, f"{args.model} random-init (tp={args.tp}) in {time.perf_counter() - t0:.1f}s")
     # continuous: ~4k-token steps keep most steps mixed (decode rows ride on the prefill
     # GEMMs) without starving decode (profiles/r1_sched_sweep.md)
     mbt = args.max_batched_tokens or (4096 if args.mode == "continuous" else 65536)
     runner_kw = dict(block_size=16, max_model_len=8192, max_num_seqs=max(args.batch, 64), kv_cache_gb=args.kv_gb,
-                     use_graphs=not args.no_graphs)
+                     use_graphs=on_gpu and not args.no_graphs)
+    if not on_gpu:
+        runner_kw.pop("kv_cache_gb")
+        runner_kw["num_blocks"] = max(256, args.batch * 80)
     engine_kw = dict(max_num_batched_tokens=mbt, enable_prefix_caching=not args.no_prefix_cache, eos_ids=set())
     params = SamplingParams.greedy(args.max_new_tokens, ignore_eos=True)
     results, trace, elapsed, tim_setup = [], [], 0.0, 0.0
@@ -175,11 +193,11 @@ def main():
     else:
         if args.tp > 1:
             engine = make_tp_engine(llm, tpg, tok, engine_kw=engine_kw, **runner_kw)
-            if not args.no_graphs:
+            if runner_kw["use_graphs"]:
                 tp_capture_all(engine, max_batch=max(args.batch, 1), variants=(True,))
         else:
             engine = LLMEngine(llm, tok, **runner_kw, **engine_kw)
-            if not args.no_graphs:
+            if runner_kw["use_graphs"]:
                 engine.runner.capture_all(max_batch=max(args.batch, 1), variants=(True,))
         k8s = FakeCluster.default()
         rag = RagAgentPipeline(index, engine, tok, k8s, cfg)
@@ -225,7 +243,7 @@ def main():
 
         if world > 1:
             tp_barrier(engine)
-        torch.cuda.synchronize()
+        sync()
         engine.step_trace = []
         t0 = time.perf_counter()
         if load is not None:
@@ -233,7 +251,7 @@ def main():
         else:
             for _ in range(args.steps):
                 results.extend(batch_step())
-        torch.cuda.synchronize()
+        sync()
         if world > 1:
             tp_barrier(engine)
         elapsed = time.perf_counter() - t0
@@ -293,12 +311,12 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if on_gpu else "fp32",
             "data": f"synthetic ({args.docs} runbook docs -> {n} chunks; random-init weights)",
             "p50_latency_ms": round(p50, 1) if p50 is not None else None,
             "p90_latency_ms": round(p90, 1) if p90 is not None else None,
             "config": {
-                "model": f"{args.model} (bf16, TP={args.tp}) + {args.embedder} embedder",
+                "model": f"{args.model} ({'bf16' if on_gpu else 'fp32, CPU'}, TP={args.tp}) + {args.embedder} embedder",
                 "workload": args.workload,
                 "global_batch": args.batch * n_replicas,
                 "seq_len": round(avg_prompt, 1),
