@@ -1,0 +1,58 @@
+"""bench.py contract on the CPU (gloo): one JSON line with the required fields, for a
+single rank and for 2-rank DP / TP launches through torch.distributed.run (the same
+launcher and rendezvous the driver uses on the 8-GPU node)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(extra, nproc=1, timeout=600):
+    args = ["--device", "cpu", "--model", "llama-tiny", "--embedder", "bert-tiny", "--docs", "8", "--batch", "2",
+            "--steps", "1", "--warmup", "1", "--max-new-tokens", "3", *extra]
+    if nproc == 1:
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), *args]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+               "--gpus", str(nproc), *args]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd="/tmp", env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert REQUIRED <= set(d)
+    assert {"model", "global_batch", "seq_len", "parallelism"} <= set(d["config"])
+    return d
+
+
+@pytest.mark.parametrize("workload", ["rag", "agent"])
+def test_bench_single_rank_json(workload):
+    d = _run(["--workload", workload])
+    assert d["n_gpus"] == 1 and d["value"] > 0 and d["config"]["parallelism"] == "dp1"
+
+
+def test_bench_two_rank_dp():
+    d = _run([], nproc=2)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 4
+
+
+def test_bench_two_rank_tp():
+    d = _run(["--tp", "2"], nproc=2)
+    assert d["config"]["parallelism"] == "tp2" and d["config"]["global_batch"] == 2 and d["value"] > 0
