@@ -254,14 +254,6 @@ def _decode_gemm_kind(x, w, swiglu: bool) -> Optional[str]:
     return None
 
 
-def _skinny_wanted(M: int, N: int, swiglu: bool) -> bool:  # kept for tests / tooling
-    return M <= SKINNY_MAX_M
-
-
-def _skinny_ok(x, w, swiglu: bool) -> bool:
-    return _decode_gemm_kind(x, w, swiglu) is not None
-
-
 def linear(x, w, b=None):
     """Projection GEMM: decode-sized batches (M <= SKINNY_MAX_M) on the hand-written
     weight-streaming MFMA kernel, everything else on hipBLASLt through torch."""

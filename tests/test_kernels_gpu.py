@@ -309,9 +309,9 @@ def test_skinny_swiglu_matches_unfused(hip, M, IK):
 def test_linear_dispatch_uses_skinny(hip):
     x = torch.randn(8, 4096, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(6144, 4096, device=DEV, dtype=torch.bfloat16) * 0.05
-    assert ops._skinny_ok(x, w, False)
+    assert ops._decode_gemm_kind(x, w, False) == "skinny"
     _close(ops.linear(x, w), x.float() @ w.float().t(), 0.02, 0.01)
-    assert not ops._skinny_ok(torch.randn(512, 4096, device=DEV, dtype=torch.bfloat16), w, False)
+    assert ops._decode_gemm_kind(torch.randn(512, 4096, device=DEV, dtype=torch.bfloat16), w, False) is None
     x128 = torch.randn(128, 4096, device=DEV, dtype=torch.bfloat16)
     assert ops._decode_gemm_kind(x128, w, False) == "ws"
     _close(ops.linear(x128, w), x128.float() @ w.float().t(), 0.02, 0.01)
