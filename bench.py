@@ -68,6 +68,9 @@ def parse():
                     help="token budget per engine step (default: 4096 continuous, 65536 batch)")
     ap.add_argument("--admit-chunk", type=int, default=8,
                     help="continuous mode: requests retrieved + admitted together (batched embed/kNN)")
+    ap.add_argument("--constrained", action="store_true",
+                    help="tool-call grammar (engine/constrained.py): random weights then emit valid tool calls, so "
+                         "every request also runs the k8s dispatch / gating path (the reference decodes unconstrained)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
@@ -185,6 +188,14 @@ def main():
         runner_kw["num_blocks"] = max(256, args.batch * 80)
     engine_kw = dict(max_num_batched_tokens=mbt, enable_prefix_caching=not args.no_prefix_cache, eos_ids=set())
     params = SamplingParams.greedy(args.max_new_tokens, ignore_eos=True)
+    if args.constrained:
+        from llm_kubernetes_minikube_sharp4dev_amd.engine.constrained import tool_call_processor
+
+        # namespaces from the RAG allowlist, deployment names from the (fake) cluster,
+        # pod names free-form (<= 16 chars) -- keeps a call within --max-new-tokens
+        params.logits_processor = tool_call_processor(
+            tok, max_str=16, enums={"namespace": list(cfg.agent.allowed_namespaces) + ["default"],
+                                    "name": ["echoserver", "api", "web", "worker"]})
     results, trace, elapsed, tim_setup = [], [], 0.0, 0.0
 
     if not leader:
@@ -328,7 +339,7 @@ def main():
                 "admit_chunk": args.admit_chunk if args.mode == "continuous" else None,
                 "corpus_chunks": n,
                 "max_new_tokens": args.max_new_tokens,
-                "decoding": "greedy, ignore_eos",
+                "decoding": "greedy, ignore_eos" + (", tool-call grammar" if args.constrained else ""),
                 "prefix_caching": not args.no_prefix_cache,
                 "hip_graphs": not args.no_graphs,
                 "avg_cached_prefix_tokens": round(statistics.mean(pre), 1) if pre else 0,

@@ -213,10 +213,12 @@ class ToolCallGrammar:
     """Constrains output to ``{"action":"<tool>"[,"field":...]}``.  Fields per tool from
     TOOL_FIELDS; strings are k8s names (``[a-z0-9-.]{1,max_str}``), ints 1-2 digits."""
 
-    def __init__(self, tok, tools: Optional[dict] = None, max_str: int = 24):
+    def __init__(self, tok, tools: Optional[dict] = None, max_str: int = 24, enums: Optional[dict] = None):
         self.tok = tok
         self.tools = tools or TOOL_FIELDS
         self.max_str = max_str
+        # field name -> allowed string values (e.g. namespace -> the RAG allowlist)
+        self.enums = {k: list(v) for k, v in (enums or {}).items()}
         self.tt = _TokenTable.get(tok)
         texts = self.tt.texts
         self.name_tokens = [i for i, t in enumerate(texts) if t and set(t) <= K8S_CHARS]
@@ -228,10 +230,16 @@ class ToolCallGrammar:
         self._prefix_cache: dict[str, list] = {}
 
     def _literal_tokens(self, rest: str) -> list:
-        """Tokens whose text is a non-empty prefix of ``rest``."""
+        """Tokens for a forced literal: those spelling the LONGEST prefix of ``rest`` the
+        vocabulary has (the canonical tokenisation a tokenizer would produce; a forced
+        literal is not a choice, so fast-forwarding it keeps calls short)."""
         c = self._prefix_cache.get(rest)
         if c is None:
-            c = [i for k in range(1, len(rest) + 1) for i in self.by_text.get(rest[:k], ())]
+            c = []
+            for k in range(len(rest), 0, -1):
+                c = list(self.by_text.get(rest[:k], ()))
+                if c:
+                    break
             if len(self._prefix_cache) < 8192:
                 self._prefix_cache[rest] = c
         return c
@@ -244,6 +252,9 @@ class ToolCallGrammar:
         prog.append(("lit", action + '"'))
         for name, kind in self.tools[action]:
             prog.append(("lit", f',"{name}":' + ('"' if kind == "str" else "")))
+            if kind == "str" and name in self.enums:
+                prog.append(("enum", name))
+                continue  # the enum step consumes its closing quote
             prog.append((kind,))
             if kind == "str":
                 prog.append(("lit", '"'))
@@ -282,6 +293,19 @@ class ToolCallGrammar:
                 if seg != lit:
                     return self.tt.eos or [0]
                 pos += len(lit)
+            elif step[0] == "enum":
+                vals = self.enums[step[1]]
+                seg = s[pos:]
+                q2 = seg.find('"')
+                if q2 < 0:  # still choosing the value
+                    out = set()
+                    for v in vals:
+                        if v.startswith(seg):
+                            out.update(self._literal_tokens((v + '"')[len(seg):]))
+                    return sorted(out) or (self.tt.eos or [0])
+                if seg[:q2] not in vals:
+                    return self.tt.eos or [0]
+                pos += q2 + 1
             else:
                 kind = step[0]
                 m = re.match(r"[a-z0-9\-.]*" if kind == "str" else r"\d*", s[pos:])
@@ -292,6 +316,11 @@ class ToolCallGrammar:
                     toks = self.name_tokens if kind == "str" else self.digit_tokens
                     room = limit - len(val)
                     allowed = [i for i in toks if len(self.tt.texts[i]) <= room] if room > 0 else []
+                    if kind == "int":  # JSON integers: no leading zero ("0" alone is fine)
+                        if val == "0":
+                            allowed = []
+                        elif not val:
+                            allowed = [i for i in allowed if self.tt.texts[i] == "0" or self.tt.texts[i][0] != "0"]
                     if val:  # may close the field
                         allowed = allowed + self._literal_tokens(prog[si + 1][1])
                     return allowed or (self.tt.eos or [0])
@@ -301,5 +330,5 @@ class ToolCallGrammar:
         return self.tt.eos or [0]  # complete object -> only EOS
 
 
-def tool_call_processor(tok, tools: Optional[dict] = None):
-    return ToolCallGrammar(tok, tools)
+def tool_call_processor(tok, tools: Optional[dict] = None, max_str: int = 24, enums: Optional[dict] = None):
+    return ToolCallGrammar(tok, tools, max_str, enums)

@@ -10,6 +10,7 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import Callable, Optional
 
+import numpy as np
 import torch
 
 from .. import ops
@@ -70,14 +71,26 @@ class Sampler:
         self.step += 1
         B = logits.shape[0]
         dev = logits.device
-        # constrained decoding: mask everything outside the allowed set
+        # constrained decoding: mask everything outside the allowed set -- one host->device
+        # copy of all (row, token) pairs and one scatter for the whole batch
+        rows, toks, crow = [], [], []
         for i, p in enumerate(params):
             if p.logits_processor is not None:
                 allowed = p.logits_processor(histories[i])
                 if allowed is not None:
-                    mask = torch.full((logits.shape[1],), float("-inf"), device=dev)
-                    mask[torch.as_tensor(allowed, device=dev, dtype=torch.long)] = 0.0
-                    logits[i] += mask
+                    a = np.asarray(allowed, dtype=np.int64)
+                    rows.append(np.full(a.shape[0], len(crow), dtype=np.int64))
+                    toks.append(a)
+                    crow.append(i)
+        if crow:
+            V = logits.shape[1]
+            r = torch.from_numpy(np.concatenate(rows))
+            t = torch.from_numpy(np.concatenate(toks))
+            keep = (t >= 0) & (t < V)
+            mask = torch.full((len(crow), V), float("-inf"), device=dev)
+            mask[r[keep].to(dev, non_blocking=True), t[keep].to(dev, non_blocking=True)] = 0.0
+            sel = torch.as_tensor(crow, dtype=torch.long).to(dev, non_blocking=True)
+            logits.index_add_(0, sel, mask)
         # repetition penalty
         if any(p.repeat_penalty != 1.0 and p.repeat_last_n != 0 for p in params):
             W = max(max((p.repeat_last_n if p.repeat_last_n > 0 else len(h)) for p, h in zip(params, histories)), 1)

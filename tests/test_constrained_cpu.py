@@ -53,3 +53,34 @@ def test_json_grammar_random_walk_prefix_valid():
         assert json_feed_text(JSON_START, tok.decode(ids)) is not None
         if fin:
             json.loads(tok.decode(ids))
+
+
+def test_tool_call_grammar_enums_and_fast_forward():
+    """Enum-valued fields (namespace allowlist / deployment names) and forced literals
+    emitted as the longest vocabulary token; random walks always produce parseable,
+    strictly typed tool calls with allowlisted namespaces."""
+    import json
+    import random
+
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.constrained import tool_call_processor
+    from llm_kubernetes_minikube_sharp4dev_amd.models.tokenizer import builtin_tokenizer
+
+    tok = builtin_tokenizer()
+    ns = ["dev", "staging", "sharp4dev", "test-ns-giovanni", "default"]
+    proc = tool_call_processor(tok, max_str=16, enums={"namespace": ns, "name": ["echoserver", "api"]})
+    rng = random.Random(3)
+    eos = set(tok.eos_ids)
+    for _ in range(60):
+        ids = []
+        for _ in range(64):
+            allowed = proc(ids)
+            if set(allowed) <= eos:
+                break
+            ids.append(rng.choice(list(allowed)))
+        obj = json.loads(tok.decode(ids))
+        assert obj["action"] in ("list_pods", "get_logs", "scale_deployment", "cluster_context", "final_answer")
+        if "namespace" in obj:
+            assert obj["namespace"] in ns
+        if "replicas" in obj:
+            assert isinstance(obj["replicas"], int) and (obj["replicas"] == 0 or not str(obj["replicas"]).startswith("0"))
+        assert len(ids) <= 40
