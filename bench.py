@@ -20,9 +20,11 @@ replica; a step = ``--batch`` completions per replica).  Other BASELINE configs:
 With ``--tp T`` the world is split into TP groups of T ranks: the group's rank 0
 drives the engine (scheduler, retrieval, sampling) and the others follow in lockstep.
 
-Weights are random-init (no checkpoints offline), data synthetic; random weights
-never emit EOS on purpose, so every request generates exactly ``--max-new-tokens``
-tokens (the reference's tool call is ~20-60 tokens; default 48).
+Weights are random-init (no checkpoints offline), data synthetic.  Decoding is greedy
+under the tool-call grammar (so the random model's output is a valid, allowlisted tool
+call and the k8s action / gating path runs for every request), with EOS ignored so
+every request generates exactly ``--max-new-tokens`` tokens (the reference's tool call
+is ~20-60 tokens; default 48).
 
   python bench.py [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node 8 bench.py --gpus 8 ...
@@ -68,9 +70,10 @@ def parse():
                     help="token budget per engine step (default: 4096 continuous, 65536 batch)")
     ap.add_argument("--admit-chunk", type=int, default=8,
                     help="continuous mode: requests retrieved + admitted together (batched embed/kNN)")
-    ap.add_argument("--constrained", action="store_true",
-                    help="tool-call grammar (engine/constrained.py): random weights then emit valid tool calls, so "
-                         "every request also runs the k8s dispatch / gating path (the reference decodes unconstrained)")
+    ap.add_argument("--unconstrained", dest="constrained", action="store_false",
+                    help="decode without the tool-call grammar.  Default: the grammar (engine/constrained.py) makes "
+                         "the random-init model emit valid tool calls, so every request also runs the k8s dispatch "
+                         "and RAG gating path (same token counts; measured at the same speed)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
