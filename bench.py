@@ -208,11 +208,11 @@ def main():
         if args.tp > 1:
             engine = make_tp_engine(llm, tpg, tok, engine_kw=engine_kw, **runner_kw)
             if runner_kw["use_graphs"]:
-                tp_capture_all(engine, max_batch=max(args.batch, 1), variants=(True,))
+                tp_capture_all(engine, max_batch=max(args.batch, 1), variants=(not args.constrained,))
         else:
             engine = LLMEngine(llm, tok, **runner_kw, **engine_kw)
             if runner_kw["use_graphs"]:
-                engine.runner.capture_all(max_batch=max(args.batch, 1), variants=(True,))
+                engine.runner.capture_all(max_batch=max(args.batch, 1), variants=(not args.constrained,))
         k8s = FakeCluster.default()
         rag = RagAgentPipeline(index, engine, tok, k8s, cfg)
         agent = AgentPipeline(engine, tok, k8s, cfg)
