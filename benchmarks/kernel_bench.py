@@ -73,6 +73,24 @@ def case_prefill(B=32, L=1024, Hq=32, Hkv=8, D=128):
     return {"case": f"flash_prefill causal B{B} L{L} Hq{Hq} Hkv{Hkv} D{D}", "us": t * 1e6, "TFLOP/s": flops / t / 1e12}
 
 
+def case_prefill_chunk(B=6, q=643, ctx=930, Hq=32, Hkv=8, D=128):
+    """The in-situ shape of a mixed serving step: B prompts whose first ctx-q tokens are a
+    cached prefix (the shared system prompt), q new tokens each, K/V from the paged cache."""
+    kc, vc, bt = paged_setup(B, ctx, Hkv, D)
+    T = B * q
+    qq = torch.randn(T, Hq * D, device=DEV, dtype=torch.bfloat16)
+    cu = torch.arange(0, T + 1, q, dtype=torch.int32, device=DEV)
+    cl = torch.full((B,), ctx, dtype=torch.int32, device=DEV)
+    ts, tq = ops.prefill_tiles([q] * B, [ctx] * B, Hq // Hkv, True)
+    tiles = (torch.from_numpy(ts).to(DEV), torch.from_numpy(tq).to(DEV))
+    t = timeit(lambda: ops.flash_prefill(qq, kc, vc, cu, Hq, Hkv, D, 1 / math.sqrt(D), True, block_tables=bt,
+                                         ctx_lens=cl, tiles=tiles))
+    keys = sum(ctx - q + i + 1 for i in range(q))
+    flops = B * 4 * keys * D * Hq
+    return {"case": f"flash_prefill chunk B{B} q{q} ctx{ctx} Hq{Hq} Hkv{Hkv} D{D}", "us": t * 1e6,
+            "TFLOP/s": flops / t / 1e12}
+
+
 def case_encoder_attn(B=1600, L=80, H=12, D=64):
     T = B * L
     qkv = torch.randn(T, 3 * H * D, device=DEV, dtype=torch.bfloat16)
@@ -193,7 +211,8 @@ LLAMA8B_SHAPES = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]
 
 CASES = {
     "decode": lambda: [case_decode(), case_decode(B=128, ctx=1000), case_decode(B=8, ctx=3000)],
-    "prefill": lambda: [case_prefill(), case_prefill(B=8, L=4096)],
+    "prefill": lambda: [case_prefill(), case_prefill(B=8, L=4096), case_prefill_chunk()],
+    "prefill_chunk": lambda: [case_prefill_chunk()],
     "encoder": lambda: [case_encoder_attn()],
     "norm": lambda: [case_rmsnorm(), case_silu()],
     "knn": lambda: [case_knn(), case_knn(nq=8), case_knn(N=1_000_000, nq=8), case_knn(N=1_000_000, nq=128)],

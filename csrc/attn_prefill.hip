@@ -54,7 +54,7 @@ struct PrefillParams {
   const int* tile_q0;
   bf16_t* out;
   long os;
-  int Hq, Hkv, BS;
+  int Hq, Hkv, BS, bs_shift;  // BS is a power of two (paged cache block size)
   float scale_log2;
 };
 
@@ -119,8 +119,8 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(PrefillParams p) 
       const int key = min(kt + row, ctx - 1);  // clamp: masked later
       const bf16_t *kp, *vp;
       if constexpr (PAGED) {
-        const long blk = p.block_tables[(long)b * p.bt_stride + key / p.BS];
-        const long off = ((blk * p.Hkv + kvh) * p.BS + key % p.BS) * D + ch * 8;
+        const long blk = p.block_tables[(long)b * p.bt_stride + (key >> p.bs_shift)];
+        const long off = (((blk * p.Hkv + kvh) << p.bs_shift) + (key & (p.BS - 1))) * D + ch * 8;
         kp = p.k + off;
         vp = p.v + off;
       } else {
@@ -141,6 +141,22 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(PrefillParams p) 
     }
   };
 
+  // loop-invariant LDS offsets (elements): the swizzle of K row 32m + r and of the
+  // V^T rows 32m + 16s2 + 4h + qq (+8) depends only on the lane, so the tile loop
+  // addresses LDS with per-lane bases plus compile-time row offsets.
+  int koff[KK];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) koff[kk] = r * D + k_swz<D>(r, 2 * kk + h) * 8;
+  const int g16 = lane >> 4, li = lane & 15;
+  const int qq = li >> 2, pp = li & 3;  // this lane supplies row qq, cols 4pp..4pp+3
+  int voff[ND];
+#pragma unroll
+  for (int n = 0; n < ND; ++n) {
+    const int c0 = 32 * n + 16 * (g16 & 1) + 4 * pp;
+    const int r0 = 4 * h + qq;
+    voff[n] = r0 * D + v_swz<D>(r0, c0 >> 3) * 8 + (c0 & 7);
+  }
+
   const int ntiles = (kend + KT - 1) / KT;
   if (ntiles > 0) gload(0);
   for (int t = 0; t < ntiles; ++t) {
@@ -156,79 +172,85 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(PrefillParams p) 
     for (int m = 0; m < 2; ++m) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[m][i] = 0.f;
-      const int krow = 32 * m + r;
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
-        const short8 a =
-            *reinterpret_cast<const short8*>(Ks + krow * D + k_swz<D>(krow, 2 * kk + h) * 8);
+        const short8 a = *reinterpret_cast<const short8*>(Ks + 32 * m * D + koff[kk]);
         s[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[kk], s[m], 0, 0, 0);
       }
     }
 
-    // ---- mask + online softmax (this lane = query row qrow; 32 of the 64 keys)
+    // ---- mask + online softmax (this lane = query row qrow; 32 of the 64 keys).
+    // One uniform branch for the (rare) boundary tiles; the row max is taken on the
+    // raw scores and scaled once, the scale is folded into the exp2 argument (FMA).
     const bool need_mask = (kt + KT > ctx) || (CAUSAL && kt + KT - 1 > past + q0 + rg * 32);
     float mx = -INFINITY;
+    if (need_mask) {
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+      for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float x = s[m][i] * p.scale_log2;
-        if (need_mask) {
+        for (int i = 0; i < 16; ++i) {
           const int key = kt + 32 * m + (i & 3) + 8 * (i >> 2) + 4 * h;
           const bool ok = key < ctx && (!CAUSAL || key <= qpos);
-          x = ok ? x : -INFINITY;
+          s[m][i] = ok ? s[m][i] : -INFINITY;
+          mx = fmaxf(mx, s[m][i]);
         }
-        s[m][i] = x;
-        mx = fmaxf(mx, x);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    } else {
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[m][i]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * p.scale_log2;
     const float m_new = fmaxf(m_run, mx);
     const float base = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = exp2f(m_run - base);
+    // bare v_exp_f32 (softmax tolerates flushed denormals)
+    const float alpha = __builtin_amdgcn_exp2f(m_run - base);
     float rs = 0.f;
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float e = exp2f(s[m][i] - base);
+        const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(s[m][i], p.scale_log2, -base));
         s[m][i] = e;
         rs += e;
       }
     rs += __shfl_xor(rs, 32, 64);
     l_run = l_run * alpha + rs;
     m_run = m_new;
+    // rescale O only when some row's running max moved (wave-uniform branch; once the
+    // early tiles have found each row's max this is skipped)
+    if (!__all(alpha == 1.f)) {
 #pragma unroll
-    for (int n = 0; n < ND; ++n)
+      for (int n = 0; n < ND; ++n)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) o[n][i] *= alpha;
+        for (int i = 0; i < 16; ++i) o[n][i] *= alpha;
+    }
 
     // ---- P^T fragments (B operand): k-step (m, s2) = regs 8*s2 .. 8*s2+7 of s[m]
     short8 pf[2][2];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
+      for (int s2 = 0; s2 < 2; ++s2) {
+        uint4_t pk;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pf[m][s2][j] = (short)f2bf(s[m][8 * s2 + j]);
+        for (int j = 0; j < 4; ++j) pk[j] = pack_bf2(s[m][8 * s2 + 2 * j], s[m][8 * s2 + 2 * j + 1]);
+        pf[m][s2] = __builtin_bit_cast(short8, pk);
+      }
 
     // ---- O^T += V^T . P^T ; V^T fragments by transposed LDS reads.
     // element j of lane-half h in k-step (m,s2) is key 32m + 16s2 + 8(j>>2) + 4h + (j&3)
-    const int g16 = lane >> 4, li = lane & 15;
-    const int qq = li >> 2, pp = li & 3;  // this lane supplies row qq, cols 4pp..4pp+3
 #pragma unroll
     for (int n = 0; n < ND; ++n) {
-      const int c0 = 32 * n + 16 * (g16 & 1) + 4 * pp;  // column this lane addresses
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const int r0 = 32 * m + 16 * s2 + 4 * h + qq;
-          const int r1 = r0 + 8;
-          const bf16_t* a0 = Vs + r0 * D + v_swz<D>(r0, c0 >> 3) * 8 + (c0 & 7);
-          const bf16_t* a1 = Vs + r1 * D + v_swz<D>(r1, c0 >> 3) * 8 + (c0 & 7);
+          const bf16_t* a0 = Vs + (32 * m + 16 * s2) * D + voff[n];
+          const bf16_t* a1 = a0 + 8 * D;
           const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short_ptr)(a0));
           const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short_ptr)(a1));
-          const short8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const short8 a = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
           o[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pf[m][s2], o[n], 0, 0, 0);
         }
     }
@@ -265,8 +287,11 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
   const int G = Hq / Hkv;
   if (!(G == 1 || G == 2 || G % 4 == 0)) return -2;
   if (paged && (BS <= 0)) return -4;
+  if (paged && (BS & (BS - 1))) return -4;  // power-of-two cache blocks
+  int bs_shift = 0;
+  while ((1 << bs_shift) < BS) ++bs_shift;
   PrefillParams pr{q, qs, k, v, ks, vs, block_tables, bt_stride, cu_q, ctx_lens, tile_seq,
-                   tile_q0, out, os, Hq, Hkv, BS, scale * 1.4426950408889634f};
+                   tile_q0, out, os, Hq, Hkv, BS, bs_shift, scale * 1.4426950408889634f};
   const int WH = G >= 4 ? 4 : G;
   dim3 grid(ntiles, Hq / WH);
 #define L(DD, C, PG, W) flash_prefill_kernel<DD, C, PG, W><<<grid, 256, 0, st>>>(pr)
