@@ -200,6 +200,7 @@ def main():
             tok, max_str=16, enums={"namespace": list(cfg.agent.allowed_namespaces) + ["default"],
                                     "name": ["echoserver", "api", "web", "worker"]})
     results, trace, elapsed, tim_setup = [], [], 0.0, 0.0
+    load, load_host = None, {}
 
     if not leader:
         # TP follower: execute the driver's steps (and its barriers) until it says stop
@@ -259,6 +260,7 @@ def main():
             tp_barrier(engine)
         sync()
         engine.step_trace = []
+        load_host0 = dict(load.host_s) if load is not None else {}
         t0 = time.perf_counter()
         if load is not None:
             results.extend(load.run(args.steps * args.batch))
@@ -271,6 +273,7 @@ def main():
         elapsed = time.perf_counter() - t0
         trace, engine.step_trace = engine.step_trace, None
         if load is not None:
+            load_host = {k: v - load_host0[k] for k, v in load.host_s.items()}
             load.drain()
         if args.tp > 1:
             shutdown_tp(engine)
@@ -304,7 +307,14 @@ def main():
             statuses[str(r.status)] = statuses.get(str(r.status), 0) + 1
         dec_only = [t for t in trace if t[0] == 0]
         mixed = [t for t in trace if t[0] > 0]
+        host = {}
+        if trace:
+            host = {k: round(sum(t[i] for t in trace), 3) for k, i in
+                    (("schedule_s", 3), ("prepare_launch_s", 4), ("sample_sync_s", 5), ("post_s", 6))}
+        if load is not None:
+            host.update({f"load_{k}_s": round(v, 3) for k, v in load_host.items()})
         step_mix = {
+            "host_breakdown": host,
             "steps": len(trace),
             "decode_only_steps": len(dec_only), "decode_only_s": round(sum(t[2] for t in dec_only), 3),
             "mixed_steps": len(mixed), "mixed_s": round(sum(t[2] for t in mixed), 3),

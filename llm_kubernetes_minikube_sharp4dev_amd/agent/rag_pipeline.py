@@ -16,6 +16,8 @@ import time
 from dataclasses import dataclass, field
 from typing import Any, Optional
 
+import torch
+
 from .json_extract import extract_json_object
 from .policy import select_citations
 from .prompts import RAG_AGENT_SYSTEM, json_prompt, rag_agent_input
@@ -138,16 +140,49 @@ class ContinuousLoad:
         self.pipe, self.next_queries, self.params = pipe, next_queries, params
         self.concurrency, self.admit_chunk = concurrency, admit_chunk
         self.inflight: dict = {}
+        self.host_s = {"plan": 0.0, "step": 0.0, "finish": 0.0}  # wall time by phase
 
     def run(self, n_complete: int, on_done=None) -> list[RagAgentResult]:
+        """Step N's kernels run while the host admits new requests: step_begin launches
+        the step, admission (retrieval on a side HIP stream, prompt building,
+        tokenisation, add_request) overlaps it, step_end collects the tokens."""
         pipe = self.pipe
         done: list[RagAgentResult] = []
-        while len(done) < n_complete:
+        pending = None
+        dev = getattr(getattr(pipe.llm, "model", None), "device", None)
+        side = torch.cuda.Stream(dev) if dev is not None and dev.type == "cuda" else None
+        while len(done) < n_complete or pending is not None:
+            if pending is not None:
+                t_st = time.perf_counter()
+                pipe.llm.step_end(pending)
+                pending = None
+                t_fin = time.perf_counter()
+                self.host_s["step"] += t_fin - t_st
+                for rid in [r for r, v in self.inflight.items() if v[0].finished]:
+                    seq, p, ids, ctx, tim = self.inflight.pop(rid)
+                    r = pipe.finish_request(p, seq.output_ids, ctx)
+                    r.prompt_tokens = len(ids)
+                    r.timings = {**tim, **seq.metrics(), "e2e_s": time.perf_counter() - seq.arrival}
+                    done.append(r)
+                    if on_done is not None:
+                        on_done(r)
+                self.host_s["finish"] += time.perf_counter() - t_fin
+            if len(done) >= n_complete:
+                continue
+            if pipe.llm.has_work():
+                t_st = time.perf_counter()
+                pending = pipe.llm.step_begin()
+                self.host_s["step"] += time.perf_counter() - t_st
             free = self.concurrency - len(self.inflight)
-            if free >= min(self.admit_chunk, self.concurrency) or not self.inflight:
+            if free >= min(self.admit_chunk, self.concurrency) or (not self.inflight and pending is None):
                 qs = self.next_queries(free)
                 t_adm = time.perf_counter()
-                reqs, tim = pipe.plan_requests(qs)
+                if side is not None:
+                    with torch.cuda.stream(side):
+                        reqs, tim = pipe.plan_requests(qs)
+                else:
+                    reqs, tim = pipe.plan_requests(qs)
+                self.host_s["plan"] += time.perf_counter() - t_adm
                 for p, ids, ctx in reqs:
                     if ids is None:
                         done.append(pipe.finish_request(p, [], None))
@@ -155,15 +190,6 @@ class ContinuousLoad:
                     seq = pipe.llm.add_request(ids, self.params.__class__(**{**self.params.__dict__}))
                     seq.arrival = t_adm
                     self.inflight[seq.req_id] = (seq, p, ids, ctx, tim)
-            pipe.llm.step()
-            for rid in [r for r, v in self.inflight.items() if v[0].finished]:
-                seq, p, ids, ctx, tim = self.inflight.pop(rid)
-                r = pipe.finish_request(p, seq.output_ids, ctx)
-                r.prompt_tokens = len(ids)
-                r.timings = {**tim, **seq.metrics(), "e2e_s": time.perf_counter() - seq.arrival}
-                done.append(r)
-                if on_done is not None:
-                    on_done(r)
         return done
 
     def drain(self):

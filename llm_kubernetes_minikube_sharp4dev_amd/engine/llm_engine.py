@@ -76,35 +76,61 @@ class LLMEngine:
     @torch.inference_mode()
     def step(self) -> list:
         """One scheduler iteration.  Returns the sequences that produced a token."""
+        return self.step_end(self.step_begin())
+
+    @torch.inference_mode()
+    def step_begin(self):
+        """First half of a step: schedule, launch the forward (and the sampler's device
+        work; grammar masks are built on the host while the GPU runs) without waiting
+        for the device.  Host work placed between :meth:`step_begin` and
+        :meth:`step_end` (request admission, retrieval, tokenisation) overlaps the
+        step's kernels.  Returns an opaque pending step (None if nothing to do)."""
         with self.lock:
+            ts = time.perf_counter()
             batch = self.scheduler.schedule()
             # requests that could never fit were finished by the scheduler
             if batch.empty:
-                return []
+                return None
             t0 = time.perf_counter()
             # plain greedy steps get token ids straight from the model (no fp32 logits;
             # under TP an all-gather of (max, argmax) pairs instead of the vocab)
             greedy = all(_plain_greedy(sq.params) for sq, _, _ in batch.items)
             rows, logits = self.runner.forward_logits(batch.items, greedy)
+            t1 = time.perf_counter()
             for seq, start, n in batch.items:
                 seq.num_computed = start + n
                 self.scheduler.publish_blocks(seq)
-            out = []
+            ids = None
             if rows:
                 seqs = [s for s, _ in rows]
-                if greedy:
-                    ids = logits.tolist()
-                else:
-                    ids = self.sampler(logits, [s.params for s in seqs], [s.output_ids for s in seqs]).tolist()
-                now = time.perf_counter()
-                for seq, tid in zip(seqs, ids):
+                ids = logits if greedy else self.sampler(logits, [s.params for s in seqs],
+                                                         [s.output_ids for s in seqs])
+            return (batch, rows, ids, ts, t0, t1)
+
+    @torch.inference_mode()
+    def step_end(self, pending) -> list:
+        """Second half: wait for the sampled ids and append them (stop conditions,
+        streaming callbacks)."""
+        if pending is None:
+            return []
+        batch, rows, ids_t, ts, t0, t1 = pending
+        with self.lock:
+            out = []
+            t2 = time.perf_counter()
+            if rows:
+                ids = ids_t.tolist()
+                now = t2 = time.perf_counter()
+                for (seq, _), tid in zip(rows, ids):
                     self._append(seq, int(tid), now)
                     out.append(seq)
             self.steps += 1
             if self.step_trace is not None:
+                t3 = time.perf_counter()
                 npre = sum(n for sq, st, n in batch.items if st < len(sq.prompt_ids))
-                self.step_trace.append((npre, len(batch.items) - sum(
-                    1 for sq, st, n in batch.items if st < len(sq.prompt_ids)), time.perf_counter() - t0))
+                ndec = len(batch.items) - sum(1 for sq, st, n in batch.items if st < len(sq.prompt_ids))
+                # (prefill tokens, decode rows, step s, schedule s, prepare+launch s, sample+sync s, post s)
+                self.step_trace.append((npre, ndec, t3 - t0, t0 - ts, t1 - t0,
+                                        (t2 - t1) if rows else 0.0, (t3 - t2) if rows else 0.0))
             M.STEP_TOKENS.observe(batch.num_tokens)
             M.STEP_TIME.observe(time.perf_counter() - t0)
             M.KV_USAGE.set(self.allocator.usage())

@@ -19,6 +19,13 @@ from typing import Optional
 import numpy as np
 import torch
 
+try:  # native step-input builder (csrc/runtime/step_builder.cpp)
+    from ..native import runtime as _nrt
+
+    _native_rt = _nrt.load() if _nrt.available() and hasattr(_nrt.load(), "decode_rows") else None
+except Exception:  # pragma: no cover
+    _native_rt = None
+
 from .. import ops
 from ..models.attention import AttnMeta
 from ..utils.logging import get_logger
@@ -99,6 +106,27 @@ class ModelRunner:
         blk = np.asarray(table, dtype=np.int64)[pos // self.bs]
         return (blk * self.bs + pos % self.bs).astype(np.int32), pos.astype(np.int32)
 
+    def _decode_rows(self, dec, width, pad_to=0):
+        """(ids, positions, slots, ctx, block tables) of the decode rows; native
+        (csrc/runtime/step_builder.cpp) when the runtime is built."""
+        tables = [s.block_table for s, _, _ in dec]
+        starts = [st for _, st, _ in dec]
+        toks = [s.token_at(st) for s, st, _ in dec]
+        lens = [s.length for s, _, _ in dec]
+        if _native_rt is not None:
+            return _native_rt.decode_rows(tables, starts, toks, lens, self.bs, width, pad_to)
+        P = max(len(dec), pad_to)
+        ids = np.zeros(P, dtype=np.int32)
+        pos = np.zeros(P, dtype=np.int32)
+        slots = np.full(P, -1, dtype=np.int32)
+        ctx = np.ones(P, dtype=np.int32)
+        bt = np.zeros((P, width), dtype=np.int32)
+        for i, t in enumerate(tables):
+            bt[i, : len(t)] = t
+            ids[i], pos[i], ctx[i] = toks[i], starts[i], lens[i]
+            slots[i] = t[starts[i] // self.bs] * self.bs + starts[i] % self.bs
+        return ids, pos, slots, ctx, bt
+
     def _bt(self, tables, width):
         bt = np.zeros((len(tables), width), dtype=np.int32)
         for i, t in enumerate(tables):
@@ -134,38 +162,28 @@ class ModelRunner:
             r += n
             if start + n == seq.length:
                 rows.append((seq, r - 1))
-        for seq, start, n in dec:
-            ids.append(seq.token_at(start))
-            s, p = self._slots(seq.block_table, start, 1)
-            slots.append(s)
-            pos.append(p)
-            rows.append((seq, r))
-            r += 1
+        ctx_d = tables_d = None
+        if dec:
+            d_ids, d_pos, d_slots, ctx_d, tables_d = self._decode_rows(
+                dec, max(len(s.block_table) for s, _, _ in dec))
+            ids.extend(d_ids.tolist())
+            pos.append(d_pos)
+            slots.append(d_slots)
+            for seq, _, _ in dec:
+                rows.append((seq, r))
+                r += 1
         si = StepInputs(decode_graph=0, ids=np.asarray(ids, dtype=np.int32), positions=np.concatenate(pos),
                         slots=np.concatenate(slots), q_lens=q_lens, ctx_lens=ctx,
                         tables_p=self._bt(tables, max(len(t) for t in tables)) if pre else None,
-                        ctx_d=np.asarray([s.length for s, _, _ in dec], dtype=np.int32) if dec else None,
-                        tables_d=self._bt([s.block_table for s, _, _ in dec],
-                                          max(len(s.block_table) for s, _, _ in dec)) if dec else None,
+                        ctx_d=ctx_d, tables_d=tables_d,
                         num_decode=len(dec), logits_rows=np.asarray([row for _, row in rows], dtype=np.int64))
         return si, rows
 
     def _prepare_graph(self, items):
         B = len(items)
         Bg = self._graph_bucket(B)
-        ids = np.zeros(Bg, dtype=np.int32)
-        pos = np.zeros(Bg, dtype=np.int32)
-        slots = np.full(Bg, -1, dtype=np.int32)
-        ctx = np.ones(Bg, dtype=np.int32)
-        bt = np.zeros((Bg, self.max_blocks), dtype=np.int32)
-        rows = []
-        for i, (seq, start, n) in enumerate(items):
-            ids[i] = seq.token_at(start)
-            pos[i] = start
-            slots[i] = seq.block_table[start // self.bs] * self.bs + start % self.bs
-            ctx[i] = seq.length
-            bt[i, : len(seq.block_table)] = seq.block_table
-            rows.append((seq, i))
+        ids, pos, slots, ctx, bt = self._decode_rows(items, self.max_blocks, Bg)
+        rows = [(seq, i) for i, (seq, _, _) in enumerate(items)]
         si = StepInputs(decode_graph=Bg, ids=ids, positions=pos, slots=slots, ctx_d=ctx, tables_d=bt,
                         num_decode=B, logits_rows=np.arange(B, dtype=np.int64))
         return si, rows

@@ -132,3 +132,22 @@ def test_native_bpe_matches_hf_llama3_pretokenizer():
     assert enc is not None
     allt = texts + _adversarial_texts()
     assert enc.encode_batch(allt, 3) == [e.ids for e in hf.encode_batch(allt, add_special_tokens=False)]
+
+
+def test_native_decode_rows_matches_python():
+    import numpy as np
+
+    from llm_kubernetes_minikube_sharp4dev_amd.native import runtime as nrt
+
+    m = nrt.load()
+    rng = np.random.default_rng(0)
+    tables = [list(rng.integers(0, 1000, n)) for n in (3, 1, 7, 5)]
+    starts = [40, 3, 100, 79]
+    toks = [11, 12, 13, 14]
+    lens = [41, 4, 101, 80]
+    ids, pos, slots, ctx, bt = m.decode_rows([list(map(int, t)) for t in tables], starts, toks, lens, 16, 8, 8)
+    assert ids.shape == (8,) and bt.shape == (8, 8)
+    for i, t in enumerate(tables):
+        assert slots[i] == t[starts[i] // 16] * 16 + starts[i] % 16
+        assert list(bt[i, : len(t)]) == list(t) and not bt[i, len(t):].any()
+    assert list(slots[4:]) == [-1] * 4 and list(ctx[4:]) == [1] * 4 and list(ids[:4]) == toks
