@@ -52,7 +52,7 @@ MODEL_NAMES = {"llama-3-8b": "Llama-3-8B", "llama-3-70b": "Llama-3-70B", "opt-12
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=8, help="timed steps (continuous mode: a step = --batch completions per replica; 8 x 128 keeps the window-boundary noise of in-flight requests under 1%%)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=128,
                     help="requests per replica per step (= in-flight concurrency in continuous mode)")
@@ -323,6 +323,9 @@ def main():
         }
         tim = {k: statistics.mean(r.timings.get(k, 0.0) for r in results if r.timings)
                for k in ("embed_s", "knn_s", "prompt_s")} if results else {}
+        steps_acct = {k: round(statistics.mean(r.timings[k] for r in results if r.timings and r.timings.get(k) is not None), 2)
+                      for k in ("steps_queued", "steps_in_system", "steps_run")
+                      if any(r.timings and r.timings.get(k) is not None for r in results)}
         par = f"dp{n_replicas}" if args.tp == 1 else f"tp{args.tp}" + (f"xdp{n_replicas}" if n_replicas > 1 else "")
         out = {
             "metric": METRICS[args.workload].format(model=MODEL_NAMES.get(args.model, args.model)),
@@ -357,6 +360,7 @@ def main():
                 "hip_graphs": not args.no_graphs,
                 "avg_cached_prefix_tokens": round(statistics.mean(pre), 1) if pre else 0,
                 "stage_means_s": {k: round(v, 4) for k, v in tim.items()},
+                "engine_steps_per_request": steps_acct,
                 "step_mix_rank0": step_mix,
                 "index_build_s": round(t_index, 2),
                 "setup_s": round(tim_setup, 1),

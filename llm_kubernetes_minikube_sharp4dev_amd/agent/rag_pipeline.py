@@ -143,38 +143,40 @@ class ContinuousLoad:
         self.host_s = {"plan": 0.0, "step": 0.0, "finish": 0.0}  # wall time by phase
 
     def run(self, n_complete: int, on_done=None) -> list[RagAgentResult]:
-        """Step N's kernels run while the host admits new requests: step_begin launches
-        the step, admission (retrieval on a side HIP stream, prompt building,
-        tokenisation, add_request) overlaps it, step_end collects the tokens."""
+        """Pipelined engine steps (``LLMEngine.step_pipelined``): step N+1's forward is
+        enqueued before the host waits for step N, and admission (retrieval on a side
+        HIP stream, prompt building, tokenisation, add_request) runs while the device
+        works through both."""
         pipe = self.pipe
+        llm = pipe.llm
         done: list[RagAgentResult] = []
-        pending = None
-        dev = getattr(getattr(pipe.llm, "model", None), "device", None)
+        dev = getattr(getattr(llm, "model", None), "device", None)
         side = torch.cuda.Stream(dev) if dev is not None and dev.type == "cuda" else None
-        while len(done) < n_complete or pending is not None:
-            if pending is not None:
-                t_st = time.perf_counter()
-                pipe.llm.step_end(pending)
-                pending = None
-                t_fin = time.perf_counter()
-                self.host_s["step"] += t_fin - t_st
-                for rid in [r for r, v in self.inflight.items() if v[0].finished]:
-                    seq, p, ids, ctx, tim = self.inflight.pop(rid)
-                    r = pipe.finish_request(p, seq.output_ids, ctx)
-                    r.prompt_tokens = len(ids)
-                    r.timings = {**tim, **seq.metrics(), "e2e_s": time.perf_counter() - seq.arrival}
-                    done.append(r)
-                    if on_done is not None:
-                        on_done(r)
-                self.host_s["finish"] += time.perf_counter() - t_fin
+
+        def reap():
+            for rid in [r for r, v in self.inflight.items() if v[0].finished]:
+                seq, p, ids, ctx, tim = self.inflight.pop(rid)
+                r = pipe.finish_request(p, seq.output_ids, ctx)
+                r.prompt_tokens = len(ids)
+                r.timings = {**tim, **seq.metrics(), "e2e_s": time.perf_counter() - seq.arrival}
+                done.append(r)
+                if on_done is not None:
+                    on_done(r)
+
+        while len(done) < n_complete:
+            t_st = time.perf_counter()
+            if llm.has_work():
+                llm.step_pipelined()
+            else:
+                llm.flush()
+            t_fin = time.perf_counter()
+            self.host_s["step"] += t_fin - t_st
+            reap()
+            self.host_s["finish"] += time.perf_counter() - t_fin
             if len(done) >= n_complete:
-                continue
-            if pipe.llm.has_work():
-                t_st = time.perf_counter()
-                pending = pipe.llm.step_begin()
-                self.host_s["step"] += time.perf_counter() - t_st
+                break
             free = self.concurrency - len(self.inflight)
-            if free >= min(self.admit_chunk, self.concurrency) or (not self.inflight and pending is None):
+            if free >= min(self.admit_chunk, self.concurrency) or not self.inflight:
                 qs = self.next_queries(free)
                 t_adm = time.perf_counter()
                 if side is not None:
@@ -187,9 +189,11 @@ class ContinuousLoad:
                     if ids is None:
                         done.append(pipe.finish_request(p, [], None))
                         continue
-                    seq = pipe.llm.add_request(ids, self.params.__class__(**{**self.params.__dict__}))
+                    seq = llm.add_request(ids, self.params.__class__(**{**self.params.__dict__}))
                     seq.arrival = t_adm
                     self.inflight[seq.req_id] = (seq, p, ids, ctx, tim)
+        llm.flush()
+        reap()
         return done
 
     def drain(self):

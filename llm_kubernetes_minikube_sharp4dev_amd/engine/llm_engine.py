@@ -45,6 +45,8 @@ class LLMEngine:
         self.eos_ids = set(eos_ids)
         self.lock = threading.RLock()
         self.steps = 0
+        self.launches = 0
+        self._inflight = None  # the launched-and-sampled step not yet collected (step_pipelined)
         # optional per-step trace: (prefill tokens, decode rows, wall seconds) -- bench.py
         self.step_trace: Optional[list] = None
 
@@ -56,6 +58,7 @@ class LLMEngine:
         if req_id:
             seq.req_id = req_id
         seq.on_token = on_token
+        seq.step_arrival = self.launches
         budget = self.max_model_len - len(seq.prompt_ids)
         if budget <= 0:
             raise ValueError("prompt longer than max_model_len")
@@ -73,18 +76,51 @@ class LLMEngine:
         return self.scheduler.has_work()
 
     # ------------------------------------------------------------------ step
-    @torch.inference_mode()
-    def step(self) -> list:
-        """One scheduler iteration.  Returns the sequences that produced a token."""
-        return self.step_end(self.step_begin())
+    # A step is three phases: _launch (schedule, build the inputs, enqueue the forward),
+    # _sample (grammar masks on the host + the sampling kernels, then a non-blocking
+    # copy of the ids to pinned memory and an event), _collect (wait for that event,
+    # append the tokens, stop conditions, callbacks, prefix-cache publishing).
+    #
+    #   step()            launch -> sample -> collect: every token is on the host when
+    #                     it returns (server / tests / run_until_done).
+    #   step_pipelined()  launch(N+1) -> collect(N) -> sample(N+1): the forward of step
+    #                     N+1 is enqueued before the host waits for step N, its decode
+    #                     inputs gathered on the device from step N's ids, so the GPU
+    #                     never idles across the host's per-step work (stop checks,
+    #                     grammar masks, scheduling, input building, admission).  A
+    #                     request finishing by length is not stepped speculatively; one
+    #                     stopping on EOS / a stop string wastes one row of one step.
 
     @torch.inference_mode()
-    def step_begin(self):
-        """First half of a step: schedule, launch the forward (and the sampler's device
-        work; grammar masks are built on the host while the GPU runs) without waiting
-        for the device.  Host work placed between :meth:`step_begin` and
-        :meth:`step_end` (request admission, retrieval, tokenisation) overlaps the
-        step's kernels.  Returns an opaque pending step (None if nothing to do)."""
+    def step(self) -> list:
+        """One synchronous scheduler iteration.  Returns the sequences that got a token."""
+        out = self.flush()
+        nxt = self._launch()
+        if nxt is None:
+            return out
+        return out + self._collect(self._sample(nxt))
+
+    @torch.inference_mode()
+    def step_pipelined(self) -> list:
+        """One pipelined iteration; returns the sequences that got a token (from the
+        PREVIOUS launch).  Call :meth:`flush` when done.  Falls back to :meth:`step`
+        under tensor parallelism (the worker ranks replay host-built inputs)."""
+        if self.runner.step_hook is not None:
+            return self.step()
+        nxt = self._launch()
+        out = self._collect(self._inflight) if self._inflight is not None else []
+        self._inflight = self._sample(nxt) if nxt is not None else None
+        return out
+
+    @torch.inference_mode()
+    def flush(self) -> list:
+        """Collect the in-flight pipelined step, if any."""
+        if self._inflight is None:
+            return []
+        p, self._inflight = self._inflight, None
+        return self._collect(p)
+
+    def _launch(self):
         with self.lock:
             ts = time.perf_counter()
             batch = self.scheduler.schedule()
@@ -95,39 +131,57 @@ class LLMEngine:
             # plain greedy steps get token ids straight from the model (no fp32 logits;
             # under TP an all-gather of (max, argmax) pairs instead of the vocab)
             greedy = all(_plain_greedy(sq.params) for sq, _, _ in batch.items)
-            rows, logits = self.runner.forward_logits(batch.items, greedy)
-            t1 = time.perf_counter()
+            rows, out = self.runner.forward_logits(batch.items, greedy)
             for seq, start, n in batch.items:
                 seq.num_computed = start + n
-                self.scheduler.publish_blocks(seq)
-            ids = None
-            if rows:
-                seqs = [s for s, _ in rows]
-                ids = logits if greedy else self.sampler(logits, [s.params for s in seqs],
-                                                         [s.output_ids for s in seqs])
-            return (batch, rows, ids, ts, t0, t1)
+                seq.steps_run += 1
+                if seq.step_first is None:
+                    seq.step_first = self.launches
+            self.launches += 1
+            return [batch, rows, out, greedy, ts, t0, time.perf_counter()]
 
-    @torch.inference_mode()
-    def step_end(self, pending) -> list:
-        """Second half: wait for the sampled ids and append them (stop conditions,
-        streaming callbacks)."""
-        if pending is None:
-            return []
-        batch, rows, ids_t, ts, t0, t1 = pending
+    def _sample(self, launched):
+        batch, rows, out, greedy, ts, t0, t1 = launched
+        host = ev = ids = None
+        if rows:
+            seqs = [s for s, _ in rows]
+            ids = out if greedy else self.sampler(out, [s.params for s in seqs], [s.output_ids for s in seqs])
+            if ids.is_cuda:
+                host = torch.empty(ids.shape, dtype=ids.dtype, pin_memory=True)
+                host.copy_(ids, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+            else:
+                host = ids
+            for i, s in enumerate(seqs):
+                s.num_inflight, s.inflight_row = 1, i
+            self.runner.prev_ids = ids
+        return (batch, rows, host, ev, ts, t0, t1, time.perf_counter())
+
+    def _collect(self, pending) -> list:
+        batch, rows, host, ev, ts, t0, t1, t1s = pending
         with self.lock:
             out = []
             t2 = time.perf_counter()
             if rows:
-                ids = ids_t.tolist()
+                if ev is not None:
+                    ev.synchronize()
+                ids = host.tolist()
                 now = t2 = time.perf_counter()
                 for (seq, _), tid in zip(rows, ids):
+                    seq.num_inflight, seq.inflight_row = 0, -1
+                    if seq.finished:
+                        continue  # aborted, or stopped while this step was in flight
                     self._append(seq, int(tid), now)
                     out.append(seq)
+            for seq, _, _ in batch.items:
+                if not seq.finished:
+                    self.scheduler.publish_blocks(seq)
             self.steps += 1
             if self.step_trace is not None:
                 t3 = time.perf_counter()
-                npre = sum(n for sq, st, n in batch.items if st < len(sq.prompt_ids))
                 ndec = len(batch.items) - sum(1 for sq, st, n in batch.items if st < len(sq.prompt_ids))
+                npre = sum(n for sq, st, n in batch.items if st < len(sq.prompt_ids))
                 # (prefill tokens, decode rows, step s, schedule s, prepare+launch s, sample+sync s, post s)
                 self.step_trace.append((npre, ndec, t3 - t0, t0 - ts, t1 - t0,
                                         (t2 - t1) if rows else 0.0, (t3 - t2) if rows else 0.0))
@@ -155,6 +209,7 @@ class LLMEngine:
             if any(s and s in tail for s in p.stop):
                 reason = "stop"
         if reason:
+            seq.step_finish = self.launches
             self.scheduler.finish(seq, reason)
             M.GEN_TOKENS.inc(n)
         if seq.on_token is not None:
@@ -208,12 +263,16 @@ class AsyncLLMEngine:
     def _loop(self):
         while not self._stop:
             if not self.engine.has_work():
+                if self.engine._inflight is not None:
+                    with self.watchdog.busy():
+                        self.engine.flush()
+                    continue
                 self._wake.wait(0.05)
                 self._wake.clear()
                 continue
             try:
                 with self.watchdog.busy():
-                    self.engine.step()
+                    self.engine.step_pipelined()
                 self.watchdog.beat()
             except Exception:  # pragma: no cover
                 log.exception("engine step failed; aborting in-flight requests")

@@ -63,6 +63,7 @@ class ModelRunner:
         self._graph_pool = None
         self._ws = None
         self.step_hook = None
+        self.prev_ids: Optional[torch.Tensor] = None  # previous step's sampled ids (device)
 
     @staticmethod
     def block_bytes(model, block_size: int) -> int:
@@ -111,8 +112,10 @@ class ModelRunner:
         (csrc/runtime/step_builder.cpp) when the runtime is built."""
         tables = [s.block_table for s, _, _ in dec]
         starts = [st for _, st, _ in dec]
-        toks = [s.token_at(st) for s, st, _ in dec]
-        lens = [s.length for s, _, _ in dec]
+        # an in-flight input token (pipelined stepping) is not on the host yet: 0 here,
+        # gathered on the device from the previous step's ids (StepInputs.gather)
+        toks = [s.token_at(st) if st < s.length else 0 for s, st, _ in dec]
+        lens = [s.length + s.num_inflight for s, _, _ in dec]
         if _native_rt is not None:
             return _native_rt.decode_rows(tables, starts, toks, lens, self.bs, width, pad_to)
         P = max(len(dec), pad_to)
@@ -142,6 +145,16 @@ class ModelRunner:
         si.greedy = bool(greedy)
         return si, rows
 
+    @staticmethod
+    def _gather(dec, offset: int):
+        """(dst rows, src rows in the previous step's ids) of decode rows whose input
+        token is still in flight, or None."""
+        g = [(offset + i, s.inflight_row) for i, (s, st, _) in enumerate(dec) if st >= s.length]
+        if not g:
+            return None
+        a = np.asarray(g, dtype=np.int64)
+        return a[:, 0].copy(), a[:, 1].copy()
+
     def _prepare(self, items):
         if self.use_graphs and items and all(s.is_decode for s, _, _ in items) and len(items) <= self.graph_sizes[-1]:
             return self._prepare_graph(items)
@@ -160,7 +173,7 @@ class ModelRunner:
             ctx.append(start + n)
             tables.append(seq.block_table)
             r += n
-            if start + n == seq.length:
+            if start + n == seq.length + seq.num_inflight:
                 rows.append((seq, r - 1))
         ctx_d = tables_d = None
         if dec:
@@ -176,7 +189,8 @@ class ModelRunner:
                         slots=np.concatenate(slots), q_lens=q_lens, ctx_lens=ctx,
                         tables_p=self._bt(tables, max(len(t) for t in tables)) if pre else None,
                         ctx_d=ctx_d, tables_d=tables_d,
-                        num_decode=len(dec), logits_rows=np.asarray([row for _, row in rows], dtype=np.int64))
+                        num_decode=len(dec), logits_rows=np.asarray([row for _, row in rows], dtype=np.int64),
+                        gather=self._gather(dec, r - len(dec)) if dec else None)
         return si, rows
 
     def _prepare_graph(self, items):
@@ -185,7 +199,7 @@ class ModelRunner:
         ids, pos, slots, ctx, bt = self._decode_rows(items, self.max_blocks, Bg)
         rows = [(seq, i) for i, (seq, _, _) in enumerate(items)]
         si = StepInputs(decode_graph=Bg, ids=ids, positions=pos, slots=slots, ctx_d=ctx, tables_d=bt,
-                        num_decode=B, logits_rows=np.arange(B, dtype=np.int64))
+                        num_decode=B, logits_rows=np.arange(B, dtype=np.int64), gather=self._gather(items, 0))
         return si, rows
 
     # ----------------------------------------------------------- execution (device)
@@ -211,7 +225,19 @@ class ModelRunner:
             meta.decode_split = max(ops.decode_split_size(si.num_decode, self.hkv), self.bs)
             meta.max_splits = ops.decode_splits(si.tables_d.shape[1] * self.bs, meta.decode_split)
         meta.logits_idx = t(si.logits_rows) if len(si.logits_rows) else None
-        return t(si.ids), meta
+        ids = t(si.ids)
+        self._apply_gather(ids, si)
+        return ids, meta
+
+    def _apply_gather(self, ids: torch.Tensor, si: "StepInputs"):
+        """Fill in-flight input tokens from the previous step's device ids (no host sync)."""
+        if si.gather is None:
+            return
+        if self.prev_ids is None:
+            raise RuntimeError("step has in-flight input tokens but no previous step ids")
+        dst = torch.from_numpy(si.gather[0]).to(ids.device, non_blocking=True)
+        src = torch.from_numpy(si.gather[1]).to(ids.device, non_blocking=True)
+        ids.index_copy_(0, dst, self.prev_ids.index_select(0, src).to(ids.dtype))
 
     @torch.inference_mode()
     def execute(self, si: "StepInputs"):
@@ -292,6 +318,7 @@ class ModelRunner:
         Bg = si.decode_graph
         st = self.graphs.get((Bg, si.greedy)) or self.capture(Bg, si.greedy)
         st["ids"].copy_(torch.from_numpy(si.ids), non_blocking=True)
+        self._apply_gather(st["ids"], si)
         st["pos"].copy_(torch.from_numpy(si.positions), non_blocking=True)
         st["slots"].copy_(torch.from_numpy(si.slots), non_blocking=True)
         st["ctx"].copy_(torch.from_numpy(si.ctx_d), non_blocking=True)
@@ -316,3 +343,4 @@ class StepInputs:
     tables_d: Optional[np.ndarray] = None
     logits_rows: np.ndarray = field(default_factory=lambda: np.zeros(0, dtype=np.int64))
     greedy: bool = False                  # return token ids (argmax) instead of logits
+    gather: Optional[tuple] = None        # (dst rows, src rows): in-flight ids from the previous step

@@ -96,6 +96,9 @@ class Scheduler:
         i = 0
         while i < len(self.running) and budget > 0:
             seq = self.running[i]
+            if seq.done_after_inflight or seq.length + seq.num_inflight >= self.max_model_len:
+                i += 1  # finishes when its in-flight token is collected
+                continue
             n = min(seq.pending, budget)
             if not self._ensure(seq, seq.num_computed + n):
                 victim = self.running.pop()
@@ -108,6 +111,8 @@ class Scheduler:
             i += 1
         while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs:
             seq = self.waiting[0]
+            if seq.num_inflight:
+                break  # preempted with a token in flight: re-admit once it is collected
             self._admit_prefix(seq)
             n = min(seq.pending, budget)
             if not self._ensure(seq, seq.num_computed + n):
@@ -128,8 +133,9 @@ class Scheduler:
         return batch
 
     def publish_blocks(self, seq: Sequence):
-        """Register newly completed full blocks in the prefix cache."""
-        full = seq.num_computed // self.bs
+        """Register newly completed full blocks in the prefix cache (only blocks whose
+        token values the host already holds)."""
+        full = min(seq.num_computed, seq.length) // self.bs
         while seq.num_hashed_blocks < full and seq.num_hashed_blocks < len(seq.block_table):
             j = seq.num_hashed_blocks
             toks = seq.tokens(j * self.bs, (j + 1) * self.bs)

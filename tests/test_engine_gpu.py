@@ -64,6 +64,36 @@ def test_graph_decode_equals_eager():
     assert graphed == eager
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_pipelined_steps_equal_synchronous(graphs):
+    """step_pipelined (step N+1 enqueued before step N's ids reach the host; decode
+    inputs gathered on the device, from the graph's static output buffer when graphed)
+    == synchronous stepping, greedy and with a history-dependent logits processor."""
+    _, m = _gpu_llama()
+
+    def proc(hist):
+        return list(range(1 + (len(hist) % 5), 512, 3))
+
+    def drive(pipelined, mk):
+        eng = _engine(m, use_graphs=graphs)
+        if graphs:
+            eng.runner.capture_all(max_batch=8)
+        seqs = [eng.add_request(p, mk()) for p in PROMPTS[:2]]
+        it = 0
+        while eng.has_work() or len(seqs) < len(PROMPTS):
+            if it == 3:  # staggered admission: mixed prefill + in-flight decode steps
+                seqs += [eng.add_request(p, mk()) for p in PROMPTS[2:]]
+            eng.step_pipelined() if pipelined else eng.step()
+            it += 1
+        eng.flush()
+        return [s.output_ids for s in seqs]
+
+    for mk in (lambda: SamplingParams.greedy(12), lambda: SamplingParams.greedy(12, logits_processor=proc)):
+        ref = drive(False, mk)
+        assert all(len(r) == 12 for r in ref)
+        assert drive(True, mk) == ref
+
+
 def test_bert_gpu_matches_hf_fp32():
     cfg = transformers.BertConfig(vocab_size=300, hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
                                   intermediate_size=1024, max_position_embeddings=128, hidden_act="gelu")

@@ -23,7 +23,8 @@ def _hf_llama():
 
 def _engine(model, **kw):
     kw.setdefault("num_blocks", 128)
-    return LLMEngine(model, None, block_size=16, max_model_len=512, max_num_seqs=8, eos_ids=set(), **kw)
+    kw.setdefault("eos_ids", set())
+    return LLMEngine(model, None, block_size=16, max_model_len=512, max_num_seqs=8, **kw)
 
 
 def test_llama_matches_hf():
@@ -105,3 +106,49 @@ def test_chunked_prefill_prefix_cache_and_preemption_consistent():
     out = small.generate(prompts, SamplingParams.greedy(30))
     assert [x.output_ids for x in out] == ref30
     assert sum(x.num_preemptions for x in out) > 0
+
+
+def _run_pipelined(eng, prompts, params_fn, stagger: int = 0):
+    """Drive eng with step_pipelined (requests i >= 2 admitted `stagger` iterations apart)."""
+    seqs, pending, it = [], list(enumerate(prompts)), 0
+    while pending or eng.has_work():
+        while pending and (not stagger or it >= stagger * pending[0][0] or pending[0][0] < 2):
+            i, p = pending.pop(0)
+            seqs.append((i, eng.add_request(p, params_fn())))
+        if eng.has_work():
+            eng.step_pipelined()
+        else:
+            eng.flush()
+        it += 1
+    eng.flush()
+    return [s.output_ids for _, s in sorted(seqs, key=lambda x: x[0])]
+
+
+def test_pipelined_steps_match_synchronous():
+    """step_pipelined (step N+1 launched before step N's ids reach the host, decode
+    inputs gathered on the device) gives exactly the synchronous engine's tokens:
+    chunked prefill, staggered admission, EOS stops mid-flight, a history-dependent
+    logits processor, and preemption under a tiny KV pool."""
+    m = build_decoder("llama-tiny", dtype=torch.float32)
+    prompts = [list(range(3, 3 + n)) for n in (70, 33, 5, 100, 17)]
+
+    def proc(hist):  # history-dependent constraint (like the tool-call grammar)
+        return list(range(1 + (len(hist) % 5), m.cfg.vocab_size, 3))
+
+    cases = [
+        (lambda: SamplingParams.greedy(12), {}),
+        (lambda: SamplingParams.greedy(12, logits_processor=proc), {"max_num_batched_tokens": 24}),
+        (lambda: SamplingParams.greedy(30), {"num_blocks": 10}),
+    ]
+    for params_fn, kw in cases:
+        ref = [s.output_ids for s in _engine(m, **kw).generate(prompts, params_fn())]
+        assert _run_pipelined(_engine(m, **kw), prompts, params_fn) == ref
+        assert _run_pipelined(_engine(m, **kw), prompts, params_fn, stagger=3) == ref
+    # EOS stop: pick a token the reference emits mid-sequence
+    base = [s.output_ids for s in _engine(m).generate(prompts, SamplingParams.greedy(12))]
+    eos = base[0][4]
+    ref = [s.output_ids for s in _engine(m, eos_ids={eos}).generate(prompts, SamplingParams.greedy(12))]
+    assert any(len(r) < 12 for r in ref)
+    eng = LLMEngine(m, None, block_size=16, max_model_len=512, max_num_seqs=8, eos_ids={eos}, num_blocks=128)
+    assert _run_pipelined(eng, prompts, lambda: SamplingParams.greedy(12)) == ref
+    assert eng.allocator.usage() == 0.0 or not eng.scheduler.running
