@@ -258,8 +258,10 @@ def _tiny_stack():
     return tok, idx, eng, FakeCluster.default(), Config()
 
 
-def test_continuous_load_rag_agent_mixed():
-    """Closed-loop continuous batching over the three workloads of bench.py (configs 2/3/5)."""
+@pytest.mark.parametrize("threaded", [False, True])
+def test_continuous_load_rag_agent_mixed(threaded):
+    """Closed-loop continuous batching over the three workloads of bench.py (configs 2/3/5),
+    admission planned inline or on the planner thread."""
     from llm_kubernetes_minikube_sharp4dev_amd.agent.agent_pipeline import AgentPipeline, MixedPipeline
     from llm_kubernetes_minikube_sharp4dev_amd.agent.rag_pipeline import ContinuousLoad, RagAgentPipeline
     from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import SamplingParams
@@ -276,7 +278,7 @@ def test_continuous_load_rag_agent_mixed():
 
     params = SamplingParams.greedy(4, ignore_eos=True)
     for pipe in (rag, agent, MixedPipeline(rag, agent)):
-        load = ContinuousLoad(pipe, nq, params, concurrency=4, admit_chunk=2)
+        load = ContinuousLoad(pipe, nq, params, concurrency=4, admit_chunk=2, threaded=threaded)
         out = load.run(6)
         out += load.run(3)  # continues the same stream
         load.drain()
