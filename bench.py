@@ -75,6 +75,8 @@ def parse():
                          "the random-init model emit valid tool calls, so every request also runs the k8s dispatch "
                          "and RAG gating path (same token counts; measured at the same speed)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--token-align", type=int, default=256,
+                    help="trim mixed steps' prefill chunks to a multiple of this many rows (0: off)")
     ap.add_argument("--threaded-admission", action="store_true",
                     help="continuous mode: plan admissions on a planner thread (default: inline on the engine "
                          "thread between pipelined steps; measured 1%% faster)")
@@ -192,7 +194,8 @@ def main():
     if not on_gpu:
         runner_kw.pop("kv_cache_gb")
         runner_kw["num_blocks"] = max(256, args.batch * 80)
-    engine_kw = dict(max_num_batched_tokens=mbt, enable_prefix_caching=not args.no_prefix_cache, eos_ids=set())
+    engine_kw = dict(max_num_batched_tokens=mbt, enable_prefix_caching=not args.no_prefix_cache, eos_ids=set(),
+                     token_align=args.token_align)
     params = SamplingParams.greedy(args.max_new_tokens, ignore_eos=True)
     if args.constrained:
         from llm_kubernetes_minikube_sharp4dev_amd.engine.constrained import tool_call_processor
@@ -320,8 +323,11 @@ def main():
         step_mix = {
             "host_breakdown": host,
             "steps": len(trace),
-            "decode_only_steps": len(dec_only), "decode_only_s": round(sum(t[2] for t in dec_only), 3),
-            "mixed_steps": len(mixed), "mixed_s": round(sum(t[2] for t in mixed), 3),
+            "decode_only_steps": len(dec_only), "decode_only_gpu_s": round(sum(t[7] for t in dec_only), 3),
+            "mixed_steps": len(mixed), "mixed_gpu_s": round(sum(t[7] for t in mixed), 3),
+            # GPU time inside steps (first kernel -> ids copy) over the timed wall time: the rest is
+            # device idle between steps
+            "gpu_step_busy_frac": round(sum(t[7] for t in trace) / elapsed, 3) if trace and elapsed else None,
             "avg_prefill_tokens_mixed": round(statistics.mean(t[0] for t in mixed), 1) if mixed else 0,
             "avg_decode_rows": round(statistics.mean(t[1] for t in trace), 1) if trace else 0,
         }

@@ -31,13 +31,14 @@ class LLMEngine:
                  max_num_seqs: int = 256, max_num_batched_tokens: int = 65536,
                  enable_prefix_caching: bool = True, use_graphs: bool = True, num_blocks: Optional[int] = None,
                  kv_cache_gb: Optional[float] = None, gpu_memory_fraction: float = 0.85, seed: int = 0,
-                 eos_ids: Optional[set] = None, _runner: Optional[ModelRunner] = None):
+                 eos_ids: Optional[set] = None, _runner: Optional[ModelRunner] = None, token_align: int = 256):
         self.model = model
         self.tokenizer = tokenizer
         self.runner = _runner or ModelRunner(model, block_size, max_model_len, max_num_seqs, num_blocks,
                                              kv_cache_gb, gpu_memory_fraction, use_graphs)
         self.allocator = make_allocator(self.runner.num_blocks, block_size, enable_prefix_caching)
-        self.scheduler = Scheduler(self.allocator, block_size, max_num_seqs, max_num_batched_tokens, max_model_len)
+        self.scheduler = Scheduler(self.allocator, block_size, max_num_seqs, max_num_batched_tokens, max_model_len,
+                                   token_align)
         self.sampler = Sampler(model.cfg.vocab_size, seed)
         self.max_model_len = max_model_len
         if eos_ids is None:
@@ -131,6 +132,10 @@ class LLMEngine:
             # plain greedy steps get token ids straight from the model (no fp32 logits;
             # under TP an all-gather of (max, argmax) pairs instead of the vocab)
             greedy = all(_plain_greedy(sq.params) for sq, _, _ in batch.items)
+            ev0 = None
+            if self.step_trace is not None and self.model.device.type == "cuda":
+                ev0 = torch.cuda.Event(enable_timing=True)  # GPU-side step start (after earlier work)
+                ev0.record()
             rows, out = self.runner.forward_logits(batch.items, greedy)
             for seq, start, n in batch.items:
                 seq.num_computed = start + n
@@ -138,10 +143,10 @@ class LLMEngine:
                 if seq.step_first is None:
                     seq.step_first = self.launches
             self.launches += 1
-            return [batch, rows, out, greedy, ts, t0, time.perf_counter()]
+            return [batch, rows, out, greedy, ts, t0, time.perf_counter(), ev0]
 
     def _sample(self, launched):
-        batch, rows, out, greedy, ts, t0, t1 = launched
+        batch, rows, out, greedy, ts, t0, t1, ev0 = launched
         host = ev = ids = None
         if rows:
             seqs = [s for s, _ in rows]
@@ -149,17 +154,17 @@ class LLMEngine:
             if ids.is_cuda:
                 host = torch.empty(ids.shape, dtype=ids.dtype, pin_memory=True)
                 host.copy_(ids, non_blocking=True)
-                ev = torch.cuda.Event()
+                ev = torch.cuda.Event(enable_timing=ev0 is not None)
                 ev.record()
             else:
                 host = ids
             for i, s in enumerate(seqs):
                 s.num_inflight, s.inflight_row = 1, i
             self.runner.prev_ids = ids
-        return (batch, rows, host, ev, ts, t0, t1, time.perf_counter())
+        return (batch, rows, host, ev, ts, t0, t1, time.perf_counter(), ev0)
 
     def _collect(self, pending) -> list:
-        batch, rows, host, ev, ts, t0, t1, t1s = pending
+        batch, rows, host, ev, ts, t0, t1, t1s, ev0 = pending
         with self.lock:
             out = []
             t2 = time.perf_counter()
@@ -182,9 +187,11 @@ class LLMEngine:
                 t3 = time.perf_counter()
                 ndec = len(batch.items) - sum(1 for sq, st, n in batch.items if st < len(sq.prompt_ids))
                 npre = sum(n for sq, st, n in batch.items if st < len(sq.prompt_ids))
-                # (prefill tokens, decode rows, step s, schedule s, prepare+launch s, sample+sync s, post s)
+                gpu = ev0.elapsed_time(ev) / 1e3 if (ev0 is not None and ev is not None) else 0.0
+                # (prefill tokens, decode rows, step s, schedule s, prepare+launch s, sample+sync s, post s,
+                #  GPU s from the step's first kernel to its ids copy)
                 self.step_trace.append((npre, ndec, t3 - t0, t0 - ts, t1 - t0,
-                                        (t2 - t1) if rows else 0.0, (t3 - t2) if rows else 0.0))
+                                        (t2 - t1) if rows else 0.0, (t3 - t2) if rows else 0.0, gpu))
             M.STEP_TOKENS.observe(batch.num_tokens)
             M.STEP_TIME.observe(time.perf_counter() - t0)
             M.KV_USAGE.set(self.allocator.usage())

@@ -33,8 +33,12 @@ class ScheduledBatch:
 
 class Scheduler:
     def __init__(self, allocator, block_size: int, max_num_seqs: int = 256,
-                 max_num_batched_tokens: int = 65536, max_model_len: int = 8192):
+                 max_num_batched_tokens: int = 65536, max_model_len: int = 8192, token_align: int = 256):
         self.alloc = allocator
+        # mixed steps: trim prefill chunks so the step's row count is a multiple of the
+        # library GEMM's 256-row macro tile (a 3852-row step runs 16 row tiles, the 16th
+        # nearly empty); the trimmed tokens lead the next step
+        self.token_align = token_align
         self.bs = block_size
         self.max_num_seqs = max_num_seqs
         self.max_tokens = max_num_batched_tokens
@@ -130,7 +134,25 @@ class Scheduler:
             self.running.append(seq)
             batch.items.append((seq, seq.num_computed, n))
             budget -= n
+        self._align(batch)
         return batch
+
+    def _align(self, batch: ScheduledBatch):
+        a = self.token_align
+        if not a:
+            return
+        total = batch.num_tokens
+        ex = total % a
+        if total <= a or not ex:
+            return
+        for k in range(len(batch.items) - 1, -1, -1):
+            seq, st, n = batch.items[k]
+            if n > 1:  # a prefill chunk (decode rows are 1 token)
+                cut = min(ex, n - 1)
+                batch.items[k] = (seq, st, n - cut)
+                ex -= cut
+                if not ex:
+                    return
 
     def publish_blocks(self, seq: Sequence):
         """Register newly completed full blocks in the prefix cache (only blocks whose
