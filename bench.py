@@ -75,6 +75,9 @@ def parse():
                          "the random-init model emit valid tool calls, so every request also runs the k8s dispatch "
                          "and RAG gating path (same token counts; measured at the same speed)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--sp-min-tokens", type=int, default=None,
+                    help="with --tp > 1: steps of at least this many rows run sequence-parallel "
+                         "(reduce-scatter / all-gather around the norms); default off")
     ap.add_argument("--token-align", type=int, default=256,
                     help="trim mixed steps' prefill chunks to a multiple of this many rows (0: off)")
     ap.add_argument("--threaded-admission", action="store_true",
@@ -184,6 +187,8 @@ def main():
     # ---- generator + engine
     t0 = time.perf_counter()
     llm = build_decoder(args.model, device=dev, seed=args.seed, tp=tpg, dtype=wdtype)
+    if args.sp_min_tokens is not None and hasattr(llm, "sp_min_tokens"):
+        llm.sp_min_tokens = args.sp_min_tokens
     sync()
     log(rank, f"{args.model} random-init (tp={args.tp}) in {time.perf_counter() - t0:.1f}s")
     # continuous: ~4k-token steps keep most steps mixed (decode rows ride on the prefill

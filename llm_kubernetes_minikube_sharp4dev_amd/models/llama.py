@@ -8,11 +8,14 @@ MI355X layout decisions:
   * RoPE and the paged-KV write are one kernel on the QKV output;
   * attention reads K/V from the paged cache (flash prefill / split-K decode);
   * tensor parallel: column-parallel QKV / gate_up, row-parallel o / down with one
-    RCCL all-reduce each, vocab-parallel embedding + LM head.
+    RCCL all-reduce each, vocab-parallel embedding + LM head;
+  * sequence parallel for prefill-sized steps (``sp_min_tokens``): residual stream and
+    norms sharded over the T rows, reduce-scatter / all-gather instead of all-reduce.
 """
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -59,6 +62,9 @@ class LlamaModel(nn.Module):
         self.final_norm = nn.Parameter(torch.ones(cfg.hidden, **e), requires_grad=False)
         self.lm_head = self.embed if cfg.tie_word_embeddings else nn.Parameter(
             torch.empty(vloc, cfg.hidden, **e), requires_grad=False)
+        # steps of at least this many rows run sequence-parallel under TP (None: never)
+        sp = os.environ.get("LK_SP_MIN_TOKENS")
+        self.sp_min_tokens: Optional[int] = int(sp) if sp else None
         max_pos = min(cfg.max_position, 1 << 17)
         self.register_buffer("cos_sin", ops.rope_cos_sin(max_pos, self.D, cfg.rope_theta,
                                                          cfg.rope_scaling, device=device),
@@ -90,6 +96,9 @@ class LlamaModel(nn.Module):
 
     def forward(self, ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
         """ids [T] -> final hidden states of rows ``meta.logits_idx`` (or all rows)."""
+        if (self.tp.enabled and self.sp_min_tokens is not None and ids.shape[0] >= self.sp_min_tokens
+                and not (ids.is_cuda and torch.cuda.is_current_stream_capturing())):
+            return self._forward_sp(ids, meta, kv_caches)
         cfg = self.cfg
         res = self.embed_tokens(ids)
         x = ops.rmsnorm(res, self.layers[0].input_norm, cfg.norm_eps)
@@ -109,6 +118,44 @@ class LlamaModel(nn.Module):
             self.tp.all_reduce_(d)
             nxt = self.layers[li + 1].input_norm if li + 1 < n else self.final_norm
             x = ops.rmsnorm(d, nxt, cfg.norm_eps, residual=res)
+        if meta.logits_idx is not None:
+            x = x.index_select(0, meta.logits_idx)
+        return x
+
+    def _forward_sp(self, ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
+        """Sequence-parallel forward: this rank keeps rows [r*n, (r+1)*n) of the
+        (padded) residual stream; each row-parallel partial sum is reduce-scattered
+        into the owner's rows, normed there, and all-gathered for the next
+        column-parallel GEMM."""
+        cfg, tp = self.cfg, self.tp
+        T = ids.shape[0]
+        n = (T + tp.size - 1) // tp.size
+        pad = n * tp.size - T
+
+        def padded(t):
+            return torch.nn.functional.pad(t, (0, 0, 0, pad)) if pad else t
+
+        local = ids.long() - self.vocab_lo
+        mask = (local < 0) | (local >= self.embed.shape[0])
+        h = self.embed[local.clamp(0, self.embed.shape[0] - 1)].masked_fill(mask[:, None], 0)
+        res = tp.reduce_scatter_rows(padded(h))                      # [n, H]
+        x = ops.rmsnorm(res, self.layers[0].input_norm, cfg.norm_eps)
+        attn_out = None
+        nl = len(self.layers)
+        for li, L in enumerate(self.layers):
+            xf = tp.all_gather_rows(x)[:T]
+            qkv = ops.linear(xf, L.qkv)
+            kc, vc = kv_caches[li]
+            ops.rope_kv_(qkv, meta.positions, self.cos_sin, self.hq, self.hkv, self.D, kc, vc,
+                         meta.slots, True, False)
+            attn_out = paged_attention(qkv, kc, vc, meta, self.hq, self.hkv, self.D, self.scale, attn_out)
+            o = tp.reduce_scatter_rows(padded(ops.linear(attn_out, L.o)))
+            x = ops.rmsnorm(o, L.post_norm, cfg.norm_eps, residual=res)
+            a = ops.linear_swiglu(tp.all_gather_rows(x)[:T], L.gate_up)
+            d = tp.reduce_scatter_rows(padded(ops.linear(a, L.down)))
+            nxt = self.layers[li + 1].input_norm if li + 1 < nl else self.final_norm
+            x = ops.rmsnorm(d, nxt, cfg.norm_eps, residual=res)
+        x = tp.all_gather_rows(x)[:T]
         if meta.logits_idx is not None:
             x = x.index_select(0, meta.logits_idx)
         return x

@@ -6,6 +6,11 @@ Sharding scheme (Megatron-style, sized for 8xMI355X xGMI full mesh):
   * row-parallel:    o_proj, down_proj -> one all-reduce each per layer
   * vocab-parallel:  embedding (masked lookup + all-reduce) and LM head
                      (local logits; greedy = all-gather of per-rank (max, argmax))
+  * sequence-parallel (prefill-sized steps, Megatron SP): the residual stream and
+                     the RMSNorms run on T/tp rows; each row-parallel all-reduce
+                     becomes a reduce-scatter, and an all-gather feeds the next
+                     column-parallel GEMM (same bytes on the wire, 1/tp of the
+                     norm / residual traffic and activation memory per rank)
 """
 from __future__ import annotations
 
@@ -35,6 +40,28 @@ class TPGroup:
         if self.size > 1:
             dist.all_reduce(t, group=self.group)
         return t
+
+    def reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """Sum over ranks of t [size*n, ...], this rank's rows [rank*n, (rank+1)*n)."""
+        if self.size == 1:
+            return t
+        n = t.shape[0] // self.size
+        if dist.get_backend(self.group) == "gloo":  # gloo has no reduce_scatter
+            dist.all_reduce(t, group=self.group)
+            return t[self.rank * n:(self.rank + 1) * n].contiguous()
+        out = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.reduce_scatter_tensor(out, t.contiguous(), group=self.group)
+        return out
+
+    def all_gather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenation over ranks of t [n, ...] -> [size*n, ...]."""
+        if self.size == 1:
+            return t
+        if dist.get_backend(self.group) == "gloo":
+            return self.all_gather_cat(t, dim=0)
+        out = torch.empty((t.shape[0] * self.size,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out
 
     def all_gather_cat(self, t: torch.Tensor, dim: int = -1) -> torch.Tensor:
         if self.size == 1:

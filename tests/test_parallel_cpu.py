@@ -55,7 +55,7 @@ def _hf(arch):
 PROMPTS = [[5, 17, 99, 3, 250, 7, 7, 1, 400, 33, 21, 8, 2, 9, 11, 60, 61, 62, 63], [7, 8, 9], list(range(10, 60))]
 
 
-def _tp_worker(rank, world, port, arch, out_path):
+def _tp_worker(rank, world, port, arch, out_path, sp_min_tokens=None):
     _init(rank, world, port)
     from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import SamplingParams
     from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder
@@ -65,6 +65,8 @@ def _tp_worker(rank, world, port, arch, out_path):
     tp = TPGroup(rank, world, dist.group.WORLD)
     m = build_decoder(_ours_cfg(arch), dtype=torch.float32, tp=tp)
     m.load_hf_state_dict(_hf(arch).state_dict())
+    if sp_min_tokens is not None:
+        m.sp_min_tokens = sp_min_tokens
     kw = dict(block_size=16, max_model_len=512, max_num_seqs=8, num_blocks=96)
     if rank == 0:
         eng = make_tp_engine(m, tp, None, engine_kw={"eos_ids": set(), "max_num_batched_tokens": 40}, **kw)
@@ -76,8 +78,10 @@ def _tp_worker(rank, world, port, arch, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("arch", ["llama", "opt"])
-def test_tp2_generation_matches_single_process(arch):
+@pytest.mark.parametrize("arch,sp", [("llama", None), ("opt", None), ("llama", 2)])
+def test_tp2_generation_matches_single_process(arch, sp):
+    """TP=2 == one process; ("llama", 2): sequence parallel on every step of >= 2 rows
+    (odd row counts exercise the padding)."""
     from llm_kubernetes_minikube_sharp4dev_amd.engine.llm_engine import LLMEngine
     from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import SamplingParams
     from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder
@@ -88,7 +92,7 @@ def test_tp2_generation_matches_single_process(arch):
     ref = [s.output_ids for s in eng.generate(PROMPTS, SamplingParams.greedy(10))]
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "out.pt")
-        mp.spawn(_tp_worker, args=(2, _free_port(), arch, out), nprocs=2, join=True)
+        mp.spawn(_tp_worker, args=(2, _free_port(), arch, out, sp), nprocs=2, join=True)
         got = torch.load(out, weights_only=True)
     assert got == ref
 
