@@ -141,6 +141,22 @@ def case_gemm(M, N, K, layout="NT"):
             "GB/s": (M * K + N * K + M * N) * 2 / t / 1e9}
 
 
+def case_big(M, N, K, swiglu=False):
+    """Hand-written 256x256 prefill GEMM (csrc/big_gemm.hip) vs hipBLASLt (+ silu_mul when swiglu)."""
+    L = ops.lib()
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    t0 = timeit(lambda: L.big_linear(x, w, swiglu, None, 0))
+    t1 = timeit(lambda: L.big_linear(x, w, swiglu, None, 1))
+    t = timeit(lambda: L.big_linear(x, w, swiglu, None, 2))
+    if swiglu:
+        tb = timeit(lambda: L.silu_mul(torch.nn.functional.linear(x, w)))
+    else:
+        tb = timeit(lambda: torch.nn.functional.linear(x, w))
+    return {"case": f"big M{M} N{N} K{K}{' swiglu' if swiglu else ''}", "us": t * 1e6,
+            "TFLOP/s": 2 * M * N * K / t / 1e12, "v0_us": t0 * 1e6, "v1_us": t1 * 1e6, "hipblaslt_us": tb * 1e6, "speedup": tb / t}
+
+
 def case_skinny(M, N, K, swiglu=False):
     """Hand-written decode-regime GEMM vs hipBLASLt (+ silu_mul when swiglu) at the same shape."""
     a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
@@ -224,6 +240,11 @@ CASES = {
                    for (N, K) in LLAMA8B_SHAPES + [(128256, 4096), (10240, 8192), (8192, 8192), (57344, 8192),
                                                    (8192, 28672)]],
     "ws_sweep": lambda: case_ws_sweep(),
+    "gemm_mid": lambda: [case_gemm(M, N, K) for M in (1024, 2048, 2560, 3072, 3328, 3584, 3840, 4096, 4352,
+                                                      5120, 5376, 6144, 8192)
+                         for (N, K) in LLAMA8B_SHAPES],
+    "big": lambda: [case_big(M, N, K, N == 28672) for M in (2048, 3328, 3584, 3840, 4096, 8192)
+                    for (N, K) in LLAMA8B_SHAPES],
     "gemm_sweep": lambda: [case_gemm(M, N, K, lay) for M in (128, 256, 1024, 4096, 8192, 16384)
                            for (N, K) in LLAMA8B_SHAPES for lay in ("NT", "NN")],
 }

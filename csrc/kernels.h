@@ -34,6 +34,10 @@ int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, i
 int lk_ws_scores_f32(const bf16_t* x, long ldx, const bf16_t* w, int M, long N, int K, float* out, long ldo,
                      hipStream_t st);
 
+// big_gemm.hip (prefill-regime linear, 256x256 MFMA tiles, optional fused SwiGLU)
+int lk_big_gemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int swiglu, bf16_t* out,
+                long ldo, int variant, hipStream_t st);
+
 // rope_kv.hip
 int lk_rope_kv(bf16_t* qkv, long qs, const int* positions, const float* cos_sin, long T, int Hq,
                int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,

@@ -207,6 +207,11 @@ class LlamaModel(nn.Module):
             self.lm_head.copy_(t(key)[self.vocab_lo:self.vocab_hi])
         return self
 
+    def gemm_shapes(self):
+        """(weight, swiglu) of one layer's projections, for GEMM autotuning."""
+        L = self.layers[0]
+        return [(L.qkv, False), (L.o, False), (L.gate_up, True), (L.down, False)]
+
     def kv_cache_shape(self, num_blocks: int, block_size: int):
         return (num_blocks, self.hkv, block_size, self.D)
 

@@ -19,7 +19,7 @@ __all__ = [
     "rmsnorm", "layernorm", "embed_layernorm", "silu_mul", "gelu_", "relu_", "rope_kv_",
     "kv_write", "paged_decode", "flash_prefill", "prefill_tiles", "knn_topk", "knn_merge",
     "pool_normalize", "row_norms", "select_tokens", "repeat_penalty_", "linear", "linear_swiglu",
-    "decode_splits", "rope_cos_sin",
+    "decode_splits", "rope_cos_sin", "tune_big_gemm",
 ]
 
 rope_cos_sin = ref.rope_cos_sin
@@ -254,26 +254,89 @@ def _decode_gemm_kind(x, w, swiglu: bool) -> Optional[str]:
     return None
 
 
+# Prefill-regime GEMMs (M > WS_MAX_M): hipBLASLt, or the hand-written 256x256 MFMA kernel
+# (csrc/big_gemm.hip, SwiGLU fused) for the (M bucket, N, K, swiglu) shapes where
+# ``tune_big_gemm`` measured it faster on this device (hipBLASLt's heuristic is uneven
+# across M: profiles/r1_big_gemm.md).  M is bucketed up to the 256-row macro tile.
+BIG_VARIANT = 2
+_BIG_TABLE: dict = {}
+
+
+def _big_key(x, w, swiglu: bool):
+    M = x.shape[0]
+    return ((M + 255) // 256, w.shape[0], w.shape[1], swiglu)
+
+
+def _use_big(x, w, swiglu: bool) -> bool:
+    if not _BIG_TABLE or not (use_hip(x) and x.dim() == 2 and x.dtype == torch.bfloat16
+                              and w.dtype == torch.bfloat16 and x.stride(1) == 1 and w.is_contiguous()):
+        return False
+    return _BIG_TABLE.get(_big_key(x, w, swiglu), False)
+
+
+def tune_big_gemm(weights, max_m: int, min_m: int = 512, iters: int = 6) -> dict:
+    """Time hipBLASLt (+ silu_mul) against the big-tile kernel for every 256-row M bucket
+    in [min_m, max_m] and each (weight, swiglu) pair; record where the kernel wins.
+    ``weights``: [(w [N, K] bf16 CUDA tensor, swiglu)].  Returns {key: (big_us, lib_us)}."""
+    import statistics
+
+    L = lib()
+    out = {}
+    for w, swiglu in weights:
+        N, K = w.shape
+        if K % 64 or N % 256:
+            continue
+        for mb in range(max(min_m, 256) // 256, max_m // 256 + 1):
+            M = mb * 256
+            x = torch.randn(M, K, device=w.device, dtype=torch.bfloat16)
+
+            def t(fn):
+                for _ in range(2):
+                    fn()
+                ts = []
+                for _ in range(iters):
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record()
+                    fn()
+                    b.record()
+                    b.synchronize()
+                    ts.append(a.elapsed_time(b))
+                return statistics.median(ts) * 1e3
+
+            tb = t(lambda: L.big_linear(x, w, swiglu, None, BIG_VARIANT))
+            tl = t(lambda: silu_mul(torch.nn.functional.linear(x, w)) if swiglu else torch.nn.functional.linear(x, w))
+            key = (mb, N, K, swiglu)
+            _BIG_TABLE[key] = tb < 0.98 * tl
+            out[key] = (round(tb, 1), round(tl, 1))
+    return out
+
+
 def linear(x, w, b=None):
-    """Projection GEMM: decode-sized batches (M <= SKINNY_MAX_M) on the hand-written
-    weight-streaming MFMA kernel, everything else on hipBLASLt through torch."""
+    """Projection GEMM: decode-sized batches on the hand-written weight-streaming MFMA
+    kernels (skinny / ws), prefill-sized ones on hipBLASLt or the big-tile MFMA kernel
+    where tuned faster."""
     if b is None:
         kind = _decode_gemm_kind(x, w, False)
         if kind == "skinny":
             return lib().skinny_linear(x, w)
         if kind == "ws":
             return lib().ws_linear(x, w)
+        if kind is None and x.shape[0] > WS_MAX_M and _use_big(x, w, False):
+            return lib().big_linear(x, w, False, None, BIG_VARIANT)
     return torch.nn.functional.linear(x, w, b)
 
 
 def linear_swiglu(x, w_gate_up):
     """silu(x Wg^T) * (x Wu^T) for a fused [Wg; Wu] weight: one kernel (GEMM with the
-    SwiGLU epilogue) in the decode regime, hipBLASLt + silu_mul otherwise."""
+    SwiGLU epilogue) in the decode regime and where the big-tile kernel was tuned
+    faster, hipBLASLt + silu_mul otherwise."""
     kind = _decode_gemm_kind(x, w_gate_up, True)
     if kind == "skinny":
         return lib().skinny_linear(x, w_gate_up, True)
     if kind == "ws":
         return lib().ws_linear(x, w_gate_up, True)
+    if x.shape[0] > WS_SWIGLU_MAX_M and _use_big(x, w_gate_up, True):
+        return lib().big_linear(x, w_gate_up, True, None, BIG_VARIANT)
     return silu_mul(linear(x, w_gate_up))
 
 

@@ -343,3 +343,29 @@ def test_ws_swiglu(hip, M, IK):
     a_ref = ref.silu_mul((x.float() @ w.float().t()).to(torch.bfloat16))
     _close(hip.ws_linear(x, w, True), a_ref, 0.03, 0.01, f"ws swiglu M{M} I{I}")
     _close(hip.ws_linear(x, w, True, 64, 2), a_ref, 0.03, 0.01, "ws swiglu bn64 S2")
+
+
+@pytest.mark.parametrize("M", [257, 512, 1000, 3584])
+@pytest.mark.parametrize("NK", [(6144, 4096), (4096, 14336), (768, 768), (1280, 8192)])
+def test_big_linear(hip, M, NK):
+    """Prefill-regime 256x256 MFMA GEMM (LDS-DMA staged, XCD-grouped tiles) vs an fp32
+    matmul, including an M tail (masked rows)."""
+    N, K = NK
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    y_ref = x.float() @ w.float().t()
+    for v in (0, 1, 2):
+        _close(hip.big_linear(x, w, False, None, v), y_ref, 0.02, 0.01, f"big v{v} M{M} N{N} K{K}")
+
+
+@pytest.mark.parametrize("M", [300, 2048])
+@pytest.mark.parametrize("IK", [(14336, 4096), (3584, 8192), (1536, 768)])
+def test_big_swiglu_matches_unfused(hip, M, IK):
+    I, K = IK
+    torch.manual_seed(3)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(2 * I, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    a_ref = ref.silu_mul((x.float() @ w.float().t()).to(torch.bfloat16))
+    for v in (0, 1, 2):
+        _close(hip.big_linear(x, w, True, None, v), a_ref, 0.03, 0.01, f"big v{v} swiglu M{M} I{I}")
