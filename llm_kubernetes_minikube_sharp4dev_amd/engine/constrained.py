@@ -228,6 +228,35 @@ class ToolCallGrammar:
             if t and i not in self.tt.eos:
                 self.by_text.setdefault(t, []).append(i)
         self._prefix_cache: dict[str, list] = {}
+        # (kind, room, value state, closing literal) -> allowed ids of a free string / int
+        # field (a few dozen keys; building one scans the vocabulary subset, ~1 ms)
+        self._free_cache: dict = {}
+
+    def _free_tokens(self, kind: str, room: int, val: str, close: Optional[str]):
+        toks = self.name_tokens if kind == "str" else self.digit_tokens
+        allowed = [i for i in toks if len(self.tt.texts[i]) <= room] if room > 0 else []
+        if kind == "int":  # JSON integers: no leading zero ("0" alone is fine)
+            if val == "0":
+                allowed = []
+            elif not val:
+                allowed = [i for i in allowed if self.tt.texts[i] == "0" or self.tt.texts[i][0] != "0"]
+        if close is not None:
+            allowed = allowed + self._literal_tokens(close)
+        return allowed or list(self.tt.eos or [0])
+
+    def _choice(self, options: tuple, typed: str) -> list:
+        """Tokens continuing ``typed`` towards any of ``options`` + closing quote (cached)."""
+        key = (options, typed)
+        c = self._free_cache.get(key)
+        if c is None:
+            out = set()
+            for a in options:
+                if a.startswith(typed):
+                    out.update(self._literal_tokens((a + '"')[len(typed):]))
+            c = sorted(out) or list(self.tt.eos or [0])
+            if len(self._free_cache) < 8192:
+                self._free_cache[key] = c
+        return c
 
     def _literal_tokens(self, rest: str) -> list:
         """Tokens for a forced literal: those spelling the LONGEST prefix of ``rest`` the
@@ -271,11 +300,7 @@ class ToolCallGrammar:
         rest = text[len(head):]
         q = rest.find('"')
         if q < 0:  # choosing the tool name
-            opts = [a for a in self.tools if a.startswith(rest)]
-            out = set()
-            for a in opts:
-                out.update(self._literal_tokens((a + '"')[len(rest):]))
-            return sorted(out) or (self.tt.eos or [0])
+            return self._choice(tuple(self.tools), rest)
         action = rest[:q]
         if action not in self.tools:
             return self.tt.eos or [0]
@@ -298,11 +323,7 @@ class ToolCallGrammar:
                 seg = s[pos:]
                 q2 = seg.find('"')
                 if q2 < 0:  # still choosing the value
-                    out = set()
-                    for v in vals:
-                        if v.startswith(seg):
-                            out.update(self._literal_tokens((v + '"')[len(seg):]))
-                    return sorted(out) or (self.tt.eos or [0])
+                    return self._choice(tuple(vals), seg)
                 if seg[:q2] not in vals:
                     return self.tt.eos or [0]
                 pos += q2 + 1
@@ -313,17 +334,13 @@ class ToolCallGrammar:
                 after = s[pos + len(val):]
                 limit = self.max_str if kind == "str" else 2
                 if after == "":
-                    toks = self.name_tokens if kind == "str" else self.digit_tokens
-                    room = limit - len(val)
-                    allowed = [i for i in toks if len(self.tt.texts[i]) <= room] if room > 0 else []
-                    if kind == "int":  # JSON integers: no leading zero ("0" alone is fine)
-                        if val == "0":
-                            allowed = []
-                        elif not val:
-                            allowed = [i for i in allowed if self.tt.texts[i] == "0" or self.tt.texts[i][0] != "0"]
-                    if val:  # may close the field
-                        allowed = allowed + self._literal_tokens(prog[si + 1][1])
-                    return allowed or (self.tt.eos or [0])
+                    close = prog[si + 1][1] if val else None  # may close the field
+                    key = (kind, limit - len(val), "0" if val == "0" else bool(val), close)
+                    allowed = self._free_cache.get(key)
+                    if allowed is None:
+                        allowed = self._free_tokens(kind, limit - len(val), val, close)
+                        self._free_cache[key] = allowed
+                    return allowed
                 if not val:
                     return self.tt.eos or [0]
                 pos += len(val)

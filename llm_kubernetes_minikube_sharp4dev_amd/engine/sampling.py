@@ -65,6 +65,22 @@ class Sampler:
         self.vocab_size = vocab_size
         self.seed = seed
         self.step = 0
+        # processors return the same cached list objects for recurring grammar states:
+        # memoise their int64 arrays (id -> (list, array); the list reference keeps the id valid)
+        self._arr_cache: dict = {}
+
+    def _as_array(self, allowed):
+        if isinstance(allowed, np.ndarray):
+            return allowed.astype(np.int64, copy=False)
+        hit = self._arr_cache.get(id(allowed))
+        if hit is not None and hit[0] is allowed:
+            return hit[1]
+        a = np.asarray(allowed, dtype=np.int64)
+        if len(a) > 64:
+            if len(self._arr_cache) > 4096:
+                self._arr_cache.clear()
+            self._arr_cache[id(allowed)] = (allowed, a)
+        return a
 
     def __call__(self, logits: torch.Tensor, params: list, histories: list) -> torch.Tensor:
         """logits [B, V] (f32) -> int32 token ids [B] (on logits.device)."""
@@ -82,8 +98,9 @@ class Sampler:
             if p.logits_processor is not None:
                 allowed = p.logits_processor(histories[i])
                 if allowed is not None:
-                    a = np.asarray(allowed, dtype=np.int64)
-                    a = a[(a >= 0) & (a < V)]
+                    a = self._as_array(allowed)
+                    if len(a) and (a.min() < 0 or a.max() >= V):
+                        a = a[(a >= 0) & (a < V)]
                     flat.append(a + len(crow) * V)
                     crow.append(i)
         if crow:

@@ -83,8 +83,8 @@ class FakeCluster:
             self.pods.pop(k)
             self.logs.pop(k, None)
         ctr = dep["spec"]["template"]["spec"]["containers"][0]["name"]
-        i = 0
-        while len([k for k in self.pods if k[0] == ns and self.pods[k]["metadata"].get("labels", {}).get("app") == name]) < want:
+        have, i = min(len(mine), want), 0
+        while have < want:
             pname = f"{name}-{_suffix(name, i)}"
             i += 1
             if (ns, pname) in self.pods:
@@ -94,10 +94,19 @@ class FakeCluster:
                 "spec": {"nodeName": self.nodes[0]["metadata"]["name"], "containers": [{"name": ctr}]},
                 "status": {"phase": "Running"},
             }
-            self.logs[(ns, pname)] = "".join(
-                f"2025-09-17T10:{j // 60:02d}:{j % 60:02d}Z {name} GET /health 200 {self.rng.randint(1, 40)}ms\n"
-                for j in range(300))
+            self.logs[(ns, pname)] = None  # generated on first read (a scale to 90 replicas stays cheap)
+            have += 1
         dep["status"]["replicas"] = dep["status"]["readyReplicas"] = want
+
+    def _log_text(self, ns: str, pname: str) -> str:
+        text = self.logs.get((ns, pname))
+        if text is None:
+            app = self.pods[(ns, pname)]["metadata"].get("labels", {}).get("app", pname)
+            rng = random.Random(f"{ns}/{pname}")
+            text = "".join(f"2025-09-17T10:{j // 60:02d}:{j % 60:02d}Z {app} GET /health 200 {rng.randint(1, 40)}ms\n"
+                           for j in range(300))
+            self.logs[(ns, pname)] = text
+        return text
 
     # ------------------------------------------------------------ fault injection
     def _enter(self, op: str, *args):
@@ -122,7 +131,7 @@ class FakeCluster:
                 names = [c["name"] for c in self.pods[(namespace, name)]["spec"]["containers"]]
                 if container not in names:
                     raise K8sApiError(400, f"container {container} is not valid for pod {name}")
-            text = self.logs.get((namespace, name), "")
+            text = self._log_text(namespace, name) if (namespace, name) in self.logs else ""
         if tail_lines is not None:
             lines = text.splitlines(keepends=True)
             text = "".join(lines[-int(tail_lines):]) if int(tail_lines) > 0 else ""
