@@ -36,6 +36,8 @@ def main():
     g = torch.Generator().manual_seed(0)
     shared = torch.randint(10, 100000, (a.prefix,), generator=g).tolist()
     seqs = []
+    first = shared + torch.randint(10, 100000, (a.ctx - a.prefix,), generator=g).tolist()
+    eng.generate([first], SamplingParams.greedy(1))  # publish the shared prefix blocks
     for i in range(a.batch):
         tail = torch.randint(10, 100000, (a.ctx - a.prefix,), generator=g).tolist()
         seqs.append(eng.add_request(shared + tail, SamplingParams.greedy(10_000, ignore_eos=True)))

@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(
     const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ctx_lens, bf16_t* __restrict__ out, long os,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int BS, int max_splits,
-    int split, float scale_log2) {
+    int split, float scale_log2, const int* __restrict__ k_start, int has_prefix) {
   constexpr int KK = D / 32;     // QK k-steps (16x16x32)
   constexpr int ND = D / 16;     // PV output tiles of 16 d
   constexpr int CPR = D / 8;     // 16-B chunks per V row
@@ -50,10 +50,13 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(
   // order put every active workgroup of a short-context batch on ONE XCD).
   const int s = blockIdx.y, kvh = blockIdx.x % Hkv, b = blockIdx.x / Hkv;
   const int ctx = ctx_lens[b];
-  const int k_begin = s * split;
+  // cascade: keys [0, k0) are a prefix shared by the whole batch, attended by the flash
+  // kernel once for all rows (its partial is merged by decode_reduce_kernel)
+  const int k0 = k_start ? k_start[0] : 0;
+  const int k_begin = k0 + s * split;
   if (k_begin >= ctx) return;  // uniform for the whole workgroup
   const int nkeys = min(split, ctx - k_begin);
-  const int nsplit = min((ctx + split - 1) / split, max_splits);
+  const int nsplit = min((ctx - k0 + split - 1) / split, max_splits);
   const int Hq = Hkv * G;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r16 = lane & 15, h4 = lane >> 4;
@@ -207,7 +210,7 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(
       O += f * mrg_o[ww][g][d];
     }
     const int qh = kvh * G + g;
-    if (nsplit == 1) {
+    if (nsplit == 1 && !has_prefix) {
       out[(long)b * os + (long)qh * D + d] = f2bf(O / L);
     } else {
       const long pi = ((long)b * Hq + qh) * max_splits + s;
@@ -220,28 +223,39 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(
   }
 }
 
-// combine split partials: grid (Hq, B), D threads
+// combine split partials (+ the shared-prefix partial of a cascade step): grid (Hq, B), D threads
 template <int D>
 __global__ __launch_bounds__(D) void decode_reduce_kernel(const float* __restrict__ part_o,
                                                           const float* __restrict__ part_ml,
                                                           const int* __restrict__ ctx_lens,
                                                           bf16_t* __restrict__ out, long os,
-                                                          int Hq, int max_splits, int split) {
+                                                          int Hq, int max_splits, int split,
+                                                          const int* __restrict__ k_start,
+                                                          const float* __restrict__ pp_o,
+                                                          const float* __restrict__ pp_ml) {
   const int qh = blockIdx.x, b = blockIdx.y;
   const int ctx = ctx_lens[b];
-  const int nsplit = min((ctx + split - 1) / split, max_splits);
-  if (nsplit <= 1) return;  // written directly by the main kernel
+  const int k0 = k_start ? k_start[0] : 0;
+  const int nsplit = max(0, min((ctx - k0 + split - 1) / split, max_splits));
+  if (nsplit <= 1 && !pp_o) return;  // written directly by the main kernel
   const long base = ((long)b * Hq + qh) * max_splits;
-  float M = -INFINITY;
+  const long pb = (long)b * Hq + qh;
+  float M = pp_o ? pp_ml[pb * 2] : -INFINITY;
   for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_ml[(base + s) * 2]);
+  if (M == -INFINITY) M = 0.f;  // no keys at all (padding row)
   float den = 0.f, num = 0.f;
   const int d = threadIdx.x;
+  if (pp_o) {
+    const float f = exp2f(pp_ml[pb * 2] - M);
+    den = f * pp_ml[pb * 2 + 1];
+    num = f * pp_o[pb * D + d];
+  }
   for (int s = 0; s < nsplit; ++s) {
     const float f = exp2f(part_ml[(base + s) * 2] - M);
     den += f * part_ml[(base + s) * 2 + 1];
     num += f * part_o[(base + s) * D + d];
   }
-  out[(long)b * os + (long)qh * D + d] = f2bf(num / den);
+  out[(long)b * os + (long)qh * D + d] = f2bf(den > 0.f ? num / den : 0.f);
 }
 
 }  // namespace
@@ -261,7 +275,8 @@ int lk_decode_splits(int max_context, int split) { return (max_context + split -
 int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc,
                     const int* block_tables, int bt_stride, const int* ctx_lens, bf16_t* out,
                     long os, float* part_o, float* part_ml, int B, int Hq, int Hkv, int D, int BS,
-                    int max_splits, int split, float scale, hipStream_t st) {
+                    int max_splits, int split, float scale, const int* k_start, const float* pp_o,
+                    const float* pp_ml, hipStream_t st) {
   if (B == 0) return 0;
   if (Hq % Hkv || BS % 16 || split % 32 || split > kMaxSplit || split % BS) return -1;
   const int G = Hq / Hkv;
@@ -270,7 +285,8 @@ int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc
 #define LAUNCH(DD, GG)                                                                        \
   paged_decode_kernel<DD, GG><<<grid, 256, 0, st>>>(q, qs, kc, vc, block_tables, bt_stride,   \
                                                     ctx_lens, out, os, part_o, part_ml, Hkv, \
-                                                    BS, max_splits, split, scale_log2)
+                                                    BS, max_splits, split, scale_log2, k_start, \
+                                                    pp_o != nullptr)
 #define BY_G(DD)                          \
   switch (G) {                            \
     case 1: LAUNCH(DD, 1); break;         \
@@ -284,13 +300,13 @@ int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc
   else return -3;
 #undef BY_G
 #undef LAUNCH
-  if (max_splits > 1) {
+  if (max_splits > 1 || pp_o) {
     if (D == 128)
       decode_reduce_kernel<128><<<dim3(Hq, B), 128, 0, st>>>(part_o, part_ml, ctx_lens, out, os, Hq,
-                                                             max_splits, split);
+                                                             max_splits, split, k_start, pp_o, pp_ml);
     else
       decode_reduce_kernel<64><<<dim3(Hq, B), 64, 0, st>>>(part_o, part_ml, ctx_lens, out, os, Hq,
-                                                           max_splits, split);
+                                                           max_splits, split, k_start, pp_o, pp_ml);
   }
   return 0;
 }

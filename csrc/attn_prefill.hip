@@ -56,6 +56,11 @@ struct PrefillParams {
   long os;
   int Hq, Hkv, BS, bs_shift;  // BS is a power of two (paged cache block size)
   float scale_log2;
+  // partial mode (cascade decode over a shared prefix): instead of the normalised
+  // bf16 `out`, write the unnormalised f32 O [row][Hq][D] and (max, sum) [row][Hq][2]
+  // in the log2 domain of the split-K decode partials
+  float* part_o;
+  float* part_ml;
 };
 
 template <int D, bool CAUSAL, bool PAGED, int WH>
@@ -257,7 +262,20 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(PrefillParams p) 
   }
 
   // ---- epilogue: O^T lane layout: d = 32n + (i&3) + 8(i>>2) + 4h, query row = qrow
-  if (qvalid) {
+  if (qvalid && p.part_o) {
+    const long pr = (long)(qbeg + qrow) * p.Hq + head;
+    float* po = p.part_o + pr * D;
+#pragma unroll
+    for (int n = 0; n < ND; ++n)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+        *reinterpret_cast<floatx4*>(po + 32 * n + 8 * g4 + 4 * h) =
+            floatx4{o[n][4 * g4 + 0], o[n][4 * g4 + 1], o[n][4 * g4 + 2], o[n][4 * g4 + 3]};
+    if (h == 0) {
+      p.part_ml[pr * 2] = m_run;
+      p.part_ml[pr * 2 + 1] = l_run;
+    }
+  } else if (qvalid) {
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
     bf16_t* op = p.out + (long)(qbeg + qrow) * p.os + (long)head * D;
 #pragma unroll
@@ -281,7 +299,7 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
                      const int* block_tables, int bt_stride, const int* cu_q, const int* ctx_lens,
                      const int* tile_seq, const int* tile_q0, int ntiles, bf16_t* out, long os,
                      int Hq, int Hkv, int D, int BS, float scale, int causal, int paged,
-                     hipStream_t st) {
+                     float* part_o, float* part_ml, hipStream_t st) {
   if (ntiles == 0) return 0;
   if (Hq % Hkv) return -1;
   const int G = Hq / Hkv;
@@ -291,7 +309,7 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
   int bs_shift = 0;
   while ((1 << bs_shift) < BS) ++bs_shift;
   PrefillParams pr{q, qs, k, v, ks, vs, block_tables, bt_stride, cu_q, ctx_lens, tile_seq,
-                   tile_q0, out, os, Hq, Hkv, BS, bs_shift, scale * 1.4426950408889634f};
+                   tile_q0, out, os, Hq, Hkv, BS, bs_shift, scale * 1.4426950408889634f, part_o, part_ml};
   const int WH = G >= 4 ? 4 : G;
   dim3 grid(ntiles, Hq / WH);
 #define L(DD, C, PG, W) flash_prefill_kernel<DD, C, PG, W><<<grid, 256, 0, st>>>(pr)

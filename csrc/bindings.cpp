@@ -242,10 +242,15 @@ void kv_write(const at::Tensor& k, const at::Tensor& v, at::Tensor& k_cache, at:
 int64_t decode_splits(int64_t max_context, int64_t split) { return lk_decode_splits((int)max_context, (int)split); }
 int64_t decode_split_size(int64_t B, int64_t Hkv) { return lk_decode_split_size((int)B, (int)Hkv); }
 
+// k_start: optional device int32 [1] -- keys [0, k_start) are a prefix shared by every row,
+// attended separately (flash_prefill partial mode) into pp_o [B, Hq, D] / pp_ml [B, Hq, 2]
+// and merged by the reduce kernel (cascade decode).
 at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                         const at::Tensor& block_tables, const at::Tensor& ctx_lens, int64_t max_splits,
                         int64_t split, double scale, const c10::optional<at::Tensor>& part_o,
-                        const c10::optional<at::Tensor>& part_ml, const c10::optional<at::Tensor>& out_) {
+                        const c10::optional<at::Tensor>& part_ml, const c10::optional<at::Tensor>& out_,
+                        const c10::optional<at::Tensor>& k_start, const c10::optional<at::Tensor>& pp_o,
+                        const c10::optional<at::Tensor>& pp_ml) {
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
   CHECK_I32(block_tables); CHECK_I32(ctx_lens); CHECK_CONTIG(ctx_lens);
   TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == q.size(2), "q must be [B, Hq, D] (row-strided)");
@@ -258,19 +263,29 @@ at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at
   TORCH_CHECK(split >= 32 && split <= 2048 && split % 32 == 0 && split % BS == 0, "decode split must be a multiple of 32 and of the block size, <= 2048");
   TORCH_CHECK(max_splits >= 1 && (long)(max_splits - 1) * split < (long)block_tables.size(1) * BS, "max_splits exceeds block table capacity");
   check_rows16(q, "q");
+  const bool cascade = pp_o.has_value();
+  TORCH_CHECK(cascade == pp_ml.has_value() && cascade == k_start.has_value(), "cascade needs k_start, pp_o and pp_ml");
+  if (cascade) {
+    CHECK_CUDA(*k_start); CHECK_I32(*k_start); TORCH_CHECK(k_start->numel() >= 1, "k_start");
+    CHECK_F32(*pp_o); CHECK_F32(*pp_ml); CHECK_CONTIG(*pp_o); CHECK_CONTIG(*pp_ml);
+    TORCH_CHECK(pp_o->numel() >= (long)B * Hq * D && pp_ml->numel() >= (long)B * Hq * 2, "prefix partials too small");
+  }
   at::Tensor out = out_ ? *out_ : at::empty({B, Hq, D}, q.options());
   TORCH_CHECK(out.size(0) == B && out.size(1) == Hq && out.size(2) == D && out.stride(2) == 1 && out.stride(1) == D, "out layout");
   at::Tensor po, pm;
-  if (max_splits > 1) {
+  const bool parts = max_splits > 1 || cascade;
+  if (parts) {
     po = part_o ? *part_o : at::empty({B, Hq, max_splits, D}, q.options().dtype(at::kFloat));
     pm = part_ml ? *part_ml : at::empty({B, Hq, max_splits, 2}, q.options().dtype(at::kFloat));
     TORCH_CHECK(po.numel() >= (long)B * Hq * max_splits * D && pm.numel() >= (long)B * Hq * max_splits * 2, "partials too small");
     CHECK_F32(po); CHECK_F32(pm);
   }
   int rc = lk_paged_decode(bp(q), q.stride(0), bp(k_cache), bp(v_cache), ip(block_tables), block_tables.stride(0),
-                           ip(ctx_lens), bp(out), out.stride(0), max_splits > 1 ? po.data_ptr<float>() : nullptr,
-                           max_splits > 1 ? pm.data_ptr<float>() : nullptr, B, Hq, Hkv, D, BS, (int)max_splits,
-                           (int)split, (float)scale, cur_stream());
+                           ip(ctx_lens), bp(out), out.stride(0), parts ? po.data_ptr<float>() : nullptr,
+                           parts ? pm.data_ptr<float>() : nullptr, B, Hq, Hkv, D, BS, (int)max_splits,
+                           (int)split, (float)scale, cascade ? ip(*k_start) : nullptr,
+                           cascade ? pp_o->data_ptr<float>() : nullptr, cascade ? pp_ml->data_ptr<float>() : nullptr,
+                           cur_stream());
   CHECK_RC(rc, "paged_decode");
   return out;
 }
@@ -281,7 +296,8 @@ at::Tensor flash_prefill(const at::Tensor& q, const at::Tensor& k, const at::Ten
                          const c10::optional<at::Tensor>& block_tables, const at::Tensor& cu_q,
                          const c10::optional<at::Tensor>& ctx_lens, const at::Tensor& tile_seq,
                          const at::Tensor& tile_q0, int64_t Hq, int64_t Hkv, int64_t D, double scale,
-                         bool causal, const c10::optional<at::Tensor>& out_) {
+                         bool causal, const c10::optional<at::Tensor>& out_,
+                         const c10::optional<at::Tensor>& part_o, const c10::optional<at::Tensor>& part_ml) {
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); CHECK_LASTDIM(q);
   CHECK_I32(cu_q); CHECK_I32(tile_seq); CHECK_I32(tile_q0);
   TORCH_CHECK(q.dim() == 2 && q.size(1) >= Hq * D, "q must be [T, >=Hq*D] (head-major rows)");
@@ -304,13 +320,23 @@ at::Tensor flash_prefill(const at::Tensor& q, const at::Tensor& k, const at::Ten
   }
   if (ctx_lens) CHECK_I32(*ctx_lens);
   TORCH_CHECK(tile_seq.numel() == tile_q0.numel(), "tile arrays");
-  at::Tensor out = out_ ? *out_ : at::empty({T, Hq * D}, q.options());
-  CHECK_LASTDIM(out); check_rows16(out, "out");
-  TORCH_CHECK(out.size(0) == T && out.size(1) >= Hq * D, "out shape");
+  const bool partial = part_o.has_value();
+  TORCH_CHECK(partial == part_ml.has_value(), "partial mode needs part_o and part_ml");
+  if (partial) {
+    CHECK_F32(*part_o); CHECK_F32(*part_ml); CHECK_CONTIG(*part_o); CHECK_CONTIG(*part_ml);
+    TORCH_CHECK(part_o->numel() >= T * Hq * D && part_ml->numel() >= T * Hq * 2, "partials too small");
+    TORCH_CHECK(D % 4 == 0, "partial mode needs D % 4 == 0");
+  }
+  at::Tensor out = out_ ? *out_ : (partial ? *part_o : at::empty({T, Hq * D}, q.options()));
+  if (!partial) {
+    CHECK_LASTDIM(out); check_rows16(out, "out");
+    TORCH_CHECK(out.size(0) == T && out.size(1) >= Hq * D, "out shape");
+  }
   int rc = lk_flash_prefill(bp(q), q.stride(0), bp(k), bp(v), ks, vs, paged ? ip(*block_tables) : nullptr,
                             bt_stride, ip(cu_q), ipo(ctx_lens), ip(tile_seq), ip(tile_q0), tile_seq.numel(),
-                            bp(out), out.stride(0), Hq, Hkv, D, BS, (float)scale, causal ? 1 : 0, paged ? 1 : 0,
-                            cur_stream());
+                            partial ? nullptr : bp(out), partial ? 0 : out.stride(0), Hq, Hkv, D, BS, (float)scale,
+                            causal ? 1 : 0, paged ? 1 : 0, partial ? part_o->data_ptr<float>() : nullptr,
+                            partial ? part_ml->data_ptr<float>() : nullptr, cur_stream());
   CHECK_RC(rc, "flash_prefill");
   return out;
 }
@@ -438,9 +464,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("kv_write", &kv_write);
   m.def("decode_splits", &decode_splits);
   m.def("decode_split_size", &decode_split_size);
-  m.def("paged_decode", &paged_decode, "", py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("max_splits"), py::arg("split"), py::arg("scale"), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("out") = py::none());
+  m.def("paged_decode", &paged_decode, "", py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("max_splits"), py::arg("split"), py::arg("scale"), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("out") = py::none(), py::arg("k_start") = py::none(), py::arg("pp_o") = py::none(), py::arg("pp_ml") = py::none());
   m.def("prefill_rows_per_tile", &prefill_rows_per_tile);
-  m.def("flash_prefill", &flash_prefill, "", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("block_tables"), py::arg("cu_q"), py::arg("ctx_lens"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("out") = py::none());
+  m.def("flash_prefill", &flash_prefill, "", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("block_tables"), py::arg("cu_q"), py::arg("ctx_lens"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("out") = py::none(), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none());
   m.def("knn_topk", &knn_topk, "", py::arg("corpus"), py::arg("cnorm"), py::arg("queries"), py::arg("qnorm"),
         py::arg("K"), py::arg("force_fused") = false);
   m.def("knn_merge", &knn_merge);

@@ -51,7 +51,8 @@ int lk_decode_splits(int max_context, int split);
 int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc,
                     const int* block_tables, int bt_stride, const int* ctx_lens, bf16_t* out,
                     long os, float* part_o, float* part_ml, int B, int Hq, int Hkv, int D, int BS,
-                    int max_splits, int split, float scale, hipStream_t st);
+                    int max_splits, int split, float scale, const int* k_start, const float* pp_o,
+                    const float* pp_ml, hipStream_t st);
 
 // attn_prefill.hip
 int lk_prefill_rows_per_tile(int G);
@@ -59,7 +60,7 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
                      const int* block_tables, int bt_stride, const int* cu_q, const int* ctx_lens,
                      const int* tile_seq, const int* tile_q0, int ntiles, bf16_t* out, long os,
                      int Hq, int Hkv, int D, int BS, float scale, int causal, int paged,
-                     hipStream_t st);
+                     float* part_o, float* part_ml, hipStream_t st);
 
 // knn.hip
 int lk_knn_nblocks(long N);

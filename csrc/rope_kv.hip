@@ -11,75 +11,78 @@
 
 namespace {
 
+// grid (T, ceil(items / 64)), 64 threads: one 16-B rotation item (or V chunk) per
+// thread, so a decode step (T ~ 128 tokens) still puts ~900 single-wave workgroups
+// on the 256 CUs instead of 128 workgroups each looping over 3 dependent items.
 template <bool NEOX>
-__global__ __launch_bounds__(128) void rope_kv_kernel(
+__global__ __launch_bounds__(64) void rope_kv_kernel(
     bf16_t* __restrict__ qkv, long qs, const int* __restrict__ positions,
     const float* __restrict__ cos_sin, int Hq, int Hkv, int D, bf16_t* __restrict__ kc,
     bf16_t* __restrict__ vc, const int* __restrict__ slots, int BS, int write_k_inplace) {
   const long t = blockIdx.x;
-  const int pos = positions[t];
+  const int it = blockIdx.y * 64 + threadIdx.x;
   const int half = D >> 1;
-  const float* cs = cos_sin + (long)pos * D;  // [cos(D/2) | sin(D/2)]
+  const int ipr = NEOX ? (D >> 4) : (D >> 3);  // rotation items per head
+  const int nrot = (Hq + Hkv) * ipr;
+  const int vpr = D >> 3;
+  if (it >= nrot + Hkv * vpr) return;
   bf16_t* row = qkv + t * qs;
   const int slot = slots ? slots[t] : -1;
   LK_DASSERT(slot >= -1);
   const long blk = slot >= 0 ? slot / BS : 0;
   const int off = slot >= 0 ? slot % BS : 0;
-  const int ipr = NEOX ? (D >> 4) : (D >> 3);  // items per head
-  const int nrot = (Hq + Hkv) * ipr;
-  for (int it = threadIdx.x; it < nrot; it += blockDim.x) {
-    const int head = it / ipr;
-    const int v = it - head * ipr;
-    bf16_t* hp = row + head * D;
-    const bool is_k = head >= Hq;
-    const int kvh = head - Hq;
-    bf16_t* kdst = (is_k && kc && slot >= 0) ? kc + ((blk * Hkv + kvh) * BS + off) * D : nullptr;
-    const bool store_src = !is_k || write_k_inplace;
-    if constexpr (NEOX) {
-      const int i0 = v * 8;
-      float x1[8], x2[8], c[8], s[8], y1[8], y2[8];
-      load8(hp + i0, x1);
-      load8(hp + half + i0, x2);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        c[j] = cs[i0 + j];
-        s[j] = cs[half + i0 + j];
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        y1[j] = x1[j] * c[j] - x2[j] * s[j];
-        y2[j] = x2[j] * c[j] + x1[j] * s[j];
-      }
-      if (store_src) {
-        store8(hp + i0, y1);
-        store8(hp + half + i0, y2);
-      }
-      if (kdst) {
-        store8(kdst + i0, y1);
-        store8(kdst + half + i0, y2);
-      }
-    } else {
-      const int e0 = v * 8;  // elements e0..e0+7 = pairs e0/2 .. e0/2+3
-      float x[8], y[8];
-      load8(hp + e0, x);
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const float c = cs[(e0 >> 1) + p], s = cs[half + (e0 >> 1) + p];
-        y[2 * p] = x[2 * p] * c - x[2 * p + 1] * s;
-        y[2 * p + 1] = x[2 * p + 1] * c + x[2 * p] * s;
-      }
-      if (store_src) store8(hp + e0, y);
-      if (kdst) store8(kdst + e0, y);
-    }
-  }
-  if (vc && slot >= 0) {
-    const int vpr = D >> 3;
-    const bf16_t* vsrc = row + (long)(Hq + Hkv) * D;
-    for (int it = threadIdx.x; it < Hkv * vpr; it += blockDim.x) {
-      const int h = it / vpr, c = (it - h * vpr) * 8;
+  if (it >= nrot) {  // V: plain copy into the cache
+    if (vc && slot >= 0) {
+      const int i = it - nrot, h = i / vpr, c = (i - h * vpr) * 8;
       *reinterpret_cast<short8*>(vc + ((blk * Hkv + h) * BS + off) * D + c) =
-          *reinterpret_cast<const short8*>(vsrc + h * D + c);
+          *reinterpret_cast<const short8*>(row + (long)(Hq + Hkv + h) * D + c);
     }
+    return;
+  }
+  const float* cs = cos_sin + (long)positions[t] * D;  // [cos(D/2) | sin(D/2)]
+  const int head = it / ipr;
+  const int v = it - head * ipr;
+  bf16_t* hp = row + head * D;
+  const bool is_k = head >= Hq;
+  const int kvh = head - Hq;
+  bf16_t* kdst = (is_k && kc && slot >= 0) ? kc + ((blk * Hkv + kvh) * BS + off) * D : nullptr;
+  const bool store_src = !is_k || write_k_inplace;
+  if constexpr (NEOX) {
+    const int i0 = v * 8;
+    float x1[8], x2[8], y1[8], y2[8];
+    load8(hp + i0, x1);
+    load8(hp + half + i0, x2);
+    const floatx4 c0 = *reinterpret_cast<const floatx4*>(cs + i0);
+    const floatx4 c1 = *reinterpret_cast<const floatx4*>(cs + i0 + 4);
+    const floatx4 s0 = *reinterpret_cast<const floatx4*>(cs + half + i0);
+    const floatx4 s1 = *reinterpret_cast<const floatx4*>(cs + half + i0 + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float c = j < 4 ? c0[j] : c1[j - 4], s = j < 4 ? s0[j] : s1[j - 4];
+      y1[j] = x1[j] * c - x2[j] * s;
+      y2[j] = x2[j] * c + x1[j] * s;
+    }
+    if (store_src) {
+      store8(hp + i0, y1);
+      store8(hp + half + i0, y2);
+    }
+    if (kdst) {
+      store8(kdst + i0, y1);
+      store8(kdst + half + i0, y2);
+    }
+  } else {
+    const int e0 = v * 8;  // elements e0..e0+7 = pairs e0/2 .. e0/2+3
+    float x[8], y[8];
+    load8(hp + e0, x);
+    const floatx4 c4 = *reinterpret_cast<const floatx4*>(cs + (e0 >> 1));
+    const floatx4 s4 = *reinterpret_cast<const floatx4*>(cs + half + (e0 >> 1));
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      y[2 * p] = x[2 * p] * c4[p] - x[2 * p + 1] * s4[p];
+      y[2 * p + 1] = x[2 * p + 1] * c4[p] + x[2 * p] * s4[p];
+    }
+    if (store_src) store8(hp + e0, y);
+    if (kdst) store8(kdst + e0, y);
   }
 }
 
@@ -111,12 +114,14 @@ int lk_rope_kv(bf16_t* qkv, long qs, const int* positions, const float* cos_sin,
                int write_k_inplace, hipStream_t st) {
   if (D % 16 || T < 0) return -1;
   if (T == 0) return 0;
+  const int items = (Hq + Hkv) * (neox ? D / 16 : D / 8) + Hkv * (D / 8);
+  const dim3 grid((unsigned)T, (items + 63) / 64);
   if (neox)
-    rope_kv_kernel<true><<<dim3(T), 128, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc,
-                                                  slots, BS, write_k_inplace);
+    rope_kv_kernel<true><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,
+                                              write_k_inplace);
   else
-    rope_kv_kernel<false><<<dim3(T), 128, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc,
-                                                   vc, slots, BS, write_k_inplace);
+    rope_kv_kernel<false><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,
+                                               write_k_inplace);
   return 0;
 }
 

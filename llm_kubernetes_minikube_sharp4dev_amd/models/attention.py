@@ -50,6 +50,16 @@ class AttnMeta:
     decode_split: Optional[int] = None
     part_o: Optional[torch.Tensor] = None
     part_ml: Optional[torch.Tensor] = None
+    # cascade decode: the first shared_len (device int32 [1]) keys of every decode row are
+    # the same cache blocks (the batch's common system prompt): attended once for all rows
+    # by the flash kernel (queries = the decode rows, keys = shared_tables' blocks) into
+    # (pp_o, pp_ml), merged by the split-K reduce
+    shared_len: Optional[torch.Tensor] = None
+    shared_cu: Optional[torch.Tensor] = None
+    shared_tables: Optional[torch.Tensor] = None
+    shared_tiles: Optional[tuple] = None
+    pp_o: Optional[torch.Tensor] = None
+    pp_ml: Optional[torch.Tensor] = None
     # rows whose hidden state feeds the LM head (last token of each prefill + decode rows)
     logits_idx: Optional[torch.Tensor] = None
 
@@ -77,8 +87,15 @@ def paged_attention(qkv: torch.Tensor, k_cache, v_cache, meta: AttnMeta, Hq: int
     def decode():
         q = qkv[Tp:Tp + Bd, : Hq * D].view(Bd, Hq, D)
         o = out[Tp:Tp + Bd].view(Bd, Hq, D)
+        prefix = None
+        if meta.shared_len is not None:
+            ops.flash_prefill(qkv[Tp:Tp + Bd, : Hq * D], k_cache, v_cache, meta.shared_cu, Hq, Hkv, D, scale,
+                              False, block_tables=meta.shared_tables, ctx_lens=meta.shared_len,
+                              tiles=meta.shared_tiles, part=(meta.pp_o, meta.pp_ml))
+            prefix = (meta.pp_o, meta.pp_ml)
         ops.paged_decode(q, k_cache, v_cache, meta.block_tables_d, meta.ctx_lens_d, scale,
-                         meta.max_splits, meta.part_o, meta.part_ml, out=o, split=meta.decode_split)
+                         meta.max_splits, meta.part_o, meta.part_ml, out=o, split=meta.decode_split,
+                         k_start=meta.shared_len, prefix=prefix)
 
     side = None
     if (Tp and Bd and OVERLAP_ATTN and qkv.is_cuda and not torch.cuda.is_current_stream_capturing()):

@@ -103,18 +103,24 @@ def decode_splits(max_context: int, split: int) -> int:
 
 
 def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_splits: Optional[int] = None,
-                 part_o=None, part_ml=None, out=None, split: Optional[int] = None):
+                 part_o=None, part_ml=None, out=None, split: Optional[int] = None, k_start=None, prefix=None):
     """q [B, Hq, D] -> [B, Hq, D].  ``split`` keys per workgroup (default from
     :func:`decode_split_size`), ``max_splits`` = splits covering the block-table width —
-    both static, so the launch is hipGraph-capturable."""
+    both static, so the launch is hipGraph-capturable.
+
+    Cascade: ``k_start`` (device int32 [1]) keys are a prefix shared by every row whose
+    attention was computed once for the batch by :func:`flash_prefill` in partial mode
+    into ``prefix`` = (o [B, Hq, D], ml [B, Hq, 2]); this call attends the rest and
+    merges (the CPU reference attends everything directly)."""
     if use_hip(q):
         BS = k_cache.shape[2]
         if split is None:
             split = max(decode_split_size(q.shape[0], k_cache.shape[1]), BS)
         if max_splits is None:
             max_splits = decode_splits(block_tables.shape[1] * BS, split)
+        pp_o, pp_ml = prefix if prefix is not None else (None, None)
         return lib().paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, max_splits, split, scale,
-                                  part_o, part_ml, out)
+                                  part_o, part_ml, out, k_start, pp_o, pp_ml)
     y = ref.paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
     if out is not None:
         out.copy_(y)
@@ -143,9 +149,11 @@ def prefill_tiles(q_lens: Sequence[int], ctx_lens: Sequence[int], G: int, causal
 
 def flash_prefill(q, k, v, cu_q, Hq: int, Hkv: int, D: int, scale: float, causal: bool,
                   block_tables=None, ctx_lens=None, q_lens_cpu=None, ctx_lens_cpu=None,
-                  tiles=None, out=None):
+                  tiles=None, out=None, part=None):
     """Varlen flash attention.  Paged when ``block_tables`` is given (K/V caches
     ``[NB, Hkv, BS, D]``), else dense K/V rows ``[T, >=Hkv*D]`` (encoder).
+    ``part`` = (o f32 [T, Hq, D], ml f32 [T, Hq, 2]): write unnormalised partials for a
+    cascade merge instead of ``out`` (GPU only).
 
     ``q_lens_cpu`` / ``ctx_lens_cpu``: host copies of the lengths (the scheduler has
     them), used to build the tile list without a device sync."""
@@ -164,8 +172,9 @@ def flash_prefill(q, k, v, cu_q, Hq: int, Hkv: int, D: int, scale: float, causal
             ts, tq = prefill_tiles(q_lens_cpu, ctx_lens_cpu, Hq // Hkv, causal)
             tiles = (torch.from_numpy(ts).to(q.device, non_blocking=True),
                      torch.from_numpy(tq).to(q.device, non_blocking=True))
+        pp_o, pp_ml = part if part is not None else (None, None)
         return lib().flash_prefill(q, k, v, block_tables, cu_q, ctx_lens, tiles[0], tiles[1], Hq,
-                                   Hkv, D, scale, causal, out)
+                                   Hkv, D, scale, causal, out, pp_o, pp_ml)
     y = ref.flash_prefill(q, k, v, block_tables, cu_q, ctx_lens, Hq, Hkv, D, scale, causal)
     if out is not None:
         out[:, : Hq * D].copy_(y)

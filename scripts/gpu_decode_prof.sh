@@ -13,4 +13,4 @@ rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
 for r in rows[:25]:
     print(f'{float(r["TotalDurationNs"])/1e6:9.2f} ms {int(r["Calls"]):7d} calls {float(r["AverageNs"])/1e3:8.2f} us  {r["Name"][:110]}')
 PY
-rm -f $R/gpurun_out/prof_dec/*/run_kernel_trace.csv $R/gpurun_out/prof_dec/run_kernel_trace.csv
+t=$(ls $R/gpurun_out/prof_dec/*/run_kernel_trace.csv $R/gpurun_out/prof_dec/run_kernel_trace.csv 2>/dev/null | head -1); python3 $R/scripts/summarize_trace.py $t 0.2 > $R/gpurun_out/decode_window.md; rm -f $t

@@ -94,6 +94,31 @@ def test_pipelined_steps_equal_synchronous(graphs):
         assert drive(True, mk) == ref
 
 
+def test_cascade_decode_engine_matches_plain(monkeypatch):
+    """Requests sharing a long prompt prefix (prefix-cache hits on the same blocks) decode
+    with the cascade path (shared blocks attended once per step) -- eager and graphed --
+    to the same tokens as engines with cascade off."""
+    _, m = _gpu_llama()
+    base = list(range(40, 40 + 70))
+    prompts = [base + [300 + i, 7, 9 + i] for i in range(6)]
+
+    def run(cascade, graphs):
+        monkeypatch.setenv("LK_CASCADE", "1" if cascade else "0")
+        eng = _engine(m, use_graphs=graphs)
+        if graphs:
+            eng.runner.capture_all(max_batch=8)
+        eng.generate([prompts[0]], SamplingParams.greedy(2))  # publish the shared prefix blocks
+        seqs = [eng.add_request(p, SamplingParams.greedy(10)) for p in prompts]
+        eng.run_until_done(seqs)
+        assert cascade == eng.runner.cascade
+        assert all(s.num_cached_prefix >= 64 for s in seqs)
+        return [s.output_ids for s in seqs]
+
+    ref = run(False, False)
+    assert run(True, False) == ref
+    assert run(True, True) == ref
+
+
 def test_bert_gpu_matches_hf_fp32():
     cfg = transformers.BertConfig(vocab_size=300, hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
                                   intermediate_size=1024, max_position_embeddings=128, hidden_act="gelu")

@@ -130,6 +130,43 @@ def test_paged_decode(hip, G, D):
         _close(y, y_ref, 0.02, 0.0, f"paged decode split={split}")
 
 
+@pytest.mark.parametrize("G", [1, 4, 8])
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("S", [0, 3, 18])
+def test_cascade_decode(hip, G, D, S):
+    """Cascade decode: the first S blocks are the same cache blocks in every row's table
+    (a prefix-cached system prompt); the flash kernel attends them once for all rows into
+    f32 partials, the split-K decode attends the rest and merges -- vs the fp32 reference
+    over the whole context (S=0: empty prefix, merge of a no-key partial)."""
+    torch.manual_seed(9)
+    Hkv, BS = 2, 16
+    Hq = Hkv * G
+    ctx = [S * BS + e for e in (1, 17, 300, 16, 900, 1, 64, 2)]
+    B = len(ctx)
+    kc, vc, bt = _paged_setup(B, ctx, Hkv, D, BS, seed=10)
+    if S:
+        bt[:, :S] = bt[0, :S]  # shared prefix blocks
+    q = torch.randn(B, Hq * D, device=DEV, dtype=torch.bfloat16)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    scale = 1 / math.sqrt(D)
+    y_ref = ref.paged_decode(q.view(B, Hq, D), kc, vc, bt, cl, scale)
+    k0 = torch.tensor([S * BS], dtype=torch.int32, device=DEV)
+    rpt = ops.prefill_rows_per_tile(G)
+    nt = (B + rpt - 1) // rpt
+    tiles = (torch.zeros(nt, dtype=torch.int32, device=DEV),
+             torch.arange(0, nt * rpt, rpt, dtype=torch.int32, device=DEV))
+    pp_o = torch.empty(B, Hq, D, device=DEV)
+    pp_ml = torch.empty(B, Hq, 2, device=DEV)
+    cu = torch.tensor([0, B], dtype=torch.int32, device=DEV)
+    for split in (128, 2048):
+        ops.flash_prefill(q, kc, vc, cu, Hq, Hkv, D, scale, False, block_tables=bt[0:1], ctx_lens=k0,
+                          tiles=tiles, part=(pp_o, pp_ml))
+        max_splits = ops.decode_splits(bt.shape[1] * BS, split)
+        y = ops.paged_decode(q.view(B, Hq, D), kc, vc, bt, cl, scale, max_splits, split=split, k_start=k0,
+                             prefix=(pp_o, pp_ml))
+        _close(y, y_ref, 0.02, 0.0, f"cascade decode S={S} split={split}")
+
+
 @pytest.mark.parametrize("G", [1, 2, 4, 8])
 @pytest.mark.parametrize("D", [64, 128])
 def test_flash_prefill_paged(G, D):
