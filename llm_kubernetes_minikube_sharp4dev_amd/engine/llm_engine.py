@@ -104,10 +104,9 @@ class LLMEngine:
     @torch.inference_mode()
     def step_pipelined(self) -> list:
         """One pipelined iteration; returns the sequences that got a token (from the
-        PREVIOUS launch).  Call :meth:`flush` when done.  Falls back to :meth:`step`
-        under tensor parallelism (the worker ranks replay host-built inputs)."""
-        if self.runner.step_hook is not None:
-            return self.step()
+        PREVIOUS launch).  Call :meth:`flush` when done.  Under tensor parallelism the
+        worker ranks gather the in-flight inputs from their own copy of greedy ids, or
+        from the driver's sampled ids broadcast over the TP group."""
         nxt = self._launch()
         out = self._collect(self._inflight) if self._inflight is not None else []
         self._inflight = self._sample(nxt) if nxt is not None else None
@@ -161,6 +160,7 @@ class LLMEngine:
             for i, s in enumerate(seqs):
                 s.num_inflight, s.inflight_row = 1, i
             self.runner.prev_ids = ids
+            self.runner.prev_sampled_rows = 0 if greedy else len(rows)
         return (batch, rows, host, ev, ts, t0, t1, time.perf_counter(), ev0)
 
     def _collect(self, pending) -> list:

@@ -71,6 +71,7 @@ class ModelRunner:
         self._ws = None
         self.step_hook = None
         self.prev_ids: Optional[torch.Tensor] = None  # previous step's sampled ids (device)
+        self.prev_sampled_rows = 0  # rows of prev_ids sampled on the driver only (non-greedy step)
         self.gemm_tuning = {}
         if self.device.type == "cuda" and os.environ.get("LK_BIG_GEMM", "1") != "0" and hasattr(model, "gemm_shapes"):
             # pick hipBLASLt vs the big-tile MFMA kernel per prefill-step M bucket (~0.5 s)
@@ -284,14 +285,35 @@ class ModelRunner:
     def execute(self, si: "StepInputs"):
         """Run one step on this rank; returns logits [R, V] f32, or int32 token ids [R]
         for a greedy step (None if no rows)."""
+        self._sync_prev(si)
         if si.decode_graph:
-            return self._graph_execute(si)
-        ids, meta = self._meta(si)
-        if meta.logits_idx is None:
-            self.model(ids, meta, self.kv_caches)  # partial prefill chunks only: KV write, no logits
-            return None
-        h = self.model(ids, meta, self.kv_caches)
-        return self.model.greedy(h) if si.greedy else self.model.logits(h)
+            out = self._graph_execute(si)
+        else:
+            ids, meta = self._meta(si)
+            if meta.logits_idx is None:
+                self.model(ids, meta, self.kv_caches)  # partial prefill chunks only: KV write, no logits
+                return None
+            h = self.model(ids, meta, self.kv_caches)
+            out = self.model.greedy(h) if si.greedy else self.model.logits(h)
+        if si.greedy:
+            self.prev_ids = out  # every TP rank holds the same greedy ids (distributed argmax)
+        return out
+
+    def _sync_prev(self, si: "StepInputs"):
+        """Pipelined TP steps: ids sampled by the driver (non-greedy previous step) exist on
+        rank 0 only; broadcast them over the TP device group (RCCL, no host round trip)
+        before this step gathers its in-flight decode inputs from them."""
+        tp = getattr(self.model, "tp", None)
+        if not si.prev_bcast or tp is None or not tp.enabled:
+            return
+        import torch.distributed as dist
+
+        if tp.rank == 0:
+            buf = self.prev_ids[: si.prev_bcast].to(torch.int32).contiguous()
+        else:
+            buf = torch.empty(si.prev_bcast, dtype=torch.int32, device=self.device)
+        dist.broadcast(buf, src=tp.ranks[0] if tp.ranks else 0, group=tp.group)
+        self.prev_ids = buf
 
     def forward_logits(self, items, greedy: bool = False):
         """Run one step; returns (rows [(seq,row)], logits [R, V] f32 -- or int32 token
@@ -299,6 +321,8 @@ class ModelRunner:
         if not items:
             return [], None
         si, rows = self.prepare(items, greedy)
+        if si.gather is not None:
+            si.prev_bcast = self.prev_sampled_rows
         if self.step_hook is not None:
             self.step_hook(si)  # e.g. TP driver broadcast to worker ranks
         lg = self.execute(si)
@@ -391,3 +415,4 @@ class StepInputs:
     greedy: bool = False                  # return token ids (argmax) instead of logits
     gather: Optional[tuple] = None        # (dst rows, src rows): in-flight ids from the previous step
     shared_len: int = 0                   # cascade: leading keys shared by every decode row
+    prev_bcast: int = 0                   # TP: rows of driver-sampled previous ids to broadcast

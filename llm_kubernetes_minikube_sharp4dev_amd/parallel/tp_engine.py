@@ -119,10 +119,13 @@ def run_tp_worker(model, tp: TPGroup, **runner_kw):
     runner, ctrl = make_tp_runner(model, tp, **runner_kw)
     wd = StepWatchdog(f"tp-worker-{tp.rank}", stall_s=stall_s)
     n = 0
+    pending: list = []
     while True:
         cmd, arg = ctrl.bcast(None)  # idle wait for the driver: not a stall
         wd.beat()
         if cmd == "stop":
+            for ev in pending:
+                ev.synchronize()
             break
         if cmd == "capture":
             runner.capture(*arg)
@@ -134,7 +137,13 @@ def run_tp_worker(model, tp: TPGroup, **runner_kw):
             with wd.busy():  # a step that never returns (dead peer in an all-reduce) is a stall
                 runner.execute(arg)
                 if torch.cuda.is_available() and model.device.type == "cuda":
-                    torch.cuda.synchronize()
+                    # keep <= 2 steps in flight (the driver pipelines: step N+1's inputs
+                    # arrive before step N is done, so the device never idles waiting here)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    pending.append(ev)
+                    if len(pending) > 2:
+                        pending.pop(0).synchronize()
             n += 1
     wd.stop()
     log.info("tp worker rank %d done after %d steps", tp.rank, n)

@@ -55,6 +55,62 @@ def _hf(arch):
 PROMPTS = [[5, 17, 99, 3, 250, 7, 7, 1, 400, 33, 21, 8, 2, 9, 11, 60, 61, 62, 63], [7, 8, 9], list(range(10, 60))]
 
 
+def _proc(hist):  # history-dependent constraint: non-greedy path (driver-side sampling)
+    return list(range(1 + (len(hist) % 5), 512, 3))
+
+
+def _drive(eng, pipelined: bool, constrained: bool):
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import SamplingParams
+
+    mk = (lambda: SamplingParams.greedy(10, logits_processor=_proc)) if constrained else (lambda: SamplingParams.greedy(10))
+    seqs = [eng.add_request(p, mk()) for p in PROMPTS[:2]]
+    it = 0
+    while eng.has_work() or len(seqs) < len(PROMPTS):
+        if it == 3:
+            seqs += [eng.add_request(p, mk()) for p in PROMPTS[2:]]
+        eng.step_pipelined() if pipelined else eng.step()
+        it += 1
+    eng.flush()
+    return [s.output_ids for s in seqs]
+
+
+def _tp_pipelined_worker(rank, world, port, out_path):
+    _init(rank, world, port)
+    from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp import TPGroup
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp_engine import make_tp_engine, run_tp_worker, shutdown_tp
+
+    tp = TPGroup(rank, world, dist.group.WORLD)
+    m = build_decoder(_ours_cfg("llama"), dtype=torch.float32, tp=tp)
+    m.load_hf_state_dict(_hf("llama").state_dict())
+    kw = dict(block_size=16, max_model_len=512, max_num_seqs=8, num_blocks=96)
+    if rank == 0:
+        eng = make_tp_engine(m, tp, None, engine_kw={"eos_ids": set(), "max_num_batched_tokens": 40}, **kw)
+        got = [_drive(eng, True, c) for c in (False, True)]
+        shutdown_tp(eng)
+        torch.save(got, out_path)
+    else:
+        run_tp_worker(m, tp, **kw)
+    dist.destroy_process_group()
+
+
+def test_tp2_pipelined_steps_match_synchronous_single_process():
+    """Pipelined stepping under TP=2 (workers gather in-flight inputs from their greedy ids,
+    or from the driver's sampled ids broadcast over the TP group) == one process, sync."""
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.llm_engine import LLMEngine
+    from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder
+
+    m = build_decoder(_ours_cfg("llama"), dtype=torch.float32)
+    m.load_hf_state_dict(_hf("llama").state_dict())
+    ref = [_drive(LLMEngine(m, None, max_model_len=512, max_num_seqs=8, num_blocks=96, eos_ids=set(),
+                            max_num_batched_tokens=40), False, c) for c in (False, True)]
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "out.pt")
+        mp.spawn(_tp_pipelined_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+        got = torch.load(out, weights_only=True)
+    assert got == ref
+
+
 def _tp_worker(rank, world, port, arch, out_path, sp_min_tokens=None):
     _init(rank, world, port)
     from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import SamplingParams
