@@ -273,6 +273,12 @@ def main():
         sync()
         engine.step_trace = []
         load_host0 = dict(load.host_s) if load is not None else {}
+        prof = None
+        if os.environ.get("LK_PROFILE_TIMED"):  # host-side cProfile of the timed window only
+            import cProfile
+
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         if load is not None:
             results.extend(load.run(args.steps * args.batch))
@@ -283,6 +289,9 @@ def main():
         if world > 1:
             tp_barrier(engine)
         elapsed = time.perf_counter() - t0
+        if prof is not None:
+            prof.disable()
+            prof.dump_stats(f"{os.environ['LK_PROFILE_TIMED']}.rank{rank}")
         trace, engine.step_trace = engine.step_trace, None
         if load is not None:
             load_host = {k: v - load_host0[k] for k, v in load.host_s.items()}

@@ -443,9 +443,90 @@ void repeat_penalty_(at::Tensor& logits, const at::Tensor& window, const at::Ten
   CHECK_RC(rc, "repeat_penalty");
 }
 
+// One-shot xGMI all-reduce state of one rank (K14): its IPC-exported staging + signal buffers
+// and the peers' buffers opened in this process.  Python exchanges handles() over the TP
+// control group, then calls open(); all_reduce() is hipGraph-capturable.
+struct XgmiAr {
+  int rank = 0, world = 1;
+  size_t bytes = 0;
+  void* data = nullptr;
+  void* sig = nullptr;
+  int* err = nullptr;
+  std::vector<void*> pdata, psig;  // per rank, as mapped here
+  std::vector<void*> opened;       // IPC mappings to close
+
+  XgmiAr(int rank_, int world_, int64_t bytes_) : rank(rank_), world(world_), bytes((size_t)bytes_) {
+    TORCH_CHECK(world >= 1 && world <= lk_xgmi_ar_max_ranks() && rank >= 0 && rank < world, "xgmi_ar: rank/world");
+    TORCH_CHECK(bytes_ > 0 && bytes_ % 16 == 0, "xgmi_ar: staging bytes must be a positive multiple of 16");
+    const size_t sig_bytes = (size_t)lk_xgmi_ar_sig_words() * sizeof(unsigned);
+    TORCH_CHECK(hipMalloc(&data, bytes) == hipSuccess, "xgmi_ar: hipMalloc staging");
+    TORCH_CHECK(hipExtMallocWithFlags(&sig, sig_bytes, hipDeviceMallocUncached) == hipSuccess, "xgmi_ar: signal alloc");
+    TORCH_CHECK(hipMalloc(reinterpret_cast<void**>(&err), sizeof(int)) == hipSuccess, "xgmi_ar: hipMalloc err");
+    TORCH_CHECK(hipMemset(sig, 0, sig_bytes) == hipSuccess && hipMemset(err, 0, sizeof(int)) == hipSuccess &&
+                hipDeviceSynchronize() == hipSuccess, "xgmi_ar: init");
+    pdata.assign(world, nullptr);
+    psig.assign(world, nullptr);
+    pdata[rank] = data;
+    psig[rank] = sig;
+  }
+  ~XgmiAr() {
+    for (void* p : opened) (void)hipIpcCloseMemHandle(p);
+    if (data) (void)hipFree(data);
+    if (sig) (void)hipFree(sig);
+    if (err) (void)hipFree(err);
+  }
+  py::bytes handles() const {
+    hipIpcMemHandle_t h[2];
+    TORCH_CHECK(hipIpcGetMemHandle(&h[0], data) == hipSuccess, "xgmi_ar: hipIpcGetMemHandle(staging)");
+    TORCH_CHECK(hipIpcGetMemHandle(&h[1], sig) == hipSuccess, "xgmi_ar: hipIpcGetMemHandle(signal)");
+    return py::bytes(reinterpret_cast<const char*>(h), sizeof(h));
+  }
+  void open(const std::vector<py::bytes>& all) {
+    TORCH_CHECK((int)all.size() == world, "xgmi_ar: one handle blob per rank");
+    for (int r = 0; r < world; ++r) {
+      if (r == rank) continue;
+      std::string s = all[r];
+      TORCH_CHECK(s.size() == 2 * sizeof(hipIpcMemHandle_t), "xgmi_ar: bad handle blob");
+      hipIpcMemHandle_t h[2];
+      memcpy(h, s.data(), sizeof(h));
+      void *d = nullptr, *g = nullptr;
+      TORCH_CHECK(hipIpcOpenMemHandle(&d, h[0], hipIpcMemLazyEnablePeerAccess) == hipSuccess,
+                  "xgmi_ar: hipIpcOpenMemHandle(staging) of rank ", r);
+      TORCH_CHECK(hipIpcOpenMemHandle(&g, h[1], hipIpcMemLazyEnablePeerAccess) == hipSuccess,
+                  "xgmi_ar: hipIpcOpenMemHandle(signal) of rank ", r);
+      opened.push_back(d);
+      opened.push_back(g);
+      pdata[r] = d;
+      psig[r] = g;
+    }
+  }
+  void all_reduce(const at::Tensor& in, at::Tensor& out) {
+    CHECK_CUDA(in); CHECK_BF16(in); CHECK_BF16(out); CHECK_CONTIG(in); CHECK_CONTIG(out);
+    TORCH_CHECK(in.numel() == out.numel(), "xgmi_ar: in/out size");
+    TORCH_CHECK(in.numel() % 8 == 0 && (size_t)in.numel() * 2 <= bytes, "xgmi_ar: numel must be a multiple of 8 and fit the staging buffer");
+    for (int r = 0; r < world; ++r) TORCH_CHECK(pdata[r] && psig[r], "xgmi_ar: open() not called");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(in.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "xgmi_ar: 16-B alignment");
+    int rc = lk_xgmi_allreduce(reinterpret_cast<bf16_t* const*>(pdata.data()), reinterpret_cast<unsigned* const*>(psig.data()),
+                               rank, world, bp(in), bp(out), in.numel(), err, cur_stream());
+    CHECK_RC(rc, "xgmi_allreduce");
+  }
+  int error() const {
+    int h = 0;
+    TORCH_CHECK(hipMemcpy(&h, err, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess, "xgmi_ar: read error word");
+    return h;
+  }
+};
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  py::class_<XgmiAr>(m, "XgmiAr")
+      .def(py::init<int, int, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("bytes"))
+      .def("handles", &XgmiAr::handles)
+      .def("open", &XgmiAr::open)
+      .def("all_reduce", &XgmiAr::all_reduce)
+      .def("error", &XgmiAr::error)
+      .def_readonly("bytes", &XgmiAr::bytes);
   m.doc() = "gfx950 (MI355X) HIP kernel library";
   m.def("rmsnorm", &rmsnorm, "", py::arg("x"), py::arg("w"), py::arg("eps"), py::arg("residual") = py::none(), py::arg("out") = py::none());
   m.def("layernorm", &layernorm, "", py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"), py::arg("residual") = py::none(), py::arg("write_residual") = false);

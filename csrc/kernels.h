@@ -34,6 +34,12 @@ int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, i
 int lk_ws_scores_f32(const bf16_t* x, long ldx, const bf16_t* w, int M, long N, int K, float* out, long ldo,
                      hipStream_t st);
 
+// xgmi_allreduce.hip (one-shot all-reduce over IPC-mapped peer buffers, K14)
+int lk_xgmi_ar_sig_words();
+int lk_xgmi_ar_max_ranks();
+int lk_xgmi_allreduce(bf16_t* const* data, unsigned* const* sig, int rank, int world, const bf16_t* in,
+                      bf16_t* out, long n, int* err, hipStream_t st);
+
 // big_gemm.hip (prefill-regime linear, 256x256 MFMA tiles, optional fused SwiGLU)
 int lk_big_gemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int swiglu, bf16_t* out,
                 long ldo, int variant, hipStream_t st);

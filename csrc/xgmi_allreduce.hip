@@ -1,0 +1,137 @@
+// K14: one-shot all-reduce over xGMI peer memory (HIP IPC), for the latency-bound
+// tensor-parallel decode all-reduces (B x hidden bf16, ~16 KiB per token row).
+//
+// RCCL's ring is per-link bound and pays several protocol hops per call; at decode
+// sizes (<= a few MB) one pass that reads every peer's buffer directly over its own
+// xGMI link (7 links per MI355X, full mesh) is latency-optimal:
+//   1. every rank copies its input slice into its own IPC-exported staging buffer;
+//   2. barrier-in: each workgroup publishes its slice (system-scope release, then a
+//      relaxed system-scope flag store into EVERY peer's signal buffer) and polls its
+//      own signal buffer until every peer's matching workgroup has published;
+//   3. system-scope acquire, then each workgroup sums its slice over all ranks' staging
+//      buffers (f32 accumulation in rank order -> bitwise identical on every rank) and
+//      writes the bf16 result (in place is fine: a slice is read before it is written);
+//   4. barrier-out: the same handshake on a second flag set, so no rank overwrites its
+//      staging buffer (next call) while a peer may still be reading it.
+// Flags are per-workgroup monotonic epochs kept in device memory (one counter per
+// workgroup, advanced by the kernel itself), so a captured hipGraph replays correctly
+// with no host-side state.  Every spin is bounded: a peer that never arrives sets the
+// error word and the kernel exits instead of hanging the device.
+#include <algorithm>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int kMaxRanks = 8;
+constexpr int kArBlocks = 32;    // workgroups per call (slices)
+constexpr int kArThreads = 512;
+// signal buffer (uncached): [2 phases][kArBlocks][kMaxRanks] flags + [kArBlocks] epoch counters
+constexpr int kSigWords = 2 * kArBlocks * kMaxRanks + kArBlocks;
+constexpr unsigned kSpinLimit = 1u << 22;  // ~4 s of polling: a decode all-reduce waits us, not s
+
+struct ArPeers {
+  bf16_t* data[kMaxRanks];
+  unsigned* sig[kMaxRanks];
+};
+
+LK_DEVICE unsigned ld_sys(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+LK_DEVICE void st_sys(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// lane t < world: signal peer t's slot [phase][blk][rank], then wait for our own slot
+// [phase][blk][t] to reach this call's epoch; false on timeout (error word set)
+LK_DEVICE bool handshake(const ArPeers& p, int rank, int world, int phase, unsigned epoch, int* err) {
+  const int t = threadIdx.x;
+  int ok = 1;
+  if (t < world) {
+    st_sys(p.sig[t] + (phase * kArBlocks + blockIdx.x) * kMaxRanks + rank, epoch);
+    const unsigned* mine = p.sig[rank] + (phase * kArBlocks + blockIdx.x) * kMaxRanks + t;
+    unsigned spins = 0;
+    while ((int)(ld_sys(mine) - epoch) < 0) {
+      if (++spins > kSpinLimit) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  return __syncthreads_and(ok) != 0;
+}
+
+__global__ __launch_bounds__(kArThreads) void xgmi_allreduce_kernel(ArPeers p, int rank, int world,
+                                                                    const bf16_t* __restrict__ in,
+                                                                    bf16_t* __restrict__ out, long n, int* err) {
+  const long nv = n >> 3;  // 16-B vectors
+  const long per = (nv + gridDim.x - 1) / gridDim.x;
+  const long v0 = (long)blockIdx.x * per, v1 = min(nv, v0 + per);
+  unsigned* ctr = p.sig[rank] + 2 * kArBlocks * kMaxRanks + blockIdx.x;
+  __shared__ unsigned s_epoch;
+  if (threadIdx.x == 0) {
+    s_epoch = *ctr + 1;  // only this workgroup of this rank touches its counter
+    *ctr = s_epoch;
+  }
+  __syncthreads();
+  const unsigned epoch = s_epoch;
+
+  // 1. stage this slice
+  bf16_t* mine = p.data[rank];
+  for (long v = v0 + threadIdx.x; v < v1; v += kArThreads)
+    *reinterpret_cast<short8*>(mine + v * 8) = *reinterpret_cast<const short8*>(in + v * 8);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: staged bytes reach memory
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // 2. barrier-in
+  if (!handshake(p, rank, world, 0, epoch, err)) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // 3. reduce the slice over all ranks, same order everywhere
+  for (long v = v0 + threadIdx.x; v < v1; v += kArThreads) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < world; ++r) {
+      float x[8];
+      load8(p.data[r] + v * 8, x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += x[j];
+    }
+    store8(out + v * 8, acc);
+  }
+  __syncthreads();
+  // 4. barrier-out: every peer finished reading our staging buffer
+  handshake(p, rank, world, 1, epoch, err);
+}
+
+}  // namespace
+
+int lk_xgmi_ar_sig_words() { return kSigWords; }
+int lk_xgmi_ar_max_ranks() { return kMaxRanks; }
+
+// data[r] / sig[r]: rank r's staging and signal buffers as mapped in THIS process (own ones
+// included).  n bf16 elements, n % 8 == 0, n * 2 <= staging bytes (checked by the caller).
+int lk_xgmi_allreduce(bf16_t* const* data, unsigned* const* sig, int rank, int world, const bf16_t* in,
+                      bf16_t* out, long n, int* err, hipStream_t st) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || n % 8) return -1;
+  if (n == 0) return 0;
+  ArPeers p{};
+  for (int r = 0; r < world; ++r) {
+    p.data[r] = data[r];
+    p.sig[r] = sig[r];
+  }
+  const long nv = n / 8;
+  const int blocks = (int)std::min<long>(kArBlocks, std::max<long>(1, (nv + kArThreads - 1) / kArThreads));
+  xgmi_allreduce_kernel<<<blocks, kArThreads, 0, st>>>(p, rank, world, in, out, n, err);
+  LK_CHECK_LAUNCH();
+  return 0;
+}

@@ -31,6 +31,8 @@ class TPGroup:
     # ranks by new_tp_groups (torch requires every rank to join every new_group call)
     ctrl: Optional[object] = None
     ranks: Optional[list] = None
+    # optional one-shot xGMI all-reduce (parallel.xgmi_ar, K14) for messages that fit it
+    xgmi: Optional[object] = None
 
     @property
     def enabled(self) -> bool:
@@ -38,6 +40,8 @@ class TPGroup:
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
+            if self.xgmi is not None and self.xgmi.eligible(t):
+                return self.xgmi.all_reduce_(t)
             dist.all_reduce(t, group=self.group)
         return t
 
@@ -133,4 +137,8 @@ def new_tp_groups(tp_size: int, with_ctrl: bool = True) -> TPGroup:
         ctrl = dist.new_group(ranks, backend="gloo") if with_ctrl and tp_size > 1 else None
         if rank in ranks:
             mine = TPGroup(ranks.index(rank), tp_size, grp, ctrl, ranks)
+    if mine is not None and tp_size > 1 and os.environ.get("LK_XGMI_AR") == "1" and torch.cuda.is_available():
+        from .xgmi_ar import attach  # one-shot xGMI all-reduce for decode-sized messages (K14)
+
+        attach(mine)
     return mine
