@@ -8,6 +8,7 @@ one HTTP round-trip per chunk (``RagIndex.cs:47``).
 """
 from __future__ import annotations
 
+import itertools
 import threading
 import time
 from typing import Optional
@@ -36,34 +37,61 @@ class EmbeddingEngine:
     def tokenize(self, texts: list[str]) -> list[list[int]]:
         ids = self.tok.encode_for_embedding(texts, self.max_len)
         V = self.model.cfg.vocab_size
-        return [[t if t < V else t % V for t in s] for s in ids]
+        return [[t % V for t in s] for s in ids]
+
+    def _flat(self, seqs) -> tuple[np.ndarray, np.ndarray]:
+        """(flat int32 ids folded into the encoder vocabulary, lengths) -- C-level loops."""
+        lens = np.fromiter(map(len, seqs), dtype=np.int64, count=len(seqs))
+        flat = np.fromiter(itertools.chain.from_iterable(seqs), dtype=np.int64, count=int(lens.sum()))
+        V = self.model.cfg.vocab_size
+        if flat.size and flat.max() >= V:
+            np.remainder(flat, V, out=flat)
+        return flat.astype(np.int32), lens
+
+    @torch.inference_mode()
+    def _run(self, flat: np.ndarray, lens: np.ndarray, out: torch.Tensor, row0: int):
+        """Embed packed sequences into out[row0:]: token-budgeted varlen micro-batches,
+        launched asynchronously (the caller tokenises the next texts meanwhile)."""
+        d = self.device
+        starts = np.zeros(len(lens) + 1, dtype=np.int64)
+        starts[1:] = np.cumsum(lens)
+        i = 0
+        while i < len(lens):
+            j = i + 1
+            while j < len(lens) and starts[j + 1] - starts[i] <= self.budget:
+                j += 1
+            a, b = int(starts[i]), int(starts[j])
+            ln = lens[i:j]
+            pos = (np.arange(b - a, dtype=np.int64) - np.repeat(starts[i:j] - a, ln)).astype(np.int32)
+            cu = (starts[i:j + 1] - a).astype(np.int32)
+            emb = self.model(torch.from_numpy(flat[a:b]).to(d, non_blocking=True),
+                             torch.from_numpy(cu).to(d, non_blocking=True),
+                             torch.from_numpy(pos).to(d, non_blocking=True), ln.tolist())
+            out[row0 + i:row0 + j] = emb
+            i = j
 
     @torch.inference_mode()
     def embed_ids(self, seqs: list[list[int]]) -> torch.Tensor:
         out = torch.empty((len(seqs), self.dim), dtype=torch.float32, device=self.device)
-        i = 0
-        while i < len(seqs):
-            j, tot = i, 0
-            while j < len(seqs) and (tot + len(seqs[j]) <= self.budget or j == i):
-                tot += len(seqs[j])
-                j += 1
-            chunk = seqs[i:j]
-            lens = [len(s) for s in chunk]
-            flat = np.fromiter((t for s in chunk for t in s), dtype=np.int32, count=tot)
-            pos = np.concatenate([np.arange(n, dtype=np.int32) for n in lens])
-            cu = np.zeros(len(chunk) + 1, dtype=np.int32)
-            cu[1:] = np.cumsum(lens)
-            d = self.device
-            emb = self.model(torch.from_numpy(flat).to(d, non_blocking=True),
-                             torch.from_numpy(cu).to(d, non_blocking=True),
-                             torch.from_numpy(pos).to(d, non_blocking=True), lens)
-            out[i:j] = emb
-            i = j
+        if seqs:
+            flat, lens = self._flat(seqs)
+            self._run(flat, lens, out, 0)
+        return out
+
+    @torch.inference_mode()
+    def _embed_texts(self, texts: list[str], group: int = 4096) -> torch.Tensor:
+        """Tokenise group by group: group g+1 is tokenised on the CPU (native encoder,
+        GIL released) while the device runs group g's encoder batches."""
+        out = torch.empty((len(texts), self.dim), dtype=torch.float32, device=self.device)
+        for g0 in range(0, len(texts), group):
+            ids = self.tok.encode_for_embedding(texts[g0:g0 + group], self.max_len)
+            flat, lens = self._flat(ids)
+            self._run(flat, lens, out, g0)
         return out
 
     def embed(self, texts: list[str]) -> torch.Tensor:
         t0 = time.perf_counter()
         with self.lock:
-            r = self.embed_ids(self.tokenize(texts)) if texts else torch.zeros((0, self.dim))
+            r = self._embed_texts(list(texts)) if texts else torch.zeros((0, self.dim))
         M.EMBED_LAT.observe(time.perf_counter() - t0)
         return r
