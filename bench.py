@@ -32,6 +32,7 @@ is ~20-60 tokens; default 48).
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import os
 import statistics
@@ -344,6 +345,9 @@ def main():
             "gpu_step_busy_frac": round(sum(t[7] for t in trace) / elapsed, 3) if trace and elapsed else None,
             "avg_prefill_tokens_mixed": round(statistics.mean(t[0] for t in mixed), 1) if mixed else 0,
             "avg_decode_rows": round(statistics.mean(t[1] for t in trace), 1) if trace else 0,
+            # mixed steps by total rows (256-row buckets): where the prefill GEMMs run
+            "mixed_rows_hist": {str(k * 256): v for k, v in sorted(collections.Counter(
+                (t[0] + t[1] + 255) // 256 for t in mixed).items())},
         }
         tim = {k: statistics.mean(r.timings.get(k, 0.0) for r in results if r.timings)
                for k in ("embed_s", "knn_s", "prompt_s")} if results else {}
