@@ -69,13 +69,18 @@ class Sampler:
         # memoise their int64 arrays (id -> (list, array); the list reference keeps the id valid)
         self._arr_cache: dict = {}
 
-    def _as_array(self, allowed):
+    def _as_array(self, allowed, V: int):
+        """int64 array of the in-vocabulary ids of ``allowed`` (memoised for the recurring
+        cached lists of a grammar)."""
         if isinstance(allowed, np.ndarray):
-            return allowed.astype(np.int64, copy=False)
+            a = allowed.astype(np.int64, copy=False)
+            return a[(a >= 0) & (a < V)] if len(a) and (a.min() < 0 or a.max() >= V) else a
         hit = self._arr_cache.get(id(allowed))
         if hit is not None and hit[0] is allowed:
             return hit[1]
         a = np.asarray(allowed, dtype=np.int64)
+        if len(a) and (a.min() < 0 or a.max() >= V):
+            a = a[(a >= 0) & (a < V)]
         if len(a) > 64:
             if len(self._arr_cache) > 4096:
                 self._arr_cache.clear()
@@ -98,9 +103,7 @@ class Sampler:
             if p.logits_processor is not None:
                 allowed = p.logits_processor(histories[i])
                 if allowed is not None:
-                    a = self._as_array(allowed)
-                    if len(a) and (a.min() < 0 or a.max() >= V):
-                        a = a[(a >= 0) & (a < V)]
+                    a = self._as_array(allowed, V)
                     flat.append(a + len(crow) * V)
                     crow.append(i)
         if crow:
