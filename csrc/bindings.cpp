@@ -160,6 +160,77 @@ at::Tensor ws_linear(const at::Tensor& x, const at::Tensor& w, bool swiglu, int6
   return out;
 }
 
+// Decode-step fusions (split-K weight-streaming GEMM whose reduction is done by the
+// consumer kernel): the partial slabs never become a bf16 tensor, one launch fewer each.
+namespace {
+struct WsSplit {
+  int M, N, K, BN, S;
+};
+WsSplit ws_split(const at::Tensor& x, const at::Tensor& w, int64_t bn, int64_t splits, const char* name) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_LASTDIM(x); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), name, ": x [M,K], w [N,K]");
+  check_rows16(x, "x"); check_rows16(w, "w");
+  WsSplit p{(int)x.size(0), (int)w.size(0), (int)x.size(1), (int)bn, (int)splits};
+  TORCH_CHECK(p.M >= 1 && p.M <= 256, name, ": M must be in [1, 256]");
+  if (p.BN <= 0 || p.S <= 0) {
+    int pb = 64, ps = 1;
+    lk_wsgemm_plan(p.M, p.N, p.K, 0, &pb, &ps);
+    if (p.BN <= 0) p.BN = pb;
+    if (p.S <= 0) p.S = ps;
+  }
+  TORCH_CHECK(p.S >= 2, name, ": needs a split-K plan (S >= 2)");
+  return p;
+}
+}  // namespace
+
+// out = RMSNorm(x W^T + residual) * norm_w, residual += x W^T (bf16, in place)
+at::Tensor ws_linear_rmsnorm(const at::Tensor& x, const at::Tensor& w, at::Tensor& residual,
+                             const at::Tensor& norm_w, double eps, int64_t bn, int64_t splits) {
+  const WsSplit p = ws_split(x, w, bn, splits, "ws_linear_rmsnorm");
+  CHECK_CUDA(residual); CHECK_BF16(residual); CHECK_LASTDIM(residual); check_rows16(residual, "residual");
+  TORCH_CHECK(residual.dim() == 2 && residual.size(0) == p.M && residual.size(1) == p.N, "residual shape");
+  CHECK_BF16(norm_w); TORCH_CHECK(norm_w.numel() == p.N && norm_w.is_contiguous(), "norm weight shape");
+  at::Tensor part = at::empty({(long)p.S * p.M * p.N}, x.options().dtype(at::kFloat));
+  at::Tensor out = at::empty({p.M, p.N}, x.options());
+  int rc = lk_wsgemm_part(bp(x), x.stride(0), bp(w), p.M, p.N, p.K, p.BN, p.S, part.data_ptr<float>(), cur_stream());
+  CHECK_RC(rc, "ws_linear_rmsnorm (gemm)");
+  rc = lk_splitk_rmsnorm(bp(out), bp(residual), part.data_ptr<float>(), p.S, bp(norm_w), p.M, p.N, (float)eps,
+                         out.stride(0), residual.stride(0), cur_stream());
+  CHECK_RC(rc, "ws_linear_rmsnorm (norm)");
+  return out;
+}
+
+// qkv = x W^T with RoPE applied and K/V scattered into the paged cache (as rope_kv_)
+at::Tensor ws_linear_rope_kv(const at::Tensor& x, const at::Tensor& w, const at::Tensor& positions,
+                             const at::Tensor& cos_sin, int64_t Hq, int64_t Hkv, int64_t D,
+                             const c10::optional<at::Tensor>& k_cache, const c10::optional<at::Tensor>& v_cache,
+                             const c10::optional<at::Tensor>& slots, bool neox, bool write_k_inplace, int64_t bn,
+                             int64_t splits) {
+  const WsSplit p = ws_split(x, w, bn, splits, "ws_linear_rope_kv");
+  TORCH_CHECK(p.N == (Hq + 2 * Hkv) * D, "w must be the fused [(Hq + 2 Hkv) * D, K] projection");
+  CHECK_I32(positions); CHECK_F32(cos_sin); CHECK_CONTIG(cos_sin); CHECK_CONTIG(positions);
+  TORCH_CHECK(positions.numel() == p.M, "positions");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D, "cos_sin must be [max_pos, D]");
+  int BS = 1;
+  if (k_cache || v_cache) {
+    TORCH_CHECK(k_cache && v_cache && slots, "k_cache, v_cache and slots go together");
+    CHECK_BF16(*k_cache); CHECK_BF16(*v_cache); CHECK_CONTIG(*k_cache); CHECK_CONTIG(*v_cache);
+    CHECK_I32(*slots); TORCH_CHECK(slots->numel() == p.M, "slots");
+    TORCH_CHECK(k_cache->dim() == 4 && k_cache->size(1) == Hkv && k_cache->size(3) == D, "k_cache must be [NB, Hkv, BS, D]");
+    TORCH_CHECK(v_cache->sizes() == k_cache->sizes(), "v_cache shape");
+    BS = k_cache->size(2);
+  }
+  at::Tensor part = at::empty({(long)p.S * p.M * p.N}, x.options().dtype(at::kFloat));
+  at::Tensor qkv = at::empty({p.M, p.N}, x.options());
+  int rc = lk_wsgemm_part(bp(x), x.stride(0), bp(w), p.M, p.N, p.K, p.BN, p.S, part.data_ptr<float>(), cur_stream());
+  CHECK_RC(rc, "ws_linear_rope_kv (gemm)");
+  rc = lk_splitk_rope_kv(part.data_ptr<float>(), p.S, bp(qkv), qkv.stride(0), ip(positions), cos_sin.data_ptr<float>(),
+                         p.M, (int)Hq, (int)Hkv, (int)D, bpo(k_cache), bpo(v_cache), ipo(slots), BS, neox ? 1 : 0,
+                         write_k_inplace ? 1 : 0, cur_stream());
+  CHECK_RC(rc, "ws_linear_rope_kv (rope)");
+  return qkv;
+}
+
 // Prefill-regime linear (csrc/big_gemm.hip): x [M, K] . w[N, K]^T -> [M, N], or the fused
 // SwiGLU [M, N/2] for w = [Wg; Wu]
 at::Tensor big_linear(const at::Tensor& x, const at::Tensor& w, bool swiglu, const c10::optional<at::Tensor>& out_,
@@ -542,6 +613,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("silu_mul", &silu_mul, "", py::arg("x"), py::arg("out") = py::none());
   m.def("activation_", &activation_);
   m.def("rope_kv_", &rope_kv_);
+  m.def("ws_linear_rmsnorm", &ws_linear_rmsnorm, "", py::arg("x"), py::arg("w"), py::arg("residual"),
+        py::arg("norm_w"), py::arg("eps"), py::arg("bn") = 0, py::arg("splits") = 0);
+  m.def("ws_linear_rope_kv", &ws_linear_rope_kv, "", py::arg("x"), py::arg("w"), py::arg("positions"),
+        py::arg("cos_sin"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("k_cache"), py::arg("v_cache"),
+        py::arg("slots"), py::arg("neox") = true, py::arg("write_k_inplace") = false, py::arg("bn") = 0,
+        py::arg("splits") = 0);
   m.def("kv_write", &kv_write);
   m.def("decode_splits", &decode_splits);
   m.def("decode_split_size", &decode_split_size);

@@ -10,6 +10,8 @@ typedef unsigned short bf16_t;
 // norm.hip
 int lk_rmsnorm(bf16_t* out, bf16_t* residual, const bf16_t* x, const bf16_t* w, long rows, int H,
                float eps, long xs, long os, long rs, hipStream_t st);
+int lk_splitk_rmsnorm(bf16_t* out, bf16_t* residual, const float* part, int S, const bf16_t* w, long rows, int H,
+                      float eps, long os, long rs, hipStream_t st);
 int lk_layernorm(bf16_t* out, const bf16_t* x, const bf16_t* res, bf16_t* res_out, const bf16_t* w,
                  const bf16_t* b, long rows, int H, float eps, long xs, long os, long rs,
                  hipStream_t st);
@@ -31,6 +33,11 @@ void lk_wsgemm_plan(int M, int N, int K, int swiglu, int* bn_out, int* s_out);
 int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, int swiglu,
               bf16_t* out, long ldo, float* part, hipStream_t st);
 
+// GEMM part only (S >= 2): f32 partial slabs part[S][M][N], for a consumer that fuses the
+// split-K reduction (lk_splitk_rmsnorm, lk_splitk_rope_kv)
+int lk_wsgemm_part(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, float* part,
+                   hipStream_t st);
+
 int lk_ws_scores_f32(const bf16_t* x, long ldx, const bf16_t* w, int M, long N, int K, float* out, long ldo,
                      hipStream_t st);
 
@@ -48,6 +55,11 @@ int lk_big_gemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K,
 int lk_rope_kv(bf16_t* qkv, long qs, const int* positions, const float* cos_sin, long T, int Hq,
                int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,
                int write_k_inplace, hipStream_t st);
+// RoPE + paged-KV write fused with the split-K reduction of the QKV projection:
+// part[S][T][N] f32 -> qkv [T, N] bf16 (q rotated, k as lk_rope_kv leaves it, v) + caches
+int lk_splitk_rope_kv(const float* part, int S, bf16_t* qkv, long qs, const int* positions, const float* cos_sin,
+                      long T, int Hq, int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,
+                      int write_k_inplace, hipStream_t st);
 int lk_kv_write(const bf16_t* k, long ks, const bf16_t* v, long vs, bf16_t* kc, bf16_t* vc,
                 const int* slots, long T, int Hkv, int D, int BS, hipStream_t st);
 

@@ -10,10 +10,16 @@
 
 namespace {
 
-template <int MAXV, int NW>
+// PART: x is not a bf16 tensor but the S f32 split-K partial slabs of the producing
+// weight-streaming GEMM (part[s][row][H], slab = rows * H floats apart): they are summed
+// in slab order and rounded to bf16 -- exactly the values splitk_reduce_kernel would have
+// stored -- so "GEMM partials -> reduce -> add + norm" becomes one launch with
+// bit-identical results (the decode step's o / down projections).
+template <int MAXV, int NW, bool PART>
 __global__ __launch_bounds__(NW * 64) void rmsnorm_kernel(
     bf16_t* __restrict__ out, bf16_t* __restrict__ residual, const bf16_t* __restrict__ x,
-    const bf16_t* __restrict__ w, int H, float eps, long xs, long os, long rs) {
+    const bf16_t* __restrict__ w, int H, float eps, long xs, long os, long rs,
+    const float* __restrict__ part, int S, long slab) {
   __shared__ float red[NW];
   const long row = blockIdx.x;
   const int nvec = H >> 3;
@@ -24,7 +30,22 @@ __global__ __launch_bounds__(NW * 64) void rmsnorm_kernel(
   for (int i = 0; i < MAXV; ++i) {
     const int c = threadIdx.x + i * NW * 64;
     if (c < nvec) {
-      load8(xr + c * 8, v[i]);
+      if constexpr (PART) {
+        const float* pp = part + row * H + c * 8;
+        floatx4 a = *reinterpret_cast<const floatx4*>(pp);
+        floatx4 b = *reinterpret_cast<const floatx4*>(pp + 4);
+        for (int s = 1; s < S; ++s) {
+          a += *reinterpret_cast<const floatx4*>(pp + s * slab);
+          b += *reinterpret_cast<const floatx4*>(pp + s * slab + 4);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[i][j] = bf2f(f2bf(a[j]));
+          v[i][j + 4] = bf2f(f2bf(b[j]));
+        }
+      } else {
+        load8(xr + c * 8, v[i]);
+      }
       if (residual) {
         float r[8];
         bf16_t* rr = residual + row * rs + c * 8;
@@ -202,8 +223,23 @@ RowCfg row_cfg(int H) {
 int lk_rmsnorm(bf16_t* out, bf16_t* residual, const bf16_t* x, const bf16_t* w, long rows, int H,
                float eps, long xs, long os, long rs, hipStream_t st) {
   if (H % 8 || rows <= 0) return rows == 0 ? 0 : -1;
-#define CALL(MV, NW) \
-  rmsnorm_kernel<MV, NW><<<dim3(rows), dim3(NW * 64), 0, st>>>(out, residual, x, w, H, eps, xs, os, rs)
+#define CALL(MV, NW)                                                                                   \
+  rmsnorm_kernel<MV, NW, false><<<dim3(rows), dim3(NW * 64), 0, st>>>(out, residual, x, w, H, eps, xs, os, rs, \
+                                                                     nullptr, 0, 0)
+  ROW_DISPATCH(H, CALL);
+#undef CALL
+  return 0;
+}
+
+// out = RMSNorm(bf16(sum of S partial slabs) + residual) * w, residual updated in place;
+// part: [S][rows][H] f32 (the layout lk_wsgemm_part writes)
+int lk_splitk_rmsnorm(bf16_t* out, bf16_t* residual, const float* part, int S, const bf16_t* w, long rows, int H,
+                      float eps, long os, long rs, hipStream_t st) {
+  if (H % 8 || S < 1 || !residual || rows <= 0) return rows == 0 ? 0 : -1;
+  const long slab = rows * H;
+#define CALL(MV, NW)                                                                               \
+  rmsnorm_kernel<MV, NW, true><<<dim3(rows), dim3(NW * 64), 0, st>>>(out, residual, nullptr, w, H, eps, 0, os, \
+                                                                    rs, part, S, slab)
   ROW_DISPATCH(H, CALL);
 #undef CALL
   return 0;

@@ -14,12 +14,38 @@ namespace {
 // grid (T, ceil(items / 64)), 64 threads: one 16-B rotation item (or V chunk) per
 // thread, so a decode step (T ~ 128 tokens) still puts ~900 single-wave workgroups
 // on the 256 CUs instead of 128 workgroups each looping over 3 dependent items.
-template <bool NEOX>
+//
+// PART: the QKV projection left S f32 split-K partial slabs (part[s][t][ld], slab floats
+// apart) instead of its bf16 output.  Each item sums its 8 columns in slab order and
+// rounds to bf16 (the values splitk_reduce_kernel would have stored), writes the qkv row
+// exactly as "reduce, then rope_kv" leaves it (q rotated, k unrotated unless
+// write_k_inplace, v copied) and scatters K/V into the cache: one launch instead of two.
+template <bool NEOX, bool PART>
 __global__ __launch_bounds__(64) void rope_kv_kernel(
     bf16_t* __restrict__ qkv, long qs, const int* __restrict__ positions,
     const float* __restrict__ cos_sin, int Hq, int Hkv, int D, bf16_t* __restrict__ kc,
-    bf16_t* __restrict__ vc, const int* __restrict__ slots, int BS, int write_k_inplace) {
+    bf16_t* __restrict__ vc, const int* __restrict__ slots, int BS, int write_k_inplace,
+    const float* __restrict__ part, int S, long slab, long ld) {
   const long t = blockIdx.x;
+  // 8 consecutive elements of this token's qkv row at column col, as f32
+  auto ld8 = [&](int col, float* f) {
+    if constexpr (PART) {
+      const float* pp = part + t * ld + col;
+      floatx4 a = *reinterpret_cast<const floatx4*>(pp);
+      floatx4 b = *reinterpret_cast<const floatx4*>(pp + 4);
+      for (int s = 1; s < S; ++s) {
+        a += *reinterpret_cast<const floatx4*>(pp + s * slab);
+        b += *reinterpret_cast<const floatx4*>(pp + s * slab + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f[j] = bf2f(f2bf(a[j]));
+        f[j + 4] = bf2f(f2bf(b[j]));
+      }
+    } else {
+      load8(qkv + t * qs + col, f);
+    }
+  };
   const int it = blockIdx.y * 64 + threadIdx.x;
   const int half = D >> 1;
   const int ipr = NEOX ? (D >> 4) : (D >> 3);  // rotation items per head
@@ -32,8 +58,13 @@ __global__ __launch_bounds__(64) void rope_kv_kernel(
   const long blk = slot >= 0 ? slot / BS : 0;
   const int off = slot >= 0 ? slot % BS : 0;
   if (it >= nrot) {  // V: plain copy into the cache
-    if (vc && slot >= 0) {
-      const int i = it - nrot, h = i / vpr, c = (i - h * vpr) * 8;
+    const int i = it - nrot, h = i / vpr, c = (i - h * vpr) * 8;
+    if constexpr (PART) {
+      float f[8];
+      ld8((Hq + Hkv + h) * D + c, f);
+      store8(row + (long)(Hq + Hkv + h) * D + c, f);
+      if (vc && slot >= 0) store8(vc + ((blk * Hkv + h) * BS + off) * D + c, f);
+    } else if (vc && slot >= 0) {
       *reinterpret_cast<short8*>(vc + ((blk * Hkv + h) * BS + off) * D + c) =
           *reinterpret_cast<const short8*>(row + (long)(Hq + Hkv + h) * D + c);
     }
@@ -50,8 +81,12 @@ __global__ __launch_bounds__(64) void rope_kv_kernel(
   if constexpr (NEOX) {
     const int i0 = v * 8;
     float x1[8], x2[8], y1[8], y2[8];
-    load8(hp + i0, x1);
-    load8(hp + half + i0, x2);
+    ld8(head * D + i0, x1);
+    ld8(head * D + half + i0, x2);
+    if (PART && !store_src) {  // k kept unrotated in the qkv row
+      store8(hp + i0, x1);
+      store8(hp + half + i0, x2);
+    }
     const floatx4 c0 = *reinterpret_cast<const floatx4*>(cs + i0);
     const floatx4 c1 = *reinterpret_cast<const floatx4*>(cs + i0 + 4);
     const floatx4 s0 = *reinterpret_cast<const floatx4*>(cs + half + i0);
@@ -73,7 +108,8 @@ __global__ __launch_bounds__(64) void rope_kv_kernel(
   } else {
     const int e0 = v * 8;  // elements e0..e0+7 = pairs e0/2 .. e0/2+3
     float x[8], y[8];
-    load8(hp + e0, x);
+    ld8(head * D + e0, x);
+    if (PART && !store_src) store8(hp + e0, x);
     const floatx4 c4 = *reinterpret_cast<const floatx4*>(cs + (e0 >> 1));
     const floatx4 s4 = *reinterpret_cast<const floatx4*>(cs + half + (e0 >> 1));
 #pragma unroll
@@ -117,11 +153,29 @@ int lk_rope_kv(bf16_t* qkv, long qs, const int* positions, const float* cos_sin,
   const int items = (Hq + Hkv) * (neox ? D / 16 : D / 8) + Hkv * (D / 8);
   const dim3 grid((unsigned)T, (items + 63) / 64);
   if (neox)
-    rope_kv_kernel<true><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,
-                                              write_k_inplace);
+    rope_kv_kernel<true, false><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,
+                                                     write_k_inplace, nullptr, 0, 0, 0);
   else
-    rope_kv_kernel<false><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,
-                                               write_k_inplace);
+    rope_kv_kernel<false, false><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,
+                                                      write_k_inplace, nullptr, 0, 0, 0);
+  return 0;
+}
+
+int lk_splitk_rope_kv(const float* part, int S, bf16_t* qkv, long qs, const int* positions, const float* cos_sin,
+                      long T, int Hq, int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,
+                      int write_k_inplace, hipStream_t st) {
+  if (D % 16 || T < 0 || S < 1) return -1;
+  if (T == 0) return 0;
+  const long ld = (long)(Hq + 2 * Hkv) * D;  // partial row = the whole projection output
+  const long slab = T * ld;
+  const int items = (Hq + Hkv) * (neox ? D / 16 : D / 8) + Hkv * (D / 8);
+  const dim3 grid((unsigned)T, (items + 63) / 64);
+  if (neox)
+    rope_kv_kernel<true, true><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,
+                                                    write_k_inplace, part, S, slab, ld);
+  else
+    rope_kv_kernel<false, true><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,
+                                                     write_k_inplace, part, S, slab, ld);
   return 0;
 }
 

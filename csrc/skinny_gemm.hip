@@ -505,6 +505,15 @@ int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, i
   return 0;
 }
 
+int lk_wsgemm_part(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, float* part,
+                   hipStream_t st) {
+  if (M < 1 || M > 256 || S < 2 || K % (S * 64) || (BN != 64 && BN != 128) || N % BN || part == nullptr) return -1;
+  const int MT = M <= 64 ? 4 : M <= 128 ? 8 : 16;
+  const int rc = dispatch_ws<false>(MT, BN, x, ldx, w, M, K, K / S, S, N / BN, 0, nullptr, 0, part, N, st);
+  LK_CHECK_LAUNCH();
+  return rc;
+}
+
 // f32 X W^T for a W of any row count (kNN scores: X = queries, W = corpus rows):
 // out[M, N] with row stride ldo; one pass over W, no split-K.
 int lk_ws_scores_f32(const bf16_t* x, long ldx, const bf16_t* w, int M, long N, int K, float* out, long ldo,

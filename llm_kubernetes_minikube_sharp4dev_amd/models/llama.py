@@ -104,19 +104,24 @@ class LlamaModel(nn.Module):
         x = ops.rmsnorm(res, self.layers[0].input_norm, cfg.norm_eps)
         attn_out = None
         n = len(self.layers)
+        fuse = not self.tp.enabled  # row-parallel outputs need their all-reduce before the add
         for li, L in enumerate(self.layers):
-            qkv = ops.linear(x, L.qkv)
             kc, vc = kv_caches[li]
-            ops.rope_kv_(qkv, meta.positions, self.cos_sin, self.hq, self.hkv, self.D, kc, vc,
-                         meta.slots, True, False)
+            qkv = ops.linear_rope_kv(x, L.qkv, meta.positions, self.cos_sin, self.hq, self.hkv, self.D, kc, vc,
+                                     meta.slots, True, False)
             attn_out = paged_attention(qkv, kc, vc, meta, self.hq, self.hkv, self.D, self.scale, attn_out)
+            nxt = self.layers[li + 1].input_norm if li + 1 < n else self.final_norm
+            if fuse:
+                x = ops.linear_add_rmsnorm(attn_out, L.o, res, L.post_norm, cfg.norm_eps)
+                a = ops.linear_swiglu(x, L.gate_up)
+                x = ops.linear_add_rmsnorm(a, L.down, res, nxt, cfg.norm_eps)
+                continue
             o = ops.linear(attn_out, L.o)
             self.tp.all_reduce_(o)
             x = ops.rmsnorm(o, L.post_norm, cfg.norm_eps, residual=res)
             a = ops.linear_swiglu(x, L.gate_up)
             d = ops.linear(a, L.down)
             self.tp.all_reduce_(d)
-            nxt = self.layers[li + 1].input_norm if li + 1 < n else self.final_norm
             x = ops.rmsnorm(d, nxt, cfg.norm_eps, residual=res)
         if meta.logits_idx is not None:
             x = x.index_select(0, meta.logits_idx)

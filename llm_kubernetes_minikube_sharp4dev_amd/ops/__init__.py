@@ -19,7 +19,7 @@ __all__ = [
     "rmsnorm", "layernorm", "embed_layernorm", "silu_mul", "gelu_", "relu_", "rope_kv_",
     "kv_write", "paged_decode", "flash_prefill", "prefill_tiles", "knn_topk", "knn_merge",
     "pool_normalize", "row_norms", "select_tokens", "repeat_penalty_", "linear", "linear_swiglu",
-    "decode_splits", "rope_cos_sin", "tune_big_gemm",
+    "decode_splits", "rope_cos_sin", "tune_big_gemm", "linear_add_rmsnorm", "linear_rope_kv",
 ]
 
 rope_cos_sin = ref.rope_cos_sin
@@ -347,6 +347,46 @@ def linear_swiglu(x, w_gate_up):
     if x.shape[0] > WS_SWIGLU_MAX_M and _use_big(x, w_gate_up, True):
         return lib().big_linear(x, w_gate_up, True, None, BIG_VARIANT)
     return silu_mul(linear(x, w_gate_up))
+
+
+# Decode-step fusions: when the weight-streaming GEMM splits K (S >= 2 partial slabs),
+# the consumer kernel does the split-K reduction itself -- RMSNorm(+residual) after the
+# o / down projections, RoPE + paged-KV write after QKV -- so each of those projections
+# costs one launch fewer (three per layer; bit-identical to the unfused ops).
+DECODE_FUSION = os.environ.get("LK_DECODE_FUSION", "1") != "0"
+_WS_PLANS: dict = {}
+
+
+def _ws_split_plan(x, w):
+    """(BN, S) of the weight-streaming GEMM when it runs split-K for this shape, else None."""
+    if not DECODE_FUSION or _decode_gemm_kind(x, w, False) != "ws":
+        return None
+    key = (x.shape[0], w.shape[0], w.shape[1])
+    plan = _WS_PLANS.get(key)
+    if plan is None:
+        plan = _WS_PLANS[key] = tuple(lib().ws_plan(*key, False))
+    return plan if plan[1] >= 2 else None
+
+
+def linear_add_rmsnorm(x, w, residual, norm_w, eps: float):
+    """RMSNorm(x W^T + residual) * norm_w, with ``residual`` updated in place to
+    x W^T + residual (the pre-norm block's "o / down projection -> add -> norm")."""
+    plan = _ws_split_plan(x, w)
+    if plan is not None and residual.is_contiguous():
+        return lib().ws_linear_rmsnorm(x, w, residual, norm_w, eps, plan[0], plan[1])
+    return rmsnorm(linear(x, w), norm_w, eps, residual=residual)
+
+
+def linear_rope_kv(x, w, positions, cos_sin, Hq: int, Hkv: int, D: int, k_cache=None, v_cache=None,
+                   slots=None, neox: bool = True, write_k_inplace: bool = False):
+    """qkv = x W^T, then :func:`rope_kv_` on it (one launch fewer on split-K decode shapes)."""
+    plan = _ws_split_plan(x, w)
+    if plan is not None:
+        return lib().ws_linear_rope_kv(x, w, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache, slots, neox,
+                                       write_k_inplace, plan[0], plan[1])
+    qkv = linear(x, w)
+    rope_kv_(qkv, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache, slots, neox, write_k_inplace)
+    return qkv
 
 
 def softmax_scale(D: int) -> float:
