@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
                                                         const bf16_t* __restrict__ W, int M, int K, int ks,
                                                         int n_tiles, int swiglu_I, bf16_t* __restrict__ out,
                                                         long ldo, float* __restrict__ part, long part_ld,
-                                                        long n_rows) {
+                                                        long n_rows, int rot_mul) {
   // n_rows: valid W rows (the last column tile may be partial: kNN over a corpus of
   // any size); loads clamp to the last row, stores are masked
   constexpr int ROWS = 16 * MT;          // padded M
@@ -281,6 +281,10 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
   const int r = lane & 15, g = lane >> 4;
   const long kbase = (long)s * ks;
   const int nst = ks / 64;
+  // K-step rotation: column tile t starts its K walk at step (t * rot_mul) % nst, so the
+  // blocks streaming at the same moment read different 128-B columns of X (every block
+  // reads all of X: in lockstep they would all hit the same few L2 channels)
+  const int rot = rot_mul ? (int)(((long)t * rot_mul) % nst) : 0;
 
   auto wrow = [&](int row) -> long {  // tile row -> global W row (output column)
     if constexpr (SWIGLU) {
@@ -306,7 +310,7 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
   }
   auto issue = [&](int st) {
     unsigned char* base = smem + (st % NS) * SB;
-    const int k = st * 64;
+    const int k = (st + rot < nst ? st + rot : st + rot - nst) * 64;
 #pragma unroll
     for (int i = 0; i < LX; ++i)
       __builtin_amdgcn_global_load_lds((gbl_void_ptr)(xsrc[i] + k),
@@ -391,6 +395,11 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
   }
 }
 
+// K-step rotation multiplier: -1 = policy (5 for unsplit-K grids -- the long-K gate_up
+// + SwiGLU and LM-head shapes, 4-8 % faster on MI355X; off for split-K grids, where it
+// measured neutral to 30 % slower: benchmarks/ws_rot_probe.py), >= 0 forces it
+int g_ws_rot_mul = -1;
+
 template <int MT, int BN, bool SWIGLU>
 void launch_ws(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks, int S, int n_tiles, int I,
                bf16_t* out, long ldo, float* part, long part_ld, long n_rows, hipStream_t st) {
@@ -402,7 +411,8 @@ void launch_ws(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks,
                               (int)lds);
     attr = true;
   }
-  kern<<<n_tiles * S, 256, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows);
+  const int rot_mul = g_ws_rot_mul >= 0 ? g_ws_rot_mul : (S == 1 ? 5 : 0);
+  kern<<<n_tiles * S, 256, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows, rot_mul);
 }
 
 template <bool SWIGLU>
@@ -504,6 +514,8 @@ int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, i
   LK_CHECK_LAUNCH();
   return 0;
 }
+
+void lk_wsgemm_set_rot(int rot_mul) { g_ws_rot_mul = rot_mul < 0 ? -1 : rot_mul; }
 
 int lk_wsgemm_part(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, float* part,
                    hipStream_t st) {

@@ -32,6 +32,8 @@ def try_lib():
                 import torch  # noqa: F401  (loads libamdhip64 / libtorch first)
 
                 _mod = importlib.import_module("llm_kubernetes_minikube_sharp4dev_amd._C")
+                if os.environ.get("LK_WS_ROT"):  # weight-streaming GEMM K-step rotation override
+                    _mod.ws_set_rot(int(os.environ["LK_WS_ROT"]))
             except Exception as e:  # pragma: no cover - depends on build state
                 _err = e
     return _mod
