@@ -614,7 +614,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("activation_", &activation_);
   m.def("rope_kv_", &rope_kv_);
   m.def("ws_set_rot", [](int64_t r) { lk_wsgemm_set_rot((int)r); });
-  m.def("ws_set_row_cap", [](int64_t c) { lk_wsgemm_set_row_cap((int)c); });
   m.def("ws_linear_rmsnorm", &ws_linear_rmsnorm, "", py::arg("x"), py::arg("w"), py::arg("residual"),
         py::arg("norm_w"), py::arg("eps"), py::arg("bn") = 0, py::arg("splits") = 0);
   m.def("ws_linear_rope_kv", &ws_linear_rope_kv, "", py::arg("x"), py::arg("w"), py::arg("positions"),

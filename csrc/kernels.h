@@ -38,7 +38,6 @@ int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, i
 int lk_wsgemm_part(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, float* part,
                    hipStream_t st);
 
-void lk_wsgemm_set_row_cap(int cap);  // split M over workgroups of <= cap rows (0 = off)
 void lk_wsgemm_set_rot(int rot_mul);  // K-step rotation per column tile (0 = off, -1 = policy)
 
 int lk_ws_scores_f32(const bf16_t* x, long ldx, const bf16_t* w, int M, long N, int K, float* out, long ldo,

@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
                                                         const bf16_t* __restrict__ W, int M, int K, int ks,
                                                         int n_tiles, int swiglu_I, bf16_t* __restrict__ out,
                                                         long ldo, float* __restrict__ part, long part_ld,
-                                                        long n_rows, int rot_mul, int R) {
+                                                        long n_rows, int rot_mul) {
   // n_rows: valid W rows (the last column tile may be partial: kNN over a corpus of
   // any size); loads clamp to the last row, stores are masked
   constexpr int ROWS = 16 * MT;          // padded M
@@ -276,12 +276,7 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
   constexpr int L = LX + LW;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
-  // R row groups: the M rows are split over R workgroups that stream the same W columns
-  // (rg fastest, so they run at the same time and the second read of W hits the caches)
-  const int rg = blockIdx.x % R, bi = blockIdx.x / R;
-  const int t = bi % n_tiles, s = bi / n_tiles;
-  const int r0 = rg * ROWS;               // first global row of this block
-  const int Mloc = min(ROWS, M - r0);     // >= 1 (host: R = ceil(M / ROWS))
+  const int t = blockIdx.x % n_tiles, s = blockIdx.x / n_tiles;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const long kbase = (long)s * ks;
@@ -306,7 +301,7 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
 #pragma unroll
   for (int i = 0; i < LX; ++i) {
     const int row = (w * LX + i) * 8 + lrow;
-    xsrc[i] = X + (long)(r0 + min(row, Mloc - 1)) * ldx + kbase + ((lch ^ wsz(row)) * 8);
+    xsrc[i] = X + (long)min(row, M - 1) * ldx + kbase + ((lch ^ wsz(row)) * 8);
   }
 #pragma unroll
   for (int i = 0; i < LW; ++i) {
@@ -375,9 +370,8 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
   for (int m = 0; m < MTW; ++m) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int lrow = w * (4 * MT) + 16 * m + 4 * g + i;
-      if (lrow >= Mloc) continue;
-      const int row = r0 + lrow;
+      const int row = w * (4 * MT) + 16 * m + 4 * g + i;
+      if (row >= M) continue;
       if (SWIGLU && !split) {
 #pragma unroll
         for (int n = 0; n < NT / 2; ++n) {
@@ -405,14 +399,6 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
 // + SwiGLU and LM-head shapes, 4-8 % faster on MI355X; off for split-K grids, where it
 // measured neutral to 30 % slower: benchmarks/ws_rot_probe.py), >= 0 forces it
 int g_ws_rot_mul = -1;
-// rows per workgroup cap (0 = all M rows in one workgroup; 64 / 32: split M over
-// ceil(M / cap) workgroups streaming the same W columns)
-int g_ws_row_cap = 0;
-
-int ws_mt(int M) {  // 16-row tiles per workgroup
-  const int rows = g_ws_row_cap > 0 ? std::min(M, g_ws_row_cap) : M;
-  return rows <= 64 ? 4 : rows <= 128 ? 8 : 16;
-}
 
 template <int MT, int BN, bool SWIGLU>
 void launch_ws(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks, int S, int n_tiles, int I,
@@ -426,9 +412,7 @@ void launch_ws(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks,
     attr = true;
   }
   const int rot_mul = g_ws_rot_mul >= 0 ? g_ws_rot_mul : (S == 1 ? 5 : 0);
-  const int R = (M + 16 * MT - 1) / (16 * MT);
-  kern<<<n_tiles * S * R, 256, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows, rot_mul,
-                                          R);
+  kern<<<n_tiles * S, 256, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows, rot_mul);
 }
 
 template <bool SWIGLU>
@@ -511,7 +495,7 @@ int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, i
   if (S > 1 && part == nullptr) return -1;
   const int I = swiglu ? N / 2 : 0;
   const int n_tiles = (swiglu ? I : N) / per;
-  const int MT = ws_mt(M);
+  const int MT = M <= 64 ? 4 : M <= 128 ? 8 : 16;
   const int ks = K / S;
   float* p = S > 1 ? part : nullptr;
   const int rc = swiglu ? dispatch_ws<true>(MT, BN, x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, p, N, st)
@@ -532,12 +516,11 @@ int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, i
 }
 
 void lk_wsgemm_set_rot(int rot_mul) { g_ws_rot_mul = rot_mul < 0 ? -1 : rot_mul; }
-void lk_wsgemm_set_row_cap(int cap) { g_ws_row_cap = (cap == 64 || cap == 128) ? cap : 0; }
 
 int lk_wsgemm_part(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, float* part,
                    hipStream_t st) {
   if (M < 1 || M > 256 || S < 2 || K % (S * 64) || (BN != 64 && BN != 128) || N % BN || part == nullptr) return -1;
-  const int MT = ws_mt(M);
+  const int MT = M <= 64 ? 4 : M <= 128 ? 8 : 16;
   const int rc = dispatch_ws<false>(MT, BN, x, ldx, w, M, K, K / S, S, N / BN, 0, nullptr, 0, part, N, st);
   LK_CHECK_LAUNCH();
   return rc;
