@@ -152,3 +152,29 @@ def test_pipelined_steps_match_synchronous():
     eng = LLMEngine(m, None, block_size=16, max_model_len=512, max_num_seqs=8, eos_ids={eos}, num_blocks=128)
     assert _run_pipelined(eng, prompts, lambda: SamplingParams.greedy(12)) == ref
     assert eng.allocator.usage() == 0.0 or not eng.scheduler.running
+
+
+def test_fused_decode_ops_cpu_fallback():
+    """ops.linear_add_rmsnorm / ops.linear_rope_kv on CPU tensors are the unfused
+    reference ops (the HIP fusions only exist for split-K decode shapes on the GPU)."""
+    from llm_kubernetes_minikube_sharp4dev_amd import ops
+
+    torch.manual_seed(0)
+    x, w = torch.randn(5, 64), torch.randn(32, 64) * 0.1
+    g, res = torch.rand(32) + 0.5, torch.randn(5, 32)
+    r1, r2 = res.clone(), res.clone()
+    y = ops.linear_add_rmsnorm(x, w, r1, g, 1e-5)
+    y2 = ops.rmsnorm(ops.linear(x, w), g, 1e-5, residual=r2)
+    assert torch.equal(y, y2) and torch.equal(r1, r2)
+
+    Hq, Hkv, D, BS, NB = 4, 2, 16, 4, 8
+    wq = torch.randn((Hq + 2 * Hkv) * D, 64) * 0.1
+    pos = torch.arange(5, dtype=torch.int32)
+    cs = ops.rope_cos_sin(64, D, 10000.0)
+    kc, vc = torch.zeros(NB, Hkv, BS, D), torch.zeros(NB, Hkv, BS, D)
+    kc2, vc2 = kc.clone(), vc.clone()
+    slots = torch.tensor([0, 1, 2, 5, 9], dtype=torch.int32)
+    q1 = ops.linear_rope_kv(x, wq, pos, cs, Hq, Hkv, D, kc, vc, slots)
+    q2 = ops.linear(x, wq)
+    ops.rope_kv_(q2, pos, cs, Hq, Hkv, D, kc2, vc2, slots)
+    assert torch.equal(q1, q2) and torch.equal(kc, kc2) and torch.equal(vc, vc2)
