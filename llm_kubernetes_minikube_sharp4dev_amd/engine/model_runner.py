@@ -34,6 +34,52 @@ from ..utils.logging import get_logger
 log = get_logger("engine.runner")
 
 
+class _PinnedStager:
+    """One host->device copy per step: the step's small host arrays (token ids, positions,
+    slots, block tables, ...) are packed into a pinned staging buffer (16-B aligned slots)
+    and land with ONE async copy in a device buffer whose slices become the step's input
+    tensors -- instead of ~10 pageable copies, each a host-staged blit on the GPU queue.
+    A ring of staging buffers, each reused only after the copy that read it has run
+    (event), keeps this safe while the host runs ahead of the device (pipelined steps)."""
+
+    def __init__(self, device, ring: int = 4):
+        self.dev = device
+        self.ring = [[None, None] for _ in range(ring)]  # [pinned uint8 buffer, event]
+        self.k = 0
+
+    @staticmethod
+    def layout(arrays):
+        offs, n = [], 0
+        for a in arrays:
+            n = (n + 15) & ~15
+            offs.append(n)
+            n += a.nbytes
+        return offs, n
+
+    def upload(self, arrays, dst: Optional[torch.Tensor] = None):
+        """arrays: C-contiguous numpy arrays -> device tensors (views of ``dst``, a uint8
+        device buffer large enough for the packed layout, or a fresh one)."""
+        offs, n = self.layout(arrays)
+        self.k = (self.k + 1) % len(self.ring)
+        slot = self.ring[self.k]
+        if slot[1] is not None:
+            slot[1].synchronize()  # the copy that last read this buffer has run
+        if slot[0] is None or slot[0].numel() < n:
+            slot[0] = torch.empty(max(2 * n, 1 << 16), dtype=torch.uint8, pin_memory=True)
+            slot[1] = None
+        host = slot[0].numpy()
+        for a, o in zip(arrays, offs):
+            host[o:o + a.nbytes] = a.reshape(-1).view(np.uint8)
+        if dst is None:
+            dst = torch.empty(max(n, 16), dtype=torch.uint8, device=self.dev)
+        dst[:n].copy_(slot[0][:n], non_blocking=True)
+        if slot[1] is None:
+            slot[1] = torch.cuda.Event()
+        slot[1].record()
+        return [dst[o:o + a.nbytes].view(torch.from_numpy(a[:0].reshape(-1)).dtype).view(a.shape)
+                for a, o in zip(arrays, offs)]
+
+
 class ModelRunner:
     def __init__(self, model, block_size: int = 16, max_model_len: int = 8192, max_num_seqs: int = 256,
                  num_blocks: Optional[int] = None, kv_cache_gb: Optional[float] = None,
@@ -72,6 +118,8 @@ class ModelRunner:
         self.step_hook = None
         self.prev_ids: Optional[torch.Tensor] = None  # previous step's sampled ids (device)
         self.prev_sampled_rows = 0  # rows of prev_ids sampled on the driver only (non-greedy step)
+        self._stager = (_PinnedStager(self.device) if self.device.type == "cuda"
+                        and os.environ.get("LK_PINNED_STAGE", "1") != "0" else None)
         self.gemm_tuning = {}
         if self.device.type == "cuda" and os.environ.get("LK_BIG_GEMM", "1") != "0" and hasattr(model, "gemm_shapes"):
             # pick hipBLASLt vs the big-tile MFMA kernel per prefill-step M bucket (~0.5 s)
@@ -230,42 +278,52 @@ class ModelRunner:
         return si, rows
 
     # ----------------------------------------------------------- execution (device)
+    def _upload(self, named: dict) -> dict:
+        """{name: host array} -> {name: device tensor}: one pinned copy on the GPU, plain
+        tensors on the CPU."""
+        arrays = {k: np.ascontiguousarray(v) for k, v in named.items() if v is not None}
+        if self._stager is None:
+            return {k: torch.from_numpy(v).to(self.device, non_blocking=True) for k, v in arrays.items()}
+        return dict(zip(arrays, self._stager.upload(list(arrays.values()))))
+
     def _meta(self, si: "StepInputs"):
-        dev = self.device
-
-        def t(a, dt=None):
-            return torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)
-
         Tp = int(sum(si.q_lens))
-        meta = AttnMeta(positions=t(si.positions), slots=t(si.slots), num_prefill_tokens=Tp,
-                        num_prefill_seqs=len(si.q_lens), num_decode=si.num_decode)
+        host = {"ids": si.ids, "pos": si.positions, "slots": si.slots}
         if si.q_lens:
             cu = np.zeros(len(si.q_lens) + 1, dtype=np.int32)
             cu[1:] = np.cumsum(si.q_lens)
-            meta.cu_q = t(cu)
-            meta.ctx_lens_p = t(np.asarray(si.ctx_lens, dtype=np.int32))
-            meta.block_tables_p = t(si.tables_p)
+            host.update(cu=cu, ctx_p=np.asarray(si.ctx_lens, dtype=np.int32), bt_p=si.tables_p)
+        if si.num_decode:
+            host.update(bt_d=si.tables_d, ctx_d=si.ctx_d)
+            if si.shared_len:
+                host["shared"] = np.asarray([si.shared_len], dtype=np.int32)
+        if len(si.logits_rows):
+            host["logits"] = si.logits_rows
+        if si.gather is not None:
+            host.update(g_dst=si.gather[0], g_src=si.gather[1])
+        d = self._upload(host)
+        meta = AttnMeta(positions=d["pos"], slots=d["slots"], num_prefill_tokens=Tp,
+                        num_prefill_seqs=len(si.q_lens), num_decode=si.num_decode)
+        if si.q_lens:
+            meta.cu_q, meta.ctx_lens_p, meta.block_tables_p = d["cu"], d["ctx_p"], d["bt_p"]
             meta.q_lens_cpu, meta.ctx_lens_cpu = list(si.q_lens), list(si.ctx_lens)
         if si.num_decode:
-            meta.block_tables_d = t(si.tables_d)
-            meta.ctx_lens_d = t(si.ctx_d)
+            meta.block_tables_d, meta.ctx_lens_d = d["bt_d"], d["ctx_d"]
             meta.decode_split = max(ops.decode_split_size(si.num_decode, self.hkv), self.bs)
             meta.max_splits = ops.decode_splits(si.tables_d.shape[1] * self.bs, meta.decode_split)
             if si.shared_len:
-                self._cascade_meta(meta, si.num_decode, t(np.asarray([si.shared_len], dtype=np.int32)))
-        meta.logits_idx = t(si.logits_rows) if len(si.logits_rows) else None
-        ids = t(si.ids)
-        self._apply_gather(ids, si)
+                self._cascade_meta(meta, si.num_decode, d["shared"])
+        meta.logits_idx = d.get("logits")
+        ids = d["ids"]
+        if si.gather is not None:
+            self._apply_gather(ids, d["g_dst"], d["g_src"])
         return ids, meta
 
-    def _apply_gather(self, ids: torch.Tensor, si: "StepInputs"):
-        """Fill in-flight input tokens from the previous step's device ids (no host sync)."""
-        if si.gather is None:
-            return
+    def _apply_gather(self, ids: torch.Tensor, dst: torch.Tensor, src: torch.Tensor):
+        """Fill in-flight input tokens (rows ``dst``) from the previous step's device ids
+        (rows ``src``): no host sync."""
         if self.prev_ids is None:
             raise RuntimeError("step has in-flight input tokens but no previous step ids")
-        dst = torch.from_numpy(si.gather[0]).to(ids.device, non_blocking=True)
-        src = torch.from_numpy(si.gather[1]).to(ids.device, non_blocking=True)
         ids.index_copy_(0, dst, self.prev_ids.index_select(0, src).to(ids.dtype))
 
     def _cascade_meta(self, meta, B: int, shared_len: torch.Tensor):
@@ -336,19 +394,29 @@ class ModelRunner:
     def _static(self, B):
         dev = self.device
         po, pm = self._decode_ws(B)
+        # the graph's inputs are slices of ONE device buffer, refilled by one pinned copy per
+        # replay: int32 [ids | pos | slots | ctx | block table | shared_len], then room for
+        # the int64 in-flight gather rows (dst, src) of up to B rows
+        nb = self.max_blocks
+        n32 = 4 * B + B * nb + 1
+        _, nbytes = _PinnedStager.layout([np.zeros(n32, np.int32), np.zeros(B, np.int64), np.zeros(B, np.int64)])
+        raw = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+        i32 = raw[: 4 * n32].view(torch.int32)
         st = {
-            "ids": torch.zeros(B, dtype=torch.int32, device=dev),
-            "pos": torch.zeros(B, dtype=torch.int32, device=dev),
-            "slots": torch.full((B,), -1, dtype=torch.int32, device=dev),
-            "bt": torch.zeros((B, self.max_blocks), dtype=torch.int32, device=dev),
-            "ctx": torch.ones(B, dtype=torch.int32, device=dev),
+            "raw": raw,
+            "ids": i32[0:B],
+            "pos": i32[B:2 * B],
+            "slots": i32[2 * B:3 * B].fill_(-1),
+            "ctx": i32[3 * B:4 * B].fill_(1),
+            "bt": i32[4 * B:4 * B + B * nb].view(B, nb),
+            "shared": i32[4 * B + B * nb:],
         }
         split, ms = self.decode_split(B)
         st["meta"] = AttnMeta(positions=st["pos"], slots=st["slots"], num_decode=B,
                               block_tables_d=st["bt"], ctx_lens_d=st["ctx"], max_splits=ms,
                               decode_split=split, part_o=po, part_ml=pm)
         if self.cascade and B >= 2:
-            st["shared_len"] = torch.zeros(1, dtype=torch.int32, device=dev)
+            st["shared_len"] = st["shared"]
             self._cascade_meta(st["meta"], B, st["shared_len"])
         return st
 
@@ -385,14 +453,21 @@ class ModelRunner:
     def _graph_execute(self, si):
         Bg = si.decode_graph
         st = self.graphs.get((Bg, si.greedy)) or self.capture(Bg, si.greedy)
-        st["ids"].copy_(torch.from_numpy(si.ids), non_blocking=True)
-        self._apply_gather(st["ids"], si)
-        st["pos"].copy_(torch.from_numpy(si.positions), non_blocking=True)
-        st["slots"].copy_(torch.from_numpy(si.slots), non_blocking=True)
-        st["ctx"].copy_(torch.from_numpy(si.ctx_d), non_blocking=True)
-        st["bt"].copy_(torch.from_numpy(si.tables_d), non_blocking=True)
-        if "shared_len" in st:
-            st["shared_len"].copy_(torch.from_numpy(np.asarray([si.shared_len], dtype=np.int32)), non_blocking=True)
+        static = np.concatenate([si.ids, si.positions, si.slots, si.ctx_d, si.tables_d.reshape(-1),
+                                 np.asarray([si.shared_len], dtype=np.int32)]).astype(np.int32, copy=False)
+        if static.size != 4 * Bg + st["bt"].numel() + 1:
+            raise ValueError("decode graph inputs do not match the captured bucket's layout")
+        arrays = [static]
+        if si.gather is not None:
+            arrays += [si.gather[0], si.gather[1]]
+        if self._stager is not None:
+            views = self._stager.upload(arrays, dst=st["raw"])
+        else:  # pageable copies (LK_PINNED_STAGE=0)
+            n32 = static.size
+            st["raw"][: 4 * n32].view(torch.int32).copy_(torch.from_numpy(static), non_blocking=True)
+            views = [None] + [torch.from_numpy(a).to(self.device, non_blocking=True) for a in arrays[1:]]
+        if si.gather is not None:
+            self._apply_gather(st["ids"], views[1], views[2])
         st["graph"].replay()
         return st["logits"][: si.num_decode]
 
