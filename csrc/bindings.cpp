@@ -505,6 +505,25 @@ at::Tensor select_tokens(const at::Tensor& logits, const c10::optional<at::Tenso
   return out;
 }
 
+// token selection restricted per row to an allowed id list (grammar-constrained decoding)
+at::Tensor select_allowed(const at::Tensor& logits, const at::Tensor& plan, const c10::optional<at::Tensor>& temps,
+                          int64_t seed, int64_t step) {
+  CHECK_CUDA(logits); CHECK_LASTDIM(logits); CHECK_CUDA(plan); CHECK_I32(plan); CHECK_CONTIG(plan);
+  TORCH_CHECK(logits.dim() == 2, "logits [B, V]");
+  const bool is_bf16 = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(is_bf16 || logits.scalar_type() == at::kFloat, "logits must be bf16 or f32");
+  TORCH_CHECK(logits.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(logits.data_ptr()) % 32 == 0, "logits rows must be 32-byte aligned");
+  const int B = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(plan.numel() >= 2 * B + 1, "plan must hold [B flags | B+1 offsets | ids]");
+  if (temps) { CHECK_F32(*temps); TORCH_CHECK(temps->numel() >= B, "temps"); }
+  at::Tensor out = at::empty({B}, logits.options().dtype(at::kInt));
+  int rc = lk_select_allowed(logits.data_ptr(), is_bf16 ? 1 : 0, logits.stride(0), B, V,
+                             temps ? temps->data_ptr<float>() : nullptr, (unsigned long long)seed, (int)step,
+                             plan.data_ptr<int>(), out.data_ptr<int>(), cur_stream());
+  CHECK_RC(rc, "select_allowed");
+  return out;
+}
+
 void repeat_penalty_(at::Tensor& logits, const at::Tensor& window, const at::Tensor& penalty) {
   CHECK_CUDA(logits); CHECK_I32(window); CHECK_F32(penalty); CHECK_CONTIG(window);
   const bool is_bf16 = logits.scalar_type() == at::kBFloat16;
@@ -631,6 +650,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("knn_merge", &knn_merge);
   m.def("pool_normalize", &pool_normalize);
   m.def("row_norms", &row_norms);
+  m.def("select_allowed", &select_allowed, "", py::arg("logits"), py::arg("plan"), py::arg("temps") = py::none(),
+        py::arg("seed") = 0, py::arg("step") = 0);
   m.def("select_tokens", &select_tokens, "", py::arg("logits"), py::arg("temps") = py::none(), py::arg("seed") = 0, py::arg("step") = 0, py::arg("out") = py::none());
   m.def("repeat_penalty_", &repeat_penalty_);
 }

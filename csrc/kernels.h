@@ -98,6 +98,9 @@ int lk_pool_normalize(const bf16_t* hidden, long hs, const int* cu, int B, int H
 int lk_row_norms(const bf16_t* x, long N, int D, float* out, hipStream_t st);
 
 // sampling.hip
+// plan: int32 [B flags | B+1 offsets | allowed ids] (ids in [0, V), checked by the caller)
+int lk_select_allowed(const void* logits, int is_bf16, long ls, int B, int V, const float* temps,
+                      unsigned long long seed, int step, const int* plan, int* out, hipStream_t st);
 int lk_select_tokens(const void* logits, int is_bf16, long ls, int B, int V, const float* temps,
                      unsigned long long seed, int step, int* out, hipStream_t st);
 int lk_repeat_penalty(void* logits, int is_bf16, long ls, int B, const int* window, int W,

@@ -21,11 +21,16 @@ LK_DEVICE unsigned hash3(unsigned a, unsigned b, unsigned c) {
   return (unsigned)(x >> 32);
 }
 
-template <bool BF16, bool SAMPLE>
+// ALLOWED: grammar-constrained rows consider only their allowed ids (plan = [B flags |
+// B+1 row offsets | ids]; flags[row] = 0 -> the whole vocabulary).  Same values, same
+// Gumbel noise per (row, step, id) and the same tie order as scanning the row with every
+// other id masked to -inf -- without materialising the [B, V] mask (3 full passes over
+// the logits) or scanning 128k entries per row.
+template <bool BF16, bool SAMPLE, bool ALLOWED = false>
 __global__ __launch_bounds__(256) void select_kernel(const void* __restrict__ logits, long ls, int V,
                                                      const float* __restrict__ temps,
                                                      unsigned long long seed, int step,
-                                                     int* __restrict__ out) {
+                                                     int* __restrict__ out, const int* __restrict__ plan = nullptr) {
   __shared__ float rs[4];
   __shared__ int ri[4];
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -35,6 +40,8 @@ __global__ __launch_bounds__(256) void select_kernel(const void* __restrict__ lo
   float best = -INFINITY;
   int bi = 0x7fffffff;
   const int nv = V / 8;
+  const int B = gridDim.x;
+  const bool sparse = ALLOWED && plan[row] != 0;
   auto consider = [&](float x, int idx) {
     if (!greedy) {
       const unsigned hsh = hash3((unsigned)(seed ^ (seed >> 32)) + row, (unsigned)step, (unsigned)idx);
@@ -46,7 +53,15 @@ __global__ __launch_bounds__(256) void select_kernel(const void* __restrict__ lo
       bi = idx;
     }
   };
-  if constexpr (BF16) {
+  if (sparse) {
+    const int* ids = plan + 2 * B + 1;
+    const int a0 = plan[B + row], a1 = plan[B + row + 1];
+    for (int j = a0 + tid; j < a1; j += 256) {
+      const int id = ids[j];
+      if constexpr (BF16) consider(bf2f(reinterpret_cast<const bf16_t*>(logits)[(long)row * ls + id]), id);
+      else consider(reinterpret_cast<const float*>(logits)[(long)row * ls + id], id);
+    }
+  } else if constexpr (BF16) {
     const bf16_t* lp = reinterpret_cast<const bf16_t*>(logits) + (long)row * ls;
     for (int c = tid; c < nv; c += 256) {
       float v[8];
@@ -128,6 +143,20 @@ int lk_select_tokens(const void* logits, int is_bf16, long ls, int B, int V, con
   } else {
     if (temps) select_kernel<false, true><<<B, 256, 0, st>>>(logits, ls, V, temps, seed, step, out);
     else select_kernel<false, false><<<B, 256, 0, st>>>(logits, ls, V, temps, seed, step, out);
+  }
+  return 0;
+}
+
+int lk_select_allowed(const void* logits, int is_bf16, long ls, int B, int V, const float* temps,
+                      unsigned long long seed, int step, const int* plan, int* out, hipStream_t st) {
+  if (B <= 0) return 0;
+  if ((ls % 8 && is_bf16) || !plan) return -1;
+  if (is_bf16) {
+    if (temps) select_kernel<true, true, true><<<B, 256, 0, st>>>(logits, ls, V, temps, seed, step, out, plan);
+    else select_kernel<true, false, true><<<B, 256, 0, st>>>(logits, ls, V, temps, seed, step, out, plan);
+  } else {
+    if (temps) select_kernel<false, true, true><<<B, 256, 0, st>>>(logits, ls, V, temps, seed, step, out, plan);
+    else select_kernel<false, false, true><<<B, 256, 0, st>>>(logits, ls, V, temps, seed, step, out, plan);
   }
   return 0;
 }

@@ -7,6 +7,7 @@ penalty (Ollama default 1.1 over the last 64 tokens) is a HIP kernel on the logi
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Callable, Optional
 
@@ -60,6 +61,11 @@ class SamplingParams:
         return self.temperature <= 0.0 or self.top_k == 1
 
 
+# grammar-constrained rows select over their allowed ids only (LK_SPARSE_SELECT=0: dense
+# -inf mask over [rows, V] + full-row select, the path CPU tensors and top-k/top-p take)
+SPARSE_SELECT = os.environ.get("LK_SPARSE_SELECT", "1") != "0"
+
+
 class Sampler:
     def __init__(self, vocab_size: int, seed: int = 0):
         self.vocab_size = vocab_size
@@ -87,26 +93,47 @@ class Sampler:
             self._arr_cache[id(allowed)] = (allowed, a)
         return a
 
+    @staticmethod
+    def _plan(rows: dict, B: int, dev) -> torch.Tensor:
+        """Device int32 [B flags | B+1 offsets | allowed ids] of the constrained rows
+        (flag 0 = unconstrained row) for the HIP select_allowed kernel."""
+        order = sorted(rows)
+        flags = np.zeros(B, dtype=np.int32)
+        counts = np.zeros(B + 1, dtype=np.int64)
+        for i in order:
+            flags[i] = 1
+            counts[i + 1] = len(rows[i])
+        offs = np.cumsum(counts)
+        ids = np.concatenate([rows[i] for i in order])
+        plan = np.concatenate([flags, offs.astype(np.int32), ids.astype(np.int32)])
+        return torch.from_numpy(plan).to(dev, non_blocking=True)
+
     def __call__(self, logits: torch.Tensor, params: list, histories: list) -> torch.Tensor:
         """logits [B, V] (f32) -> int32 token ids [B] (on logits.device)."""
         self.step += 1
         B = logits.shape[0]
         dev = logits.device
-        # constrained decoding: mask everything outside the allowed set -- one host->device
-        # copy of the flat (row * V + token) positions and one index_fill for the whole
-        # batch.  (An advanced-index assignment of a Python scalar, mask[r, t] = 0.0,
-        # blocks the host until the device queue drains -- measured 15 ms behind a
-        # queued forward -- which would serialise the engine's step pipelining.)
+        # constrained decoding: on the GPU the select kernel scans only each row's allowed
+        # ids (one host->device copy of the id lists); otherwise everything outside the
+        # allowed set is masked -- one copy of the flat (row * V + token) positions and one
+        # index_fill for the whole batch.  (An advanced-index assignment of a Python
+        # scalar, mask[r, t] = 0.0, blocks the host until the device queue drains --
+        # measured 15 ms behind a queued forward -- serialising the step pipelining.)
         V = logits.shape[1]
-        flat, crow = [], []
+        rows = {}
         for i, p in enumerate(params):
             if p.logits_processor is not None:
                 allowed = p.logits_processor(histories[i])
                 if allowed is not None:
-                    a = self._as_array(allowed, V)
-                    flat.append(a + len(crow) * V)
-                    crow.append(i)
-        if crow:
+                    rows[i] = self._as_array(allowed, V)
+        need_filter = any((not p.is_greedy) and (0 < p.top_k < V or p.top_p < 1.0) for p in params)
+        plan = None
+        if rows and not need_filter and SPARSE_SELECT and ops.use_hip(logits):
+            # selection straight over each row's allowed ids (HIP select_allowed): no mask
+            plan = self._plan(rows, B, dev)
+        elif rows:
+            crow = list(rows)
+            flat = [rows[i] + j * V for j, i in enumerate(crow)]
             idx = torch.from_numpy(np.concatenate(flat)).to(dev, non_blocking=True)
             mask = torch.full((len(crow), V), float("-inf"), device=dev)
             mask.view(-1).index_fill_(0, idx, 0.0)
@@ -125,15 +152,18 @@ class Sampler:
                     pen[i] = p.repeat_penalty
             ops.repeat_penalty_(logits, win.to(dev, non_blocking=True), pen.to(dev, non_blocking=True))
         if all(p.is_greedy for p in params):
+            if plan is not None:
+                return ops.lib().select_allowed(logits, plan)
             return ops.select_tokens(logits)
         temps = torch.tensor([0.0 if p.is_greedy else p.temperature for p in params], dtype=torch.float32)
-        need_filter = any((not p.is_greedy) and (0 < p.top_k < logits.shape[1] or p.top_p < 1.0) for p in params)
         seed = self.seed
         for p in params:
             if p.seed is not None:
                 seed = int(p.seed)
                 break
         if not need_filter:
+            if plan is not None:
+                return ops.lib().select_allowed(logits, plan, temps.to(dev), seed, self.step)
             return ops.select_tokens(logits, temps.to(dev), seed=seed, step=self.step)
         return self._filtered(logits, params, temps.to(dev), seed)
 

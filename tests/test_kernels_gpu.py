@@ -1,6 +1,7 @@
 """Numerics of every HIP kernel vs the plain-PyTorch fp32 reference (ops.reference)."""
 import math
 
+import numpy as np
 import pytest
 import torch
 
@@ -478,3 +479,30 @@ def test_linear_add_rmsnorm_dispatch(hip):
     finally:
         ops.DECODE_FUSION = True
     assert torch.equal(y, y2) and torch.equal(res, res2)
+
+
+@pytest.mark.parametrize("sample", [False, True])
+def test_select_allowed_matches_masked_select(hip, sample):
+    """Grammar-constrained selection over per-row allowed ids equals masking every other id
+    to -inf and scanning the whole row (greedy and Gumbel sampling, ties included)."""
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import Sampler
+
+    torch.manual_seed(11)
+    B, V = 7, 128256
+    logits = torch.randn(B, V, device=DEV)
+    logits[2, 500] = logits[2, 77] = 50.0  # tie: the lower id wins on both paths
+    g = torch.Generator().manual_seed(0)
+    rows = {0: torch.randint(0, V, (3000,), generator=g).numpy(), 2: np.array([77, 500, 9, 128000]),
+            3: np.array([5]), 5: torch.randint(0, V, (40,), generator=g).numpy(), 6: np.array([V - 1, 0])}
+    rows = {i: a.astype(np.int64) for i, a in rows.items()}
+    plan = Sampler._plan(rows, B, torch.device(DEV))
+    masked = logits.clone()
+    for i, a in rows.items():
+        m = torch.full((V,), float("-inf"), device=DEV)
+        m[torch.from_numpy(a).to(DEV)] = 0.0
+        masked[i] += m
+    temps = torch.tensor([0.7, 1.0, 0.0, 1.3, 0.9, 0.5, 2.0], device=DEV) if sample else None
+    a = hip.select_allowed(logits, plan, temps, 1234, 5)
+    b = hip.select_tokens(masked, temps, 1234, 5, None)
+    assert torch.equal(a, b)
+    assert int(a[2]) == 77 or sample
