@@ -115,10 +115,8 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(PrefillParams p) 
   float m_run = -INFINITY, l_run = 0.f;
 
   // ---- staging helpers: chunk c of the tile = (row c / CPR, col chunk c % CPR)
-  // two register staging sets: tile t+2's K/V loads are issued while tile t computes,
-  // so each global load has two tiles of compute to land under
-  short8 kA[CPT], vA[CPT], kB[CPT], vB[CPT];
-  auto gload = [&](int kt, short8 (&kreg)[CPT], short8 (&vreg)[CPT]) {
+  short8 kreg[CPT], vreg[CPT];
+  auto gload = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int c = tid + 256 * i;
@@ -138,7 +136,7 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(PrefillParams p) 
       vreg[i] = *reinterpret_cast<const short8*>(vp);
     }
   };
-  auto swrite = [&](const short8 (&kreg)[CPT], const short8 (&vreg)[CPT]) {
+  auto swrite = [&]() {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int c = tid + 256 * i;
@@ -165,8 +163,13 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(PrefillParams p) 
   }
 
   const int ntiles = (kend + KT - 1) / KT;
-  auto tile = [&](const int t) {
+  if (ntiles > 0) gload(0);
+  for (int t = 0; t < ntiles; ++t) {
     const int kt = t * KT;
+    __syncthreads();  // everyone finished reading the previous tile
+    swrite();
+    __syncthreads();
+    if (t + 1 < ntiles) gload(kt + KT);
 
     // ---- S^T = K . Q^T  for two 32-key halves
     floatx16 s[2];
@@ -255,23 +258,6 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(PrefillParams p) 
           const short8 a = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
           o[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pf[m][s2], o[n], 0, 0, 0);
         }
-    }
-  };
-
-  if (ntiles > 0) gload(0, kA, vA);
-  if (ntiles > 1) gload(KT, kB, vB);
-  for (int t = 0; t < ntiles; t += 2) {
-    __syncthreads();  // everyone finished reading the previous tile
-    swrite(kA, vA);
-    __syncthreads();
-    if (t + 2 < ntiles) gload((t + 2) * KT, kA, vA);
-    tile(t);
-    if (t + 1 < ntiles) {
-      __syncthreads();
-      swrite(kB, vB);
-      __syncthreads();
-      if (t + 3 < ntiles) gload((t + 3) * KT, kB, vB);
-      tile(t + 1);
     }
   }
 
