@@ -10,16 +10,18 @@
 
 namespace {
 
-// PART: x is not a bf16 tensor but the S f32 split-K partial slabs of the producing
+// SP > 0: x is not a bf16 tensor but the SP f32 split-K partial slabs of the producing
 // weight-streaming GEMM (part[s][row][H], slab = rows * H floats apart): they are summed
 // in slab order and rounded to bf16 -- exactly the values splitk_reduce_kernel would have
 // stored -- so "GEMM partials -> reduce -> add + norm" becomes one launch with
 // bit-identical results (the decode step's o / down projections).
-template <int MAXV, int NW, bool PART>
+// (SP is a template constant so all SP x MAXV slab loads of a thread are issued before the
+// first add: a runtime slab loop serialised one L2 round trip per slab)
+template <int MAXV, int NW, int SP>
 __global__ __launch_bounds__(NW * 64) void rmsnorm_kernel(
     bf16_t* __restrict__ out, bf16_t* __restrict__ residual, const bf16_t* __restrict__ x,
     const bf16_t* __restrict__ w, int H, float eps, long xs, long os, long rs,
-    const float* __restrict__ part, int S, long slab) {
+    const float* __restrict__ part, long slab) {
   __shared__ float red[NW];
   const long row = blockIdx.x;
   const int nvec = H >> 3;
@@ -30,13 +32,19 @@ __global__ __launch_bounds__(NW * 64) void rmsnorm_kernel(
   for (int i = 0; i < MAXV; ++i) {
     const int c = threadIdx.x + i * NW * 64;
     if (c < nvec) {
-      if constexpr (PART) {
+      if constexpr (SP > 0) {
         const float* pp = part + row * H + c * 8;
-        floatx4 a = *reinterpret_cast<const floatx4*>(pp);
-        floatx4 b = *reinterpret_cast<const floatx4*>(pp + 4);
-        for (int s = 1; s < S; ++s) {
-          a += *reinterpret_cast<const floatx4*>(pp + s * slab);
-          b += *reinterpret_cast<const floatx4*>(pp + s * slab + 4);
+        floatx4 pa[SP], pb[SP];
+#pragma unroll
+        for (int s = 0; s < SP; ++s) {
+          pa[s] = *reinterpret_cast<const floatx4*>(pp + s * slab);
+          pb[s] = *reinterpret_cast<const floatx4*>(pp + s * slab + 4);
+        }
+        floatx4 a = pa[0], b = pb[0];
+#pragma unroll
+        for (int s = 1; s < SP; ++s) {
+          a += pa[s];
+          b += pb[s];
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -224,8 +232,8 @@ int lk_rmsnorm(bf16_t* out, bf16_t* residual, const bf16_t* x, const bf16_t* w, 
                float eps, long xs, long os, long rs, hipStream_t st) {
   if (H % 8 || rows <= 0) return rows == 0 ? 0 : -1;
 #define CALL(MV, NW)                                                                                   \
-  rmsnorm_kernel<MV, NW, false><<<dim3(rows), dim3(NW * 64), 0, st>>>(out, residual, x, w, H, eps, xs, os, rs, \
-                                                                     nullptr, 0, 0)
+  rmsnorm_kernel<MV, NW, 0><<<dim3(rows), dim3(NW * 64), 0, st>>>(out, residual, x, w, H, eps, xs, os, rs, \
+                                                                 nullptr, 0)
   ROW_DISPATCH(H, CALL);
 #undef CALL
   return 0;
@@ -235,13 +243,22 @@ int lk_rmsnorm(bf16_t* out, bf16_t* residual, const bf16_t* x, const bf16_t* w, 
 // part: [S][rows][H] f32 (the layout lk_wsgemm_part writes)
 int lk_splitk_rmsnorm(bf16_t* out, bf16_t* residual, const float* part, int S, const bf16_t* w, long rows, int H,
                       float eps, long os, long rs, hipStream_t st) {
-  if (H % 8 || S < 1 || !residual || rows <= 0) return rows == 0 ? 0 : -1;
+  if (H % 8 || !residual || rows <= 0) return rows == 0 ? 0 : -1;
   const long slab = rows * H;
-#define CALL(MV, NW)                                                                               \
-  rmsnorm_kernel<MV, NW, true><<<dim3(rows), dim3(NW * 64), 0, st>>>(out, residual, nullptr, w, H, eps, 0, os, \
-                                                                    rs, part, S, slab)
-  ROW_DISPATCH(H, CALL);
-#undef CALL
+#define CALL_SP(MV, NW, SPC)                                                                         \
+  rmsnorm_kernel<MV, NW, SPC><<<dim3(rows), dim3(NW * 64), 0, st>>>(out, residual, nullptr, w, H, eps, 0, os, \
+                                                                   rs, part, slab)
+#define CALL2(MV, NW) CALL_SP(MV, NW, 2)
+#define CALL4(MV, NW) CALL_SP(MV, NW, 4)
+#define CALL8(MV, NW) CALL_SP(MV, NW, 8)
+  if (S == 2) ROW_DISPATCH(H, CALL2);
+  else if (S == 4) ROW_DISPATCH(H, CALL4);
+  else if (S == 8) ROW_DISPATCH(H, CALL8);
+  else return -1;
+#undef CALL2
+#undef CALL4
+#undef CALL8
+#undef CALL_SP
   return 0;
 }
 

@@ -15,27 +15,35 @@ namespace {
 // thread, so a decode step (T ~ 128 tokens) still puts ~900 single-wave workgroups
 // on the 256 CUs instead of 128 workgroups each looping over 3 dependent items.
 //
-// PART: the QKV projection left S f32 split-K partial slabs (part[s][t][ld], slab floats
+// SP > 0: the QKV projection left SP f32 split-K partial slabs (part[s][t][ld], slab floats
 // apart) instead of its bf16 output.  Each item sums its 8 columns in slab order and
 // rounds to bf16 (the values splitk_reduce_kernel would have stored), writes the qkv row
 // exactly as "reduce, then rope_kv" leaves it (q rotated, k unrotated unless
 // write_k_inplace, v copied) and scatters K/V into the cache: one launch instead of two.
-template <bool NEOX, bool PART>
+template <bool NEOX, int SP>
 __global__ __launch_bounds__(64) void rope_kv_kernel(
     bf16_t* __restrict__ qkv, long qs, const int* __restrict__ positions,
     const float* __restrict__ cos_sin, int Hq, int Hkv, int D, bf16_t* __restrict__ kc,
     bf16_t* __restrict__ vc, const int* __restrict__ slots, int BS, int write_k_inplace,
-    const float* __restrict__ part, int S, long slab, long ld) {
+    const float* __restrict__ part, long slab, long ld) {
+  constexpr bool PART = SP > 0;
   const long t = blockIdx.x;
-  // 8 consecutive elements of this token's qkv row at column col, as f32
+  // 8 consecutive elements of this token's qkv row at column col, as f32 (all SP slab
+  // loads issued before the first add)
   auto ld8 = [&](int col, float* f) {
     if constexpr (PART) {
       const float* pp = part + t * ld + col;
-      floatx4 a = *reinterpret_cast<const floatx4*>(pp);
-      floatx4 b = *reinterpret_cast<const floatx4*>(pp + 4);
-      for (int s = 1; s < S; ++s) {
-        a += *reinterpret_cast<const floatx4*>(pp + s * slab);
-        b += *reinterpret_cast<const floatx4*>(pp + s * slab + 4);
+      floatx4 pa[SP], pb[SP];
+#pragma unroll
+      for (int s = 0; s < SP; ++s) {
+        pa[s] = *reinterpret_cast<const floatx4*>(pp + s * slab);
+        pb[s] = *reinterpret_cast<const floatx4*>(pp + s * slab + 4);
+      }
+      floatx4 a = pa[0], b = pb[0];
+#pragma unroll
+      for (int s = 1; s < SP; ++s) {
+        a += pa[s];
+        b += pb[s];
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -153,29 +161,34 @@ int lk_rope_kv(bf16_t* qkv, long qs, const int* positions, const float* cos_sin,
   const int items = (Hq + Hkv) * (neox ? D / 16 : D / 8) + Hkv * (D / 8);
   const dim3 grid((unsigned)T, (items + 63) / 64);
   if (neox)
-    rope_kv_kernel<true, false><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,
-                                                     write_k_inplace, nullptr, 0, 0, 0);
+    rope_kv_kernel<true, 0><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,
+                                                 write_k_inplace, nullptr, 0, 0);
   else
-    rope_kv_kernel<false, false><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,
-                                                      write_k_inplace, nullptr, 0, 0, 0);
+    rope_kv_kernel<false, 0><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,
+                                                  write_k_inplace, nullptr, 0, 0);
   return 0;
 }
 
 int lk_splitk_rope_kv(const float* part, int S, bf16_t* qkv, long qs, const int* positions, const float* cos_sin,
                       long T, int Hq, int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,
                       int write_k_inplace, hipStream_t st) {
-  if (D % 16 || T < 0 || S < 1) return -1;
+  if (D % 16 || T < 0 || !(S == 2 || S == 4 || S == 8)) return -1;
   if (T == 0) return 0;
   const long ld = (long)(Hq + 2 * Hkv) * D;  // partial row = the whole projection output
   const long slab = T * ld;
   const int items = (Hq + Hkv) * (neox ? D / 16 : D / 8) + Hkv * (D / 8);
   const dim3 grid((unsigned)T, (items + 63) / 64);
-  if (neox)
-    rope_kv_kernel<true, true><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,
-                                                    write_k_inplace, part, S, slab, ld);
-  else
-    rope_kv_kernel<false, true><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,
-                                                     write_k_inplace, part, S, slab, ld);
+#define LK_ROPE_SP(SPC)                                                                                        \
+  if (neox)                                                                                                    \
+    rope_kv_kernel<true, SPC><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,   \
+                                                   write_k_inplace, part, slab, ld);                           \
+  else                                                                                                         \
+    rope_kv_kernel<false, SPC><<<grid, 64, 0, st>>>(qkv, qs, positions, cos_sin, Hq, Hkv, D, kc, vc, slots, BS,  \
+                                                    write_k_inplace, part, slab, ld);
+  if (S == 2) { LK_ROPE_SP(2) }
+  else if (S == 4) { LK_ROPE_SP(4) }
+  else { LK_ROPE_SP(8) }
+#undef LK_ROPE_SP
   return 0;
 }
 

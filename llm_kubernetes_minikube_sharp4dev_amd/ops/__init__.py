@@ -365,7 +365,7 @@ def _ws_split_plan(x, w):
     plan = _WS_PLANS.get(key)
     if plan is None:
         plan = _WS_PLANS[key] = tuple(lib().ws_plan(*key, False))
-    return plan if plan[1] >= 2 else None
+    return plan if plan[1] in (2, 4, 8) else None
 
 
 def linear_add_rmsnorm(x, w, residual, norm_w, eps: float):
