@@ -283,14 +283,25 @@ def _use_big(x, w, swiglu: bool) -> bool:
     return _BIG_TABLE.get(_big_key(x, w, swiglu), False)
 
 
-def tune_big_gemm(weights, max_m: int, min_m: int = 512, iters: int = 6) -> dict:
+def tune_big_gemm(weights, max_m: int, min_m: int = 512, iters: int = 8, margin: float = 0.97) -> dict:
     """Time hipBLASLt (+ silu_mul) against the big-tile kernel for every 256-row M bucket
-    in [min_m, max_m] and each (weight, swiglu) pair; record where the kernel wins.
+    in [min_m, max_m] and each (weight, swiglu) pair; record where the kernel wins by more
+    than ``margin``.  The two candidates are timed alternately (A B A B ...) so clock
+    drift during the sweep hits both alike.
     ``weights``: [(w [N, K] bf16 CUDA tensor, swiglu)].  Returns {key: (big_us, lib_us)}."""
     import statistics
 
     L = lib()
     out = {}
+
+    def once(fn):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        return a.elapsed_time(b) * 1e3
+
     for w, swiglu in weights:
         N, K = w.shape
         if K % 64 or N % 256:
@@ -298,24 +309,19 @@ def tune_big_gemm(weights, max_m: int, min_m: int = 512, iters: int = 6) -> dict
         for mb in range(max(min_m, 256) // 256, max_m // 256 + 1):
             M = mb * 256
             x = torch.randn(M, K, device=w.device, dtype=torch.bfloat16)
-
-            def t(fn):
-                for _ in range(2):
-                    fn()
-                ts = []
-                for _ in range(iters):
-                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    a.record()
-                    fn()
-                    b.record()
-                    b.synchronize()
-                    ts.append(a.elapsed_time(b))
-                return statistics.median(ts) * 1e3
-
-            tb = t(lambda: L.big_linear(x, w, swiglu, None, BIG_VARIANT))
-            tl = t(lambda: silu_mul(torch.nn.functional.linear(x, w)) if swiglu else torch.nn.functional.linear(x, w))
+            big = lambda: L.big_linear(x, w, swiglu, None, BIG_VARIANT)  # noqa: E731
+            ref = (lambda: silu_mul(torch.nn.functional.linear(x, w))) if swiglu else \
+                (lambda: torch.nn.functional.linear(x, w))
+            for _ in range(2):
+                big()
+                ref()
+            tbs, tls = [], []
+            for _ in range(iters):
+                tbs.append(once(big))
+                tls.append(once(ref))
+            tb, tl = statistics.median(tbs), statistics.median(tls)
             key = (mb, N, K, swiglu)
-            _BIG_TABLE[key] = tb < 0.98 * tl
+            _BIG_TABLE[key] = tb < margin * tl
             out[key] = (round(tb, 1), round(tl, 1))
     return out
 
