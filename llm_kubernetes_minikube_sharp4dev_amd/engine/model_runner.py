@@ -123,7 +123,8 @@ class ModelRunner:
         self.gemm_tuning = {}
         if self.device.type == "cuda" and os.environ.get("LK_BIG_GEMM", "1") != "0" and hasattr(model, "gemm_shapes"):
             # pick hipBLASLt vs the big-tile MFMA kernel per prefill-step M bucket (~0.5 s)
-            self.gemm_tuning = ops.tune_big_gemm(model.gemm_shapes(), int(os.environ.get("LK_GEMM_TUNE_MAX_M", "4096")))
+            self.gemm_tuning = ops.tune_big_gemm(model.gemm_shapes(), int(os.environ.get("LK_GEMM_TUNE_MAX_M", "4096")),
+                                                 margin=float(os.environ.get("LK_BIG_GEMM_MARGIN", "0.97")))
             wins = [k for k in self.gemm_tuning if ops._BIG_TABLE.get(k)]
             log.info("big-tile GEMM tuned: %d of %d (M bucket, N, K, swiglu) shapes faster than hipBLASLt",
                      len(wins), len(self.gemm_tuning))
