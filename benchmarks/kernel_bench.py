@@ -117,6 +117,15 @@ def case_silu(T=8192, I=14336):
     return {"case": f"silu_mul T{T} I{I}", "us": t * 1e6, "GB/s": T * I * 2 * 3 / t / 1e9}
 
 
+def case_silu_down(T=4096, I=14336, H=4096):
+    """SwiGLU followed by the down projection that consumes its output (how the engine
+    runs them), so a store policy that evicts the activation shows up in the GEMM."""
+    x = torch.randn(T, 2 * I, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(H, I, device=DEV, dtype=torch.bfloat16) * 0.02
+    t = timeit(lambda: torch.nn.functional.linear(ops.silu_mul(x), w))
+    return {"case": f"silu_mul+down T{T} I{I} H{H}", "us": t * 1e6, "TFLOP/s": 2 * T * I * H / t / 1e12}
+
+
 def case_knn(N=485_000, D=768, nq=64):
     c = torch.randn(N, D, device=DEV, dtype=torch.bfloat16)
     q = torch.randn(nq, D, device=DEV, dtype=torch.bfloat16)
@@ -230,7 +239,8 @@ CASES = {
     "prefill": lambda: [case_prefill(), case_prefill(B=8, L=4096), case_prefill_chunk()],
     "prefill_chunk": lambda: [case_prefill_chunk()],
     "encoder": lambda: [case_encoder_attn()],
-    "norm": lambda: [case_rmsnorm(), case_silu()],
+    "norm": lambda: [case_rmsnorm(), case_silu(), case_silu(3584), case_silu(4096), case_silu(128), case_silu(4096, 1792),
+                     case_silu_down(3584), case_silu_down(4096)],
     "knn": lambda: [case_knn(), case_knn(nq=8), case_knn(N=1_000_000, nq=8), case_knn(N=1_000_000, nq=128)],
     "gemm": lambda: [case_gemm(64, 6144, 4096), case_gemm(64, 28672, 4096), case_gemm(64, 4096, 14336),
                      case_gemm(32768, 6144, 4096), case_gemm(32768, 28672, 4096), case_gemm(32768, 4096, 14336)],

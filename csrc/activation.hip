@@ -1,7 +1,9 @@
 // K12 gated / plain activations: SiLU*mul (SwiGLU), GELU (erf and tanh forms,
-// optional fused bias), ReLU.  All 16-byte vectorised and grid-strided
-// (grid capped at ~8 blocks/CU worth of work so huge prefill batches do not
-// launch millions of tiny blocks).
+// optional fused bias), ReLU.  All 16-byte vectorised; the GELU/ReLU kernels are
+// grid-strided (grid capped at ~8 blocks/CU worth of work so huge prefill batches do
+// not launch millions of tiny blocks), SwiGLU uses a 2-D (row segment, row) grid.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -14,22 +16,37 @@ LK_DEVICE float gelu_tanh(float x) {
   return 0.5f * x * (1.f + tanhf(k * (x + 0.044715f * x * x * x)));
 }
 
-// x: [rows, 2*I] (gate | up) with row stride xs; out: [rows, I] with row stride os
+// x: [rows, 2*I] (gate | up) with row stride xs; out: [rows, I] with row stride os.
+// 2-D grid: blockIdx.x walks a row in 256-vector (16-byte) segments, blockIdx.y strides
+// over rows, so there is no 64-bit divide per element.  One vector per thread (more per
+// thread measured slower: benchmarks/silu_probe.hip).  NTL: non-temporal loads, used when
+// the gate_up output is too big to still sit in the 256 MB MALL (5.7 -> 6.5 TB/s at 8k
+// rows).  NTS: non-temporal stores speed this kernel up (5.9 -> 6.8 TB/s at 4k rows) but
+// the down projection that reads the result loses more than that (silu+down pair 383 ->
+// 388 us), so they are off by default.
+template <bool NTL, bool NTS>
 __global__ __launch_bounds__(256) void silu_mul_kernel(bf16_t* __restrict__ out,
                                                        const bf16_t* __restrict__ x, long rows,
                                                        int I, long xs, long os) {
-  const int vpr = I >> 3;
-  const long total = rows * vpr;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const long r = i / vpr;
-    const int c = (int)(i - r * vpr) * 8;
-    float g[8], u[8], y[8];
-    load8(x + r * xs + c, g);
-    load8(x + r * xs + I + c, u);
+  const int v = blockIdx.x * 256 + threadIdx.x;
+  if (v >= (I >> 3)) return;
+  for (long r = blockIdx.y; r < rows; r += gridDim.y) {
+    const short8* gp = reinterpret_cast<const short8*>(x + r * xs + v * 8);
+    const short8* up = reinterpret_cast<const short8*>(x + r * xs + I + v * 8);
+    short8 g, u, y;
+    if constexpr (NTL) {
+      g = __builtin_nontemporal_load(gp);
+      u = __builtin_nontemporal_load(up);
+    } else {
+      g = *gp;
+      u = *up;
+    }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) y[j] = bf2f(f2bf(silu(g[j]))) * u[j];
-    store8(out + r * os + c, y);
+    for (int j = 0; j < 8; ++j)
+      y[j] = (short)f2bf(bf2f(f2bf(silu(bf2f((bf16_t)g[j])))) * bf2f((bf16_t)u[j]));
+    short8* op = reinterpret_cast<short8*>(out + r * os + v * 8);
+    if constexpr (NTS) __builtin_nontemporal_store(y, op);
+    else *op = y;
   }
 }
 
@@ -73,7 +90,19 @@ int grid_for(long work_items) {
 int lk_silu_mul(bf16_t* out, const bf16_t* x, long rows, int I, long xs, long os, hipStream_t st) {
   if (I % 8 || rows < 0) return -1;
   if (rows == 0) return 0;
-  silu_mul_kernel<<<grid_for(rows * (I / 8)), 256, 0, st>>>(out, x, rows, I, xs, os);
+  // LK_SILU_NT: bit 0 = non-temporal stores, bit 1 = force non-temporal loads (A/B knob;
+  // default: plain stores, NT loads once the [rows, 2I] input exceeds the 256 MB MALL)
+  static const int nt_env = [] {
+    const char* e = getenv("LK_SILU_NT");
+    return e ? atoi(e) : -1;
+  }();
+  const bool nts = nt_env < 0 ? false : (nt_env & 1);
+  const bool ntl = nt_env < 0 ? rows * (long)I * 4 > (256L << 20) : ((nt_env >> 1) & 1);
+  const dim3 grid((I / 8 + 255) / 256, (unsigned)(rows < 65535 ? rows : 65535));
+  if (ntl && nts) silu_mul_kernel<true, true><<<grid, 256, 0, st>>>(out, x, rows, I, xs, os);
+  else if (ntl) silu_mul_kernel<true, false><<<grid, 256, 0, st>>>(out, x, rows, I, xs, os);
+  else if (nts) silu_mul_kernel<false, true><<<grid, 256, 0, st>>>(out, x, rows, I, xs, os);
+  else silu_mul_kernel<false, false><<<grid, 256, 0, st>>>(out, x, rows, I, xs, os);
   return 0;
 }
 

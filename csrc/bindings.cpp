@@ -100,6 +100,7 @@ at::Tensor silu_mul(const at::Tensor& x, const c10::optional<at::Tensor>& out_) 
   const int I = x.size(1) / 2;
   at::Tensor out = out_ ? *out_ : at::empty({T, I}, x.options());
   TORCH_CHECK(out.size(0) == T && out.size(1) == I, "out shape"); CHECK_LASTDIM(out);
+  check_rows16(out, "out");
   int rc = lk_silu_mul(bp(out), bp(x), T, I, x.stride(0), out.stride(0), cur_stream());
   CHECK_RC(rc, "silu_mul");
   return out;

@@ -67,6 +67,14 @@ def test_activations(hip):
     torch.manual_seed(3)
     x = torch.randn(33, 2 * 1536, device=DEV, dtype=torch.bfloat16)
     _close(hip.silu_mul(x, None), ref.silu_mul(x), 0.02, 0.01, "silu_mul")
+    # 2-vector-per-thread path (I >= 4096), partial last segment, strided rows in and out
+    for rows, I in ((130, 14336), (7, 4104), (3, 1792)):
+        xw = torch.randn(rows, 2 * I + 64, device=DEV, dtype=torch.bfloat16)
+        xv = xw[:, : 2 * I]
+        ow = torch.full((rows, I + 32), 7.0, device=DEV, dtype=torch.bfloat16)
+        hip.silu_mul(xv, ow[:, :I])
+        _close(ow[:, :I], ref.silu_mul(xv), 0.02, 0.01, f"silu_mul rows{rows} I{I}")
+        assert (ow[:, I:] == 7.0).all(), "silu_mul wrote past the row"
     for kind in (0, 1, 2):
         y = torch.randn(17, 3072, device=DEV, dtype=torch.bfloat16)
         bias = torch.randn(3072, device=DEV, dtype=torch.bfloat16)
