@@ -117,6 +117,14 @@ def case_silu(T=8192, I=14336):
     return {"case": f"silu_mul T{T} I{I}", "us": t * 1e6, "GB/s": T * I * 2 * 3 / t / 1e9}
 
 
+def case_gelu(T=32768, N=3072):
+    """Encoder FFN activation: in-place GELU(erf) with the fused bias, bge-base width."""
+    x = torch.randn(T, N, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    t = timeit(lambda: ops.lib().activation_(x, b, 0))
+    return {"case": f"gelu+bias T{T} N{N}", "us": t * 1e6, "GB/s": T * N * 2 * 2 / t / 1e9}
+
+
 def case_silu_down(T=4096, I=14336, H=4096):
     """SwiGLU followed by the down projection that consumes its output (how the engine
     runs them), so a store policy that evicts the activation shows up in the GEMM."""
@@ -239,6 +247,7 @@ CASES = {
     "prefill": lambda: [case_prefill(), case_prefill(B=8, L=4096), case_prefill_chunk()],
     "prefill_chunk": lambda: [case_prefill_chunk()],
     "encoder": lambda: [case_encoder_attn()],
+    "act": lambda: [case_gelu(), case_gelu(8192), case_gelu(65536)],
     "norm": lambda: [case_rmsnorm(), case_silu(), case_silu(3584), case_silu(4096), case_silu(128), case_silu(4096, 1792),
                      case_silu_down(3584), case_silu_down(4096)],
     "knn": lambda: [case_knn(), case_knn(nq=8), case_knn(N=1_000_000, nq=8), case_knn(N=1_000_000, nq=128)],

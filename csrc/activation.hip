@@ -1,7 +1,6 @@
 // K12 gated / plain activations: SiLU*mul (SwiGLU), GELU (erf and tanh forms,
-// optional fused bias), ReLU.  All 16-byte vectorised; the GELU/ReLU kernels are
-// grid-strided (grid capped at ~8 blocks/CU worth of work so huge prefill batches do
-// not launch millions of tiny blocks), SwiGLU uses a 2-D (row segment, row) grid.
+// optional fused bias), ReLU.  All 16-byte vectorised on a 2-D (row segment, row)
+// grid: no per-element 64-bit index divide, rows beyond 65535 are strided.
 #include <cstdlib>
 
 #include "common.h"
@@ -10,7 +9,20 @@
 namespace {
 
 LK_DEVICE float silu(float x) { return x / (1.f + __expf(-x)); }
-LK_DEVICE float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below bf16's 2^-9): one
+// hardware exp + one reciprocal + a 5-term Horner polynomial.  The library erff made the
+// GELU kernel VALU-bound at ~3.4 TB/s (benchmarks/kernel_bench.py act).
+LK_DEVICE float fast_erf(float x) {
+  const float a = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float y = 1.f - p * t * __expf(-a * a);
+  return copysignf(y, x);
+}
+LK_DEVICE float gelu_erf(float x) { return 0.5f * x * (1.f + fast_erf(x * 0.70710678118654752f)); }
 LK_DEVICE float gelu_tanh(float x) {
   const float k = 0.7978845608028654f;
   return 0.5f * x * (1.f + tanhf(k * (x + 0.044715f * x * x * x)));
@@ -50,40 +62,38 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(bf16_t* __restrict__ out,
   }
 }
 
-// in-place act(x + bias) on [rows, N] (row stride xs); kind 0 = gelu(erf), 1 = gelu(tanh), 2 = relu
+// in-place act(x + bias) on [rows, N] (row stride xs); kind 0 = gelu(erf), 1 = gelu(tanh), 2 = relu.
+// Same 2-D (row segment, row) grid as silu_mul: one 16-byte vector per thread per row.
 template <int KIND>
 __global__ __launch_bounds__(256) void act_kernel(bf16_t* __restrict__ x,
                                                   const bf16_t* __restrict__ bias, long rows,
                                                   int N, long xs) {
-  const int vpr = N >> 3;
-  const long total = rows * vpr;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const long r = i / vpr;
-    const int c = (int)(i - r * vpr) * 8;
-    float v[8];
-    load8(x + r * xs + c, v);
+  const int v = blockIdx.x * 256 + threadIdx.x;
+  if (v >= (N >> 3)) return;
+  const int c = v * 8;
+  float b[8];
+  if (bias) load8(bias + c, b);
+  for (long r = blockIdx.y; r < rows; r += gridDim.y) {
+    float e[8];
+    load8(x + r * xs + c, e);
     if (bias) {
-      float b[8];
-      load8(bias + c, b);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j] + b[j]));
+      for (int j = 0; j < 8; ++j) e[j] = bf2f(f2bf(e[j] + b[j]));
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if constexpr (KIND == 0) v[j] = gelu_erf(v[j]);
-      else if constexpr (KIND == 1) v[j] = gelu_tanh(v[j]);
-      else v[j] = fmaxf(v[j], 0.f);
+      if constexpr (KIND == 0) e[j] = gelu_erf(e[j]);
+      else if constexpr (KIND == 1) e[j] = gelu_tanh(e[j]);
+      else e[j] = fmaxf(e[j], 0.f);
     }
-    store8(x + r * xs + c, v);
+    store8(x + r * xs + c, e);
   }
 }
 
-int grid_for(long work_items) {
-  long g = (work_items + 255) / 256;
-  const long cap = 256L * 8;  // 256 CUs x 8 blocks
-  return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+dim3 row_grid(long rows, int n) {
+  return dim3((unsigned)((n / 8 + 255) / 256), (unsigned)(rows < 65535 ? rows : 65535));
 }
+
 
 }  // namespace
 
@@ -98,7 +108,7 @@ int lk_silu_mul(bf16_t* out, const bf16_t* x, long rows, int I, long xs, long os
   }();
   const bool nts = nt_env < 0 ? false : (nt_env & 1);
   const bool ntl = nt_env < 0 ? rows * (long)I * 4 > (256L << 20) : ((nt_env >> 1) & 1);
-  const dim3 grid((I / 8 + 255) / 256, (unsigned)(rows < 65535 ? rows : 65535));
+  const dim3 grid = row_grid(rows, I);
   if (ntl && nts) silu_mul_kernel<true, true><<<grid, 256, 0, st>>>(out, x, rows, I, xs, os);
   else if (ntl) silu_mul_kernel<true, false><<<grid, 256, 0, st>>>(out, x, rows, I, xs, os);
   else if (nts) silu_mul_kernel<false, true><<<grid, 256, 0, st>>>(out, x, rows, I, xs, os);
@@ -110,7 +120,7 @@ int lk_activation(bf16_t* x, const bf16_t* bias, long rows, int N, long xs, int 
                   hipStream_t st) {
   if (N % 8 || rows < 0) return -1;
   if (rows == 0) return 0;
-  const int g = grid_for(rows * (N / 8));
+  const dim3 g = row_grid(rows, N);
   if (kind == 0) act_kernel<0><<<g, 256, 0, st>>>(x, bias, rows, N, xs);
   else if (kind == 1) act_kernel<1><<<g, 256, 0, st>>>(x, bias, rows, N, xs);
   else if (kind == 2) act_kernel<2><<<g, 256, 0, st>>>(x, bias, rows, N, xs);
