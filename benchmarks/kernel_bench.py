@@ -125,6 +125,16 @@ def case_gelu(T=32768, N=3072):
     return {"case": f"gelu+bias T{T} N{N}", "us": t * 1e6, "GB/s": T * N * 2 * 2 / t / 1e9}
 
 
+def case_layernorm(T=32768, H=768):
+    """Encoder post-LN with the residual add fused (bge-base / MiniLM widths)."""
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn_like(x)
+    w = torch.randn(H, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(H, device=DEV, dtype=torch.bfloat16)
+    t = timeit(lambda: ops.layernorm(x, w, b, 1e-12, residual=r))
+    return {"case": f"layernorm+res T{T} H{H}", "us": t * 1e6, "GB/s": T * H * 2 * 3 / t / 1e9}
+
+
 def case_silu_down(T=4096, I=14336, H=4096):
     """SwiGLU followed by the down projection that consumes its output (how the engine
     runs them), so a store policy that evicts the activation shows up in the GEMM."""
@@ -248,6 +258,7 @@ CASES = {
     "prefill_chunk": lambda: [case_prefill_chunk()],
     "encoder": lambda: [case_encoder_attn()],
     "act": lambda: [case_gelu(), case_gelu(8192), case_gelu(65536)],
+    "ln": lambda: [case_layernorm(), case_layernorm(8192), case_layernorm(32768, 384), case_layernorm(4096, 1024)],
     "norm": lambda: [case_rmsnorm(), case_silu(), case_silu(3584), case_silu(4096), case_silu(128), case_silu(4096, 1792),
                      case_silu_down(3584), case_silu_down(4096)],
     "knn": lambda: [case_knn(), case_knn(nq=8), case_knn(N=1_000_000, nq=8), case_knn(N=1_000_000, nq=128)],
