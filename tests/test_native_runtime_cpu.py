@@ -102,18 +102,20 @@ def _corpus_texts():
     return texts
 
 
-def test_native_bpe_matches_hf_builtin():
-    from llm_kubernetes_minikube_sharp4dev_amd.models.tokenizer import builtin_tokenizer
+def test_native_bpe_matches_hf_builtin(native):
+    from llm_kubernetes_minikube_sharp4dev_amd.models.tokenizer import builtin_tokenizer, native_encoder
 
-    tok = builtin_tokenizer()
-    assert tok.native is not None, "native encoder should support the built-in byte-level BPE"
+    # the process-wide builtin tokenizer may have been created before the runtime was built
+    hf = builtin_tokenizer().tok
+    enc = native_encoder(hf)
+    assert enc is not None, "native encoder should support the built-in byte-level BPE"
     texts = _corpus_texts() + _adversarial_texts()
-    ref = [e.ids for e in tok.tok.encode_batch(texts, add_special_tokens=False)]
-    assert tok.native.encode_batch(texts, 4) == ref
-    assert [tok.native.encode(t) for t in texts[:200]] == ref[:200]
+    ref = [e.ids for e in hf.encode_batch(texts, add_special_tokens=False)]
+    assert enc.encode_batch(texts, 4) == ref
+    assert [enc.encode(t) for t in texts[:200]] == ref[:200]
 
 
-def test_native_bpe_matches_hf_llama3_pretokenizer():
+def test_native_bpe_matches_hf_llama3_pretokenizer(native):
     """Llama-3 layout: Split(llama-3 regex, isolated) + ByteLevel(no regex), ignore_merges."""
     from tokenizers import Regex, Tokenizer, decoders, models, pre_tokenizers, trainers
 
@@ -134,7 +136,7 @@ def test_native_bpe_matches_hf_llama3_pretokenizer():
     assert enc.encode_batch(allt, 3) == [e.ids for e in hf.encode_batch(allt, add_special_tokens=False)]
 
 
-def test_native_decode_rows_matches_python():
+def test_native_decode_rows_matches_python(native):
     import numpy as np
 
     from llm_kubernetes_minikube_sharp4dev_amd.native import runtime as nrt
