@@ -168,20 +168,22 @@ def case_gemm(M, N, K, layout="NT"):
             "GB/s": (M * K + N * K + M * N) * 2 / t / 1e9}
 
 
-def case_big(M, N, K, swiglu=False):
-    """Hand-written 256x256 prefill GEMM (csrc/big_gemm.hip) vs hipBLASLt (+ silu_mul when swiglu)."""
+def case_prefill_gemm(M, N, K, swiglu=False):
+    """Hand-written prefill GEMM (csrc/gemm.hip, best schedule / column tile) vs hipBLASLt
+    (+ silu_mul when swiglu); benchmarks/gemm_bench.py is the full interleaved sweep."""
     L = ops.lib()
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
-    t0 = timeit(lambda: L.big_linear(x, w, swiglu, None, 0))
-    t1 = timeit(lambda: L.big_linear(x, w, swiglu, None, 1))
-    t = timeit(lambda: L.big_linear(x, w, swiglu, None, 2))
+    epi = 1 if swiglu else 0
+    cfgs = ops._gemm_configs(N, epi)
+    ts = {c: timeit(lambda c=c: L.gemm(x, w, None, epi, c[1], None, c[0])) for c in cfgs}
+    c, t = min(ts.items(), key=lambda kv: kv[1])
     if swiglu:
         tb = timeit(lambda: L.silu_mul(torch.nn.functional.linear(x, w)))
     else:
         tb = timeit(lambda: torch.nn.functional.linear(x, w))
-    return {"case": f"big M{M} N{N} K{K}{' swiglu' if swiglu else ''}", "us": t * 1e6,
-            "TFLOP/s": 2 * M * N * K / t / 1e12, "v0_us": t0 * 1e6, "v1_us": t1 * 1e6, "hipblaslt_us": tb * 1e6, "speedup": tb / t}
+    return {"case": f"gemm M{M} N{N} K{K}{' swiglu' if swiglu else ''} s{c[0]}/{c[1]}", "us": t * 1e6,
+            "TFLOP/s": 2 * M * N * K / t / 1e12, "hipblaslt_us": tb * 1e6, "speedup": tb / t}
 
 
 def case_skinny(M, N, K, swiglu=False):
@@ -273,7 +275,7 @@ CASES = {
     "gemm_mid": lambda: [case_gemm(M, N, K) for M in (1024, 2048, 2560, 3072, 3328, 3584, 3840, 4096, 4352,
                                                       5120, 5376, 6144, 8192)
                          for (N, K) in LLAMA8B_SHAPES],
-    "big": lambda: [case_big(M, N, K, N == 28672) for M in (2048, 3328, 3584, 3840, 4096, 8192)
+    "prefill_gemm": lambda: [case_prefill_gemm(M, N, K, N == 28672) for M in (2048, 3328, 3584, 3840, 4096, 8192)
                     for (N, K) in LLAMA8B_SHAPES],
     "gemm_sweep": lambda: [case_gemm(M, N, K, lay) for M in (128, 256, 1024, 4096, 8192, 16384)
                            for (N, K) in LLAMA8B_SHAPES for lay in ("NT", "NN")],

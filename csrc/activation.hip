@@ -8,21 +8,8 @@
 
 namespace {
 
-LK_DEVICE float silu(float x) { return x / (1.f + __expf(-x)); }
-// erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below bf16's 2^-9): one
-// hardware exp + one reciprocal + a 5-term Horner polynomial.  The library erff made the
-// GELU kernel VALU-bound at ~3.4 TB/s (benchmarks/kernel_bench.py act).
-LK_DEVICE float fast_erf(float x) {
-  const float a = fabsf(x);
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
-  float p = fmaf(1.061405429f, t, -1.453152027f);
-  p = fmaf(p, t, 1.421413741f);
-  p = fmaf(p, t, -0.284496736f);
-  p = fmaf(p, t, 0.254829592f);
-  const float y = 1.f - p * t * __expf(-a * a);
-  return copysignf(y, x);
-}
-LK_DEVICE float gelu_erf(float x) { return 0.5f * x * (1.f + fast_erf(x * 0.70710678118654752f)); }
+LK_DEVICE float silu(float x) { return lk_silu(x); }
+LK_DEVICE float gelu_erf(float x) { return lk_gelu_erf(x); }
 LK_DEVICE float gelu_tanh(float x) {
   const float k = 0.7978845608028654f;
   return 0.5f * x * (1.f + tanhf(k * (x + 0.044715f * x * x * x)));

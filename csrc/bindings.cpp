@@ -232,26 +232,34 @@ at::Tensor ws_linear_rope_kv(const at::Tensor& x, const at::Tensor& w, const at:
   return qkv;
 }
 
-// Prefill-regime linear (csrc/big_gemm.hip): x [M, K] . w[N, K]^T -> [M, N], or the fused
-// SwiGLU [M, N/2] for w = [Wg; Wu]
-at::Tensor big_linear(const at::Tensor& x, const at::Tensor& w, bool swiglu, const c10::optional<at::Tensor>& out_,
-                      int64_t variant) {
+// Prefill / encoder-regime linear (csrc/gemm.hip): epi(x [M, K] . w[N, K]^T (+ bias)).
+// epi 0 none, 1 SwiGLU (w = [Wg; Wu], out [M, N/2]), 2 bias, 3 bias+GELU(erf), 4 bias+ReLU.
+at::Tensor gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t epi,
+                int64_t bn, const c10::optional<at::Tensor>& out_, int64_t variant) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_LASTDIM(x); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "x [M,K], w [N,K]");
   check_rows16(x, "x"); check_rows16(w, "w");
   const int M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(M >= 1 && K % 64 == 0, "big_linear: K must be a multiple of 64");
-  TORCH_CHECK(swiglu ? (N % 256 == 0) : (N % 256 == 0), "big_linear: N must be a multiple of 256");
-  const int n_out = swiglu ? N / 2 : N;
+  TORCH_CHECK(lk_gemm_supported(M, N, K, (int)epi, (int)bn), "gemm: unsupported shape M", M, " N", N, " K", K,
+              " epi", epi, " bn", bn);
+  if (epi >= 2) {
+    TORCH_CHECK(bias.has_value(), "gemm: this epilogue needs a bias");
+    CHECK_CUDA(*bias); CHECK_BF16(*bias); CHECK_CONTIG(*bias);
+    TORCH_CHECK(bias->numel() == N && reinterpret_cast<uintptr_t>(bias->data_ptr()) % 8 == 0, "gemm: bias [N], 8-B aligned");
+  }
+  const int n_out = epi == 1 ? N / 2 : N;
   at::Tensor out = out_ ? *out_ : at::empty({M, n_out}, x.options());
   CHECK_BF16(out); CHECK_LASTDIM(out);
-  TORCH_CHECK(out.size(0) == M && out.size(1) == n_out, "out shape");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == n_out, "out shape");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 8 == 0 && out.stride(0) % 4 == 0, "out alignment");
-  TORCH_CHECK(variant >= 0 && variant <= 2, "big_linear: variant 0 (2-stage), 1 (ping-pong), 2 (BK32 4-stage ring)");
-  int rc = lk_big_gemm(bp(x), x.stride(0), bp(w), M, N, K, swiglu ? 1 : 0, bp(out), out.stride(0), (int)variant,
-                       cur_stream());
-  CHECK_RC(rc, "big_linear");
+  int rc = lk_gemm(bp(x), x.stride(0), bp(w), epi >= 2 ? bp(*bias) : nullptr, M, N, K, (int)epi, (int)bn, (int)variant, bp(out),
+                   out.stride(0), cur_stream());
+  CHECK_RC(rc, "gemm");
   return out;
+}
+
+bool gemm_supported(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bn) {
+  return lk_gemm_supported((int)M, (int)N, (int)K, (int)epi, (int)bn) != 0;
 }
 
 std::vector<int64_t> ws_plan(int64_t M, int64_t N, int64_t K, bool swiglu) {
@@ -628,8 +636,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ws_linear", &ws_linear, "", py::arg("x"), py::arg("w"), py::arg("swiglu") = false, py::arg("bn") = 0,
         py::arg("splits") = 0, py::arg("out") = py::none());
   m.def("ws_plan", &ws_plan);
-  m.def("big_linear", &big_linear, "", py::arg("x"), py::arg("w"), py::arg("swiglu") = false,
-        py::arg("out") = py::none(), py::arg("variant") = 1);
+  m.def("gemm", &gemm, "", py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("epi") = 0,
+        py::arg("bn") = 256, py::arg("out") = py::none(), py::arg("variant") = 1);
+  m.def("gemm_supported", &gemm_supported);
   m.def("silu_mul", &silu_mul, "", py::arg("x"), py::arg("out") = py::none());
   m.def("activation_", &activation_);
   m.def("rope_kv_", &rope_kv_);

@@ -74,6 +74,23 @@ LK_DEVICE void store8(bf16_t* p, const float* f) {
   *reinterpret_cast<short8*>(p) = v;
 }
 
+// Activations shared by the elementwise kernels and the GEMM epilogues.
+LK_DEVICE float lk_silu(float x) { return x / (1.f + __expf(-x)); }
+// erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below bf16's 2^-9): one
+// hardware exp + one reciprocal + a 5-term Horner polynomial.  The library erff made the
+// GELU kernel VALU-bound at ~3.4 TB/s (benchmarks/kernel_bench.py act).
+LK_DEVICE float lk_fast_erf(float x) {
+  const float a = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float y = 1.f - p * t * __expf(-a * a);
+  return copysignf(y, x);
+}
+LK_DEVICE float lk_gelu_erf(float x) { return 0.5f * x * (1.f + lk_fast_erf(x * 0.70710678118654752f)); }
+
 // Bijective XCD-aware remap of a flat workgroup id (8 XCDs, round-robin dispatch):
 // consecutive logical tiles land on the same XCD so they share its L2.
 LK_DEVICE int xcd_remap(int bid, int nwg) {

@@ -1,0 +1,463 @@
+// K2, prefill / encoder regime: Y[M, N] = epilogue(X[M, K] . W[N, K]^T) for M > 256 rows
+// (chunked-prefill and mixed serving steps, encoder index-build batches).
+//
+// Epilogues (fused, so no second pass over Y):
+//   NONE       y = acc
+//   SWIGLU     y[:, c] = silu(X Wg^T) * (X Wu^T) for W = [Wg; Wu] (2I rows, out [M, I])
+//   BIAS       y = acc + b
+//   BIAS_GELU  y = gelu_erf(acc + b)          (BERT / bge / MiniLM FFN up-projection)
+//   BIAS_RELU  y = relu(acc + b)              (OPT fc1)
+// Each is rounded like the unfused library GEMM -> activation path (bf16 after the bias add,
+// bf16 after the activation).
+//
+// gfx950 design (the 256x256 LDS-DMA / ping-pong GEMM of the CDNA4 playbook, re-derived for
+// K-contiguous nn.Linear operands):
+//   * 512 threads = 8 waves as 2 (M) x 4 (N); the C tile is 256 x BN with BN = 64 * NF
+//     (NF = 4: 256, NF = 3: 192 -- the 192-wide tile turns N = 6144 into 32 column tiles, so
+//     an M = 4096 QKV projection is exactly 2 waves of 256 CUs instead of 1.5);
+//     each wave owns 128 x 16NF outputs = 8 x NF v_mfma_f32_16x16x32_bf16 fragments;
+//   * BK = 64; every K-tile is split into four LDS "slots" that are consumed at different
+//     times: SA0 / SA1 = the A rows of the waves' first / second 64-row m-half, SB0 / SB1 =
+//     the B rows of their first / second n-half.  Each phase is a READ segment (LDS ->
+//     register fragments, LDS-DMA issue) and an MFMA segment closed by raw s_barriers, with
+//     waves 4-7 one segment behind waves 0-3 so that on every SIMD one wave's MFMAs overlap
+//     its partner's LDS reads.  Two schedules (per-shape choice, ops.tune_gemm):
+//       sched 0: 4 phases per K-tile, one per C quadrant (m-half, n-half) in the order (0,0)
+//         (0,1) (1,1) (1,0); both B halves stay in registers, so SA0/SB0 die after phase 1,
+//         SB1 after 2, SA1 after 3, and each slot of K-tile t+2 is re-staged two phases after
+//         its last read (SA0/SB0 in phase 3, SB1 in 4, SA1 in phase 1 of t+1): one counted
+//         vmcnt(4 + SB1 loads) per K-tile, three slots (~1.75 K-tiles) in flight;
+//       sched 1: 2 phases per K-tile, one per m-half (32 MFMAs per segment, half the
+//         barriers); SA0/SB0/SB1 of K-tile t+1 are staged in phase 1 of t and SA1 in phase 2,
+//         one K-tile of cover; waves 4-7 hold a static s_setprio 1 instead of per-cluster flips.
+//     (PMC, profiles/r2_gemm.md: the barrier waits, not LDS or L2, separate the schedules.)
+//   * staging is 16-byte buffer_load ... lds (LDS-DMA) through wave-uniform buffer
+//     descriptors: per-lane 32-bit row offsets fixed for the whole K loop, the K offset in an
+//     SGPR, rows past M read as zeros by the descriptor's range check (no clamping, no 64-bit
+//     address VALU in the loop).  The LDS image is lane-linear with the (row >> 1) & 7 chunk
+//     XOR applied on the SOURCE offset, which keeps every ds_read_b128 lane group of the
+//     fragment reads on 16 distinct bank slots (SQ_LDS_BANK_CONFLICT = 0);
+//   * operands are swapped in the MFMA (A <- W rows, B <- X rows): a lane ends with one
+//     output row and 4 consecutive columns, so epilogues are per-lane and the stores are
+//     8-byte packed, and SwiGLU pairs the gate / up fragments of the same columns in a lane;
+//   * tiles are visited in an XCD-aware order (bijective remap, 4 row tiles x all column
+//     tiles per group), so an XCD's ~32 concurrent tiles share their X / W K-slices in L2.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
+
+constexpr int kBM = 256, kBK = 64, kGroupM = 4;
+constexpr int kSlotA = 128 * 128;  // an A slot: 128 rows x 128 B
+
+enum { EPI_NONE = 0, EPI_SWIGLU = 1, EPI_BIAS = 2, EPI_BIAS_GELU = 3, EPI_BIAS_RELU = 4 };
+
+LK_DEVICE int swz(int row) { return (row >> 1) & 7; }
+template <int N>
+LK_DEVICE void wait_vm() {  // s_waitcnt vmcnt(N), lgkmcnt / expcnt untouched
+  static_assert(N >= 0 && N < 16, "vmcnt");
+  __builtin_amdgcn_s_waitcnt(N | (0x7 << 4) | (0xF << 8));
+}
+LK_DEVICE void seg_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+LK_DEVICE float rbf(float x) { return bf2f(f2bf(x)); }
+
+template <int NF>
+struct Geo {
+  static_assert(NF == 3 || NF == 4, "NF");
+  static constexpr int BN = 64 * NF;
+  static constexpr int NF0 = 2, NF1 = NF - 2;          // fragments of n-half 0 / 1
+  static constexpr int B1ROWS = 4 * 16 * NF1;           // 128 or 64
+  static constexpr int OFF_A0 = 0, OFF_A1 = kSlotA, OFF_B0 = 2 * kSlotA, OFF_B1 = 3 * kSlotA;
+  static constexpr int BUF = 3 * kSlotA + B1ROWS * 128;  // 64 KB / 56 KB
+  static constexpr int G_B1 = B1ROWS / 64;               // LDS-DMA instructions per wave for SB1 (2 / 1)
+};
+
+// (kernel bodies are __device__ functions: the buffer-resource type exists for the device
+// target only, and a __global__ whose body names it gets no host launch stub)
+template <int NF, int EPI, int PH, int PRIO>
+__device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W,
+                                           const bf16_t* __restrict__ bias, int M, int K, int I,
+                                           bf16_t* __restrict__ out, long ldo, int TM, int TN) {
+  using G = Geo<NF>;
+  constexpr int BN = G::BN, NF0 = G::NF0, NF1 = G::NF1;
+  static_assert(EPI != EPI_SWIGLU || NF == 4, "SwiGLU pairs fragments n and n+2");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  // ---- tile of this block: XCD-contiguous logical ids, grouped 4 row tiles at a time
+  const int nwg = TM * TN;
+  const int L = xcd_remap(blockIdx.x, nwg);
+  const int per_group = kGroupM * TN;
+  const int first = (L / per_group) * kGroupM;
+  const int gm = min(TM - first, kGroupM);
+  const int tm = first + (L % per_group) % gm;
+  const int tn = (L % per_group) / gm;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases stay scalar
+  const int wr = w >> 2, wc = w & 3;
+  const int r = lane & 15, g = lane >> 4;
+
+  // W row feeding B-tile row j
+  auto wrow = [&](int j) -> long {
+    if constexpr (EPI == EPI_SWIGLU) {
+      const int q = j >> 6, jj = j & 63;
+      return (jj < 32 ? 0L : (long)I) + (long)tn * 128 + q * 32 + (jj & 31);
+    } else {
+      return (long)tn * BN + j;
+    }
+  };
+  // slot row -> tile row
+  auto a_row = [](int h, int s) { return (s & 63) + ((s >> 6) << 7) + 64 * h; };
+  auto b0_row = [](int s) { return (s >> 5) * (16 * NF) + (s & 31); };
+  auto b1_row = [](int s) { return (s / (16 * NF1)) * (16 * NF) + 32 + s % (16 * NF1); };
+
+  // ---- LDS-DMA sources and per-wave destinations: a wave instruction moves 8 slot rows x
+  // 128 B; lane l -> row l >> 3, 16-B chunk l & 7 (source chunk swizzled).  Sources are
+  // buffer_load ... lds through wave-uniform descriptors: fixed 32-bit per-lane row offsets, the
+  // K offset in an SGPR, rows past M read as zeros by the descriptor's range check.
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)X, (short)0, (int)min((long)M * ldx * 2, 0x7FFFFFF0L), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)W, (short)0, (int)min((long)(EPI == EPI_SWIGLU ? 2 * I : TN * BN) * K * 2, 0x7FFFFFF0L), 0x00020000);
+  const int lr = lane >> 3, lc = lane & 7;
+  unsigned aoff[2][2], b0off[2], b1off[G::G_B1];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int s = 16 * w + 8 * i + lr;
+      aoff[h][i] = (unsigned)(((long)tm * kBM + a_row(h, s)) * ldx * 2) + ((lc ^ swz(s)) << 4);
+    }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int s = 16 * w + 8 * i + lr;
+    b0off[i] = (unsigned)(wrow(b0_row(s)) * K * 2) + ((lc ^ swz(s)) << 4);
+  }
+#pragma unroll
+  for (int i = 0; i < G::G_B1; ++i) {
+    const int s = 8 * G::G_B1 * w + 8 * i + lr;
+    b1off[i] = (unsigned)(wrow(b1_row(s)) * K * 2) + ((lc ^ swz(s)) << 4);
+  }
+  auto dma = [](__amdgpu_buffer_rsrc_t rs, unsigned off, int kt, unsigned char* dst) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, (unsigned)kt * kBK * 2, 0, 0);
+  };
+  auto issue_a = [&](int h, int kt) {
+    unsigned char* d = smem + (kt & 1) * G::BUF + (h ? G::OFF_A1 : G::OFF_A0) + 16 * w * 128;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) dma(xrs, aoff[h][i], kt, d + i * 8 * 128);
+  };
+  auto issue_b0 = [&](int kt) {
+    unsigned char* d = smem + (kt & 1) * G::BUF + G::OFF_B0 + 16 * w * 128;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) dma(wrs, b0off[i], kt, d + i * 8 * 128);
+  };
+  auto issue_b1 = [&](int kt) {
+    unsigned char* d = smem + (kt & 1) * G::BUF + G::OFF_B1 + 8 * G::G_B1 * w * 128;
+#pragma unroll
+    for (int i = 0; i < G::G_B1; ++i) dma(wrs, b1off[i], kt, d + i * 8 * 128);
+  };
+
+  floatx4 acc[8][NF];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < NF; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // fragments: lane reads slot row (16-row fragment base + r), k chunk 4 kk + g
+  short8 fa[4][2], fb0[NF0][2], fb1[NF1][2];
+  const int rsw = swz(r);  // the fragment bases are multiples of 16: swz(base + r) = swz(r)
+  auto ld = [&](const unsigned char* slot, int s0, int kk) {
+    return *reinterpret_cast<const short8*>(slot + (s0 + r) * 128 + (((4 * kk + g) ^ rsw) << 4));
+  };
+  auto read_a = [&](const unsigned char* buf, int h) {
+    const unsigned char* slot = buf + (h ? G::OFF_A1 : G::OFF_A0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fa[m][kk] = ld(slot, wr * 64 + m * 16, kk);
+  };
+  auto read_b0 = [&](const unsigned char* buf) {
+#pragma unroll
+    for (int n = 0; n < NF0; ++n)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fb0[n][kk] = ld(buf + G::OFF_B0, wc * 32 + n * 16, kk);
+  };
+  auto read_b1 = [&](const unsigned char* buf) {
+#pragma unroll
+    for (int n = 0; n < NF1; ++n)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fb1[n][kk] = ld(buf + G::OFF_B1, wc * 16 * NF1 + n * 16, kk);
+  };
+  auto mma0 = [&](int mh) {  // quadrant (mh, n-half 0)
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < NF0; ++n)
+          acc[mh * 4 + m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[n][kk], fa[m][kk], acc[mh * 4 + m][n], 0, 0, 0);
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
+  };
+  auto mma1 = [&](int mh) {  // quadrant (mh, n-half 1)
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < NF1; ++n)
+          acc[mh * 4 + m][NF0 + n] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[n][kk], fa[m][kk], acc[mh * 4 + m][NF0 + n], 0, 0, 0);
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = K / kBK;
+  if constexpr (PH == 2) {
+    // 2 phases per K-tile: X = m-half 0 x both n-halves (32 MFMAs), Y = m-half 1.  SA0/SB0/SB1
+    // of K-tile t+1 are staged in X(t) (their buffer's previous tile was last read in X(t-1)),
+    // SA1 in Y(t); X(t+1) waits for the first three, Y(t+1) for SA1: one K-tile of cover.
+    issue_a(0, 0);
+    issue_b0(0);
+    issue_b1(0);
+    issue_a(1, 0);
+    wait_vm<0>();
+    seg_barrier();
+    if (wr == 1) seg_barrier();
+    if constexpr (PRIO == 1) {  // static priority for the lagging (younger) half, no per-cluster flips
+      if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+    }
+    for (int t = 0; t < nk; ++t) {
+      const unsigned char* buf = smem + (t & 1) * G::BUF;
+      read_a(buf, 0);
+      read_b0(buf);
+      read_b1(buf);
+      if (t + 1 < nk) {
+        issue_a(0, t + 1);
+        issue_b0(t + 1);
+        issue_b1(t + 1);
+        wait_vm<4 + G::G_B1>();  // SA1(t) landed
+      } else {
+        wait_vm<0>();
+      }
+      seg_barrier();
+      mma0(0);
+      mma1(0);
+      seg_barrier();
+      read_a(buf, 1);
+      if (t + 1 < nk) {
+        issue_a(1, t + 1);
+        wait_vm<2>();  // SA0 / SB0 / SB1 of t+1 landed
+      }
+      seg_barrier();
+      mma1(1);
+      mma0(1);
+      seg_barrier();
+    }
+  } else {
+  // prologue: K-tile 0 whole, K-tile 1 but its SA1 (issued in phase 1 of K-tile 0, as in
+  // the steady state); the counted wait retires exactly K-tile 0
+  issue_a(0, 0);
+  issue_b0(0);
+  issue_b1(0);
+  issue_a(1, 0);
+  if (nk > 1) {
+    issue_a(0, 1);
+    issue_b0(1);
+    issue_b1(1);
+    wait_vm<4 + G::G_B1>();
+  } else {
+    wait_vm<0>();
+  }
+  seg_barrier();
+  if (wr == 1) seg_barrier();  // waves 4-7 run one segment behind
+  for (int t = 0; t < nk; ++t) {
+    const unsigned char* buf = smem + (t & 1) * G::BUF;
+    // phase 1: quadrant (0, 0)
+    read_a(buf, 0);
+    read_b0(buf);
+    if (t + 1 < nk) issue_a(1, t + 1);
+    seg_barrier();
+    mma0(0);
+    seg_barrier();
+    // phase 2: quadrant (0, 1)
+    read_b1(buf);
+    seg_barrier();
+    mma1(0);
+    seg_barrier();
+    // phase 3: quadrant (1, 1); SA0 / SB0 of this buffer are dead -> K-tile t+2
+    read_a(buf, 1);
+    if (t + 2 < nk) {
+      issue_a(0, t + 2);
+      issue_b0(t + 2);
+    }
+    seg_barrier();
+    mma1(1);
+    seg_barrier();
+    // phase 4: quadrant (1, 0); SB1 is dead -> K-tile t+2, then K-tile t+1 must have
+    // landed (every wave retires its own DMA here; the barrier publishes it)
+    if (t + 2 < nk) {
+      issue_b1(t + 2);
+      wait_vm<4 + G::G_B1>();
+    } else {
+      wait_vm<0>();
+    }
+    seg_barrier();
+    mma0(1);
+    seg_barrier();
+  }
+  }
+  if (wr == 0) seg_barrier();  // equal barrier counts for both halves
+
+  // ---- epilogue: lane holds row (.. + r), columns (.. + 4g + v), v = 0..3
+  if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int row = tm * kBM + wr * 128 + m * 16 + r;
+      if (row >= M) continue;
+      bf16_t* orow = out + (long)row * ldo;
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int col = tn * 128 + wc * 32 + n * 16 + 4 * g;
+        float y[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) y[v] = rbf(lk_silu(rbf(acc[m][n][v]))) * rbf(acc[m][n + 2][v]);
+        uint2 pk;
+        pk.x = pack_bf2(y[0], y[1]);
+        pk.y = pack_bf2(y[2], y[3]);
+        *reinterpret_cast<uint2*>(orow + col) = pk;
+      }
+    }
+  } else {
+    float bv[NF][4];
+#pragma unroll
+    for (int n = 0; n < NF; ++n) {
+      const int col = tn * BN + wc * 16 * NF + n * 16 + 4 * g;
+      if constexpr (EPI != EPI_NONE) {
+        const uint2 b = *reinterpret_cast<const uint2*>(bias + col);
+        bv[n][0] = bf2f((bf16_t)(b.x & 0xFFFF));
+        bv[n][1] = bf2f((bf16_t)(b.x >> 16));
+        bv[n][2] = bf2f((bf16_t)(b.y & 0xFFFF));
+        bv[n][3] = bf2f((bf16_t)(b.y >> 16));
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int row = tm * kBM + wr * 128 + m * 16 + r;
+      if (row >= M) continue;
+      bf16_t* orow = out + (long)row * ldo;
+#pragma unroll
+      for (int n = 0; n < NF; ++n) {
+        const int col = tn * BN + wc * 16 * NF + n * 16 + 4 * g;
+        float y[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          float e = acc[m][n][v];
+          if constexpr (EPI != EPI_NONE) e = rbf(e + bv[n][v]);
+          if constexpr (EPI == EPI_BIAS_GELU) e = lk_gelu_erf(e);
+          if constexpr (EPI == EPI_BIAS_RELU) e = fmaxf(e, 0.f);
+          y[v] = e;
+        }
+        uint2 pk;
+        pk.x = pack_bf2(y[0], y[1]);
+        pk.y = pack_bf2(y[2], y[3]);
+        *reinterpret_cast<uint2*>(orow + col) = pk;
+      }
+    }
+  }
+}
+
+template <int NF, int EPI, int PH, int PRIO>
+__global__ __launch_bounds__(512, 1) void gemm_kernel(const bf16_t* __restrict__ X, long ldx,
+                                                      const bf16_t* __restrict__ W,
+                                                      const bf16_t* __restrict__ bias, int M, int K, int I,
+                                                      bf16_t* __restrict__ out, long ldo, int TM, int TN) {
+  gemm8_body<NF, EPI, PH, PRIO>(X, ldx, W, bias, M, K, I, out, ldo, TM, TN);
+}
+
+template <int NF, int EPI, int PH, int PRIO = 0>
+void launch_ph(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
+               long ldo, int TM, int TN, hipStream_t st) {
+  constexpr int lds = 2 * Geo<NF>::BUF;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_kernel<NF, EPI, PH, PRIO>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  gemm_kernel<NF, EPI, PH, PRIO><<<TM * TN, 512, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN);
+}
+// schedule: 0 = 4 phases per K-tile (per-cluster priority), 1 = 2 phases (static priority)
+template <int NF, int EPI>
+void launch(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
+            long ldo, int TM, int TN, int sched, hipStream_t st) {
+  if (sched == 1) launch_ph<NF, EPI, 2, 1>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, st);
+  else launch_ph<NF, EPI, 4, 0>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, st);
+}
+
+template <int NF>
+int dispatch(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi,
+             int sched, bf16_t* out, long ldo, hipStream_t st) {
+  const int TM = (M + kBM - 1) / kBM;
+  if (epi == EPI_SWIGLU) {
+    if constexpr (NF != 4) {
+      return -1;
+    } else {
+      if (N % 2 || (N / 2) % 128) return -1;
+      launch<4, EPI_SWIGLU>(x, ldx, w, bias, M, K, N / 2, out, ldo, TM, N / 256, sched, st);
+      return 0;
+    }
+  }
+  constexpr int BN = 64 * NF;
+  if (N % BN) return -1;
+  if (epi != EPI_NONE && bias == nullptr) return -1;
+  switch (epi) {
+    case EPI_NONE: launch<NF, EPI_NONE>(x, ldx, w, bias, M, K, 0, out, ldo, TM, N / BN, sched, st); break;
+    case EPI_BIAS: launch<NF, EPI_BIAS>(x, ldx, w, bias, M, K, 0, out, ldo, TM, N / BN, sched, st); break;
+    case EPI_BIAS_GELU: launch<NF, EPI_BIAS_GELU>(x, ldx, w, bias, M, K, 0, out, ldo, TM, N / BN, sched, st); break;
+    case EPI_BIAS_RELU: launch<NF, EPI_BIAS_RELU>(x, ldx, w, bias, M, K, 0, out, ldo, TM, N / BN, sched, st); break;
+    default: return -1;
+  }
+  return 0;
+}
+
+}  // namespace
+
+int lk_gemm_supported(int M, int N, int K, int epi, int bn) {
+  if (M < 1 || K < kBK || K % kBK || (bn != 192 && bn != 256)) return 0;
+  if (epi == EPI_SWIGLU) return bn == 256 && N % 2 == 0 && (N / 2) % 128 == 0;
+  return epi >= EPI_NONE && epi <= EPI_BIAS_RELU && N % bn == 0;
+}
+
+// out = epi(X W^T (+ bias)): X [M, K] (row stride ldx), W [N, K] contiguous, out [M, N] (SwiGLU:
+// [M, N/2]) with row stride ldo.  bn = 256 or 192 (column tile).  Requires K % 64 == 0,
+// N % bn == 0 (SwiGLU: bn = 256 and I = N/2 % 128 == 0), 16-B aligned X / W rows and
+// 8-B aligned output rows; any M >= 1.
+int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
+            int variant, bf16_t* out, long ldo, hipStream_t st) {
+  if (!lk_gemm_supported(M, N, K, epi, bn) || ldx % 8 || ldo % 4) return -1;
+  // operands are addressed through 32-bit buffer offsets: W must fit, X is cut into row chunks
+  if ((long)N * K * 2 >= 0x7FFFFFF0L) return -1;
+  const long max_rows = (0x7FFFFFF0L / (ldx * 2)) / kBM * kBM;
+  if (M > max_rows) {
+    if (max_rows < kBM) return -1;
+    for (long m0 = 0; m0 < M; m0 += max_rows) {
+      const int mc = (int)min((long)M - m0, max_rows);
+      const int rc = lk_gemm(x + m0 * ldx, ldx, w, bias, mc, N, K, epi, bn, variant, out + m0 * ldo, ldo, st);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  if (variant < 0 || variant > 1) return -1;
+  const int rc = bn == 256 ? dispatch<4>(x, ldx, w, bias, M, N, K, epi, variant, out, ldo, st)
+                           : dispatch<3>(x, ldx, w, bias, M, N, K, epi, variant, out, ldo, st);
+  LK_CHECK_LAUNCH();
+  return rc;
+}

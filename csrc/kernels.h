@@ -49,9 +49,11 @@ int lk_xgmi_ar_max_ranks();
 int lk_xgmi_allreduce(bf16_t* const* data, unsigned* const* sig, int rank, int world, const bf16_t* in,
                       bf16_t* out, long n, int* err, hipStream_t st);
 
-// big_gemm.hip (prefill-regime linear, 256x256 MFMA tiles, optional fused SwiGLU)
-int lk_big_gemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int swiglu, bf16_t* out,
-                long ldo, int variant, hipStream_t st);
+// gemm.hip (prefill / encoder-regime linear, 256 x {256,192} MFMA tiles, fused epilogues)
+// epi: 0 none, 1 SwiGLU (W = [Wg; Wu]), 2 bias, 3 bias + GELU(erf), 4 bias + ReLU; bn: 256 | 192
+int lk_gemm_supported(int M, int N, int K, int epi, int bn);
+int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
+            int variant, bf16_t* out, long ldo, hipStream_t st);
 
 // rope_kv.hip
 int lk_rope_kv(bf16_t* qkv, long qs, const int* positions, const float* cos_sin, long T, int Hq,

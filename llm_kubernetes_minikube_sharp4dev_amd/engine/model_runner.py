@@ -121,13 +121,12 @@ class ModelRunner:
         self._stager = (_PinnedStager(self.device) if self.device.type == "cuda"
                         and os.environ.get("LK_PINNED_STAGE", "1") != "0" else None)
         self.gemm_tuning = {}
-        if self.device.type == "cuda" and os.environ.get("LK_BIG_GEMM", "1") != "0" and hasattr(model, "gemm_shapes"):
-            # pick hipBLASLt vs the big-tile MFMA kernel per prefill-step M bucket (~0.5 s)
-            self.gemm_tuning = ops.tune_big_gemm(model.gemm_shapes(), int(os.environ.get("LK_GEMM_TUNE_MAX_M", "4096")),
-                                                 margin=float(os.environ.get("LK_BIG_GEMM_MARGIN", "0.97")))
-            wins = [k for k in self.gemm_tuning if ops._BIG_TABLE.get(k)]
-            log.info("big-tile GEMM tuned: %d of %d (M bucket, N, K, swiglu) shapes faster than hipBLASLt",
-                     len(wins), len(self.gemm_tuning))
+        if self.device.type == "cuda" and os.environ.get("LK_GEMM_TUNE", "0") == "1" and hasattr(model, "gemm_shapes"):
+            # opt-in: pick the prefill GEMM's column tile / K-loop schedule per M bucket by
+            # micro-benchmark (~2 s).  Off by default: in the serving A/B the static choice of
+            # ops._gemm_default was as fast or faster (profiles/r2_gemm.md)
+            self.gemm_tuning = ops.tune_gemm(model.gemm_shapes(), int(os.environ.get("LK_GEMM_TUNE_MAX_M", "4096")))
+            log.info("prefill GEMM tuned for %d (M bucket, N, K, epilogue) shapes", len(self.gemm_tuning))
 
     @staticmethod
     def block_bytes(model, block_size: int) -> int:

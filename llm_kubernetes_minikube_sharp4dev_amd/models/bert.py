@@ -5,7 +5,8 @@
 Varlen packed batches ([T, H] rows + cu_seqlens) — no padding FLOPs:
   K1 embedding gather + LayerNorm (one kernel) -> per layer: QKV GEMM ->
   (rotary for nomic) -> bidirectional flash attention (K3, dense K/V rows) ->
-  O GEMM -> residual+LayerNorm (K4, one kernel) -> FFN (GELU or SwiGLU kernel) ->
+  O GEMM (+bias) -> residual+LayerNorm (K4, one kernel) -> FFN up GEMM with the bias+GELU or
+  SwiGLU epilogue fused -> down GEMM (+bias) ->
   residual+LayerNorm -> K5 mean/CLS pooling + L2 normalisation.
 """
 from __future__ import annotations
@@ -92,11 +93,10 @@ class EncoderModel(nn.Module):
                                   False, q_lens_cpu=lens_cpu)
             o = ops.linear(a, L.o, L.o_b)
             h = ops.layernorm(o, L.ln1_w, L.ln1_b, cfg.norm_eps, residual=h)
-            f = ops.linear(h, L.fc1, L.fc1_b)
             if cfg.activation == "swiglu":
-                f = ops.silu_mul(f)
+                f = ops.linear_swiglu(h, L.fc1) if L.fc1_b is None else ops.silu_mul(ops.linear(h, L.fc1, L.fc1_b))
             else:
-                ops.gelu_(f)
+                f = ops.linear(h, L.fc1, L.fc1_b, act="gelu")  # bias + GELU fused into the GEMM
             d = ops.linear(f, L.fc2, L.fc2_b)
             h = ops.layernorm(d, L.ln2_w, L.ln2_b, cfg.norm_eps, residual=h)
         if not pool:

@@ -213,9 +213,9 @@ class LlamaModel(nn.Module):
         return self
 
     def gemm_shapes(self):
-        """(weight, swiglu) of one layer's projections, for GEMM autotuning."""
+        """(weight, epilogue) of one layer's projections, for GEMM autotuning (ops.EPI)."""
         L = self.layers[0]
-        return [(L.qkv, False), (L.o, False), (L.gate_up, True), (L.down, False)]
+        return [(L.qkv, 0), (L.o, 0), (L.gate_up, 1), (L.down, 0)]
 
     def kv_cache_shape(self, num_blocks: int, block_size: int):
         return (num_blocks, self.hkv, block_size, self.D)

@@ -87,8 +87,7 @@ class OPTModel(nn.Module):
             o = ops.linear(attn_out, L.o, L.o_b if self.tp.rank == 0 else None)
             self.tp.all_reduce_(o)
             x = ops.layernorm(o, L.ffn_ln_w, L.ffn_ln_b, cfg.norm_eps, residual=res, write_residual=True)
-            f = ops.linear(x, L.fc1, L.fc1_b)
-            ops.relu_(f)
+            f = ops.linear(x, L.fc1, L.fc1_b, act="relu")
             d = ops.linear(f, L.fc2, L.fc2_b if self.tp.rank == 0 else None)
             self.tp.all_reduce_(d)
             if li + 1 < n:

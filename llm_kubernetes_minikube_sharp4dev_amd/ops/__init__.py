@@ -19,7 +19,7 @@ __all__ = [
     "rmsnorm", "layernorm", "embed_layernorm", "silu_mul", "gelu_", "relu_", "rope_kv_",
     "kv_write", "paged_decode", "flash_prefill", "prefill_tiles", "knn_topk", "knn_merge",
     "pool_normalize", "row_norms", "select_tokens", "repeat_penalty_", "linear", "linear_swiglu",
-    "decode_splits", "rope_cos_sin", "tune_big_gemm", "linear_add_rmsnorm", "linear_rope_kv",
+    "decode_splits", "rope_cos_sin", "tune_gemm", "gemm", "linear_add_rmsnorm", "linear_rope_kv",
 ]
 
 rope_cos_sin = ref.rope_cos_sin
@@ -263,32 +263,84 @@ def _decode_gemm_kind(x, w, swiglu: bool) -> Optional[str]:
     return None
 
 
-# Prefill-regime GEMMs (M > WS_MAX_M): hipBLASLt, or the hand-written 256x256 MFMA kernel
-# (csrc/big_gemm.hip, SwiGLU fused) for the (M bucket, N, K, swiglu) shapes where
-# ``tune_big_gemm`` measured it faster on this device (hipBLASLt's heuristic is uneven
-# across M: profiles/r1_big_gemm.md).  M is bucketed up to the 256-row macro tile.
-BIG_VARIANT = 2
-_BIG_TABLE: dict = {}
+# Prefill / encoder-regime GEMMs (M > WS_MAX_M, and every GEMM with a bias / activation
+# epilogue): the hand-written 256 x {256, 192} MFMA kernel of csrc/gemm.hip with the SwiGLU /
+# bias / GELU / ReLU epilogue fused.  Two tunables per call: the column tile (192 turns
+# N = 6144 into whole waves of 256 CUs) and the K-loop schedule (4 or 2 phases per K-tile).
+# ``tune_gemm`` measures them per (M bucket, N, K, epilogue) at engine start-up; untuned
+# shapes use the wave-quantisation heuristic of ``_gemm_default``.  The vendor library is
+# only reached for shapes the kernel does not support (K % 64, N % 192) -- counted in
+# ``LIBRARY_FALLBACKS`` so a test can assert the serving path never takes it.
+EPI = {None: 0, "swiglu": 1, "bias": 2, "gelu": 3, "relu": 4}
+# measurement knob only: LK_GEMM_LIBRARY=1 sends the prefill-regime GEMMs to hipBLASLt (+ the
+# separate activation kernels) for in-situ A/B against the hand-written kernel
+GEMM_LIBRARY = os.environ.get("LK_GEMM_LIBRARY", "0") == "1"
+_GEMM_TABLE: dict = {}
+LIBRARY_FALLBACKS: dict = {}
 
 
-def _big_key(x, w, swiglu: bool):
-    M = x.shape[0]
-    return ((M + 255) // 256, w.shape[0], w.shape[1], swiglu)
+def _gemm_key(M: int, N: int, K: int, epi: int):
+    return ((M + 255) // 256, N, K, epi)
 
 
-def _use_big(x, w, swiglu: bool) -> bool:
-    if not _BIG_TABLE or not (use_hip(x) and x.dim() == 2 and x.dtype == torch.bfloat16
-                              and w.dtype == torch.bfloat16 and x.stride(1) == 1 and w.is_contiguous()):
-        return False
-    return _BIG_TABLE.get(_big_key(x, w, swiglu), False)
+def _gemm_configs(N: int, epi: int):
+    """(schedule, column tile) candidates the kernel supports for this N / epilogue."""
+    bns = [256] if epi == 1 else [bn for bn in (256, 192) if N % bn == 0]
+    return [(sched, bn) for bn in bns for sched in (0, 1)]
 
 
-def tune_big_gemm(weights, max_m: int, min_m: int = 512, iters: int = 8, margin: float = 0.97) -> dict:
-    """Time hipBLASLt (+ silu_mul) against the big-tile kernel for every 256-row M bucket
-    in [min_m, max_m] and each (weight, swiglu) pair; record where the kernel wins by more
-    than ``margin``.  The two candidates are timed alternately (A B A B ...) so clock
-    drift during the sweep hits both alike.
-    ``weights``: [(w [N, K] bf16 CUDA tensor, swiglu)].  Returns {key: (big_us, lib_us)}."""
+def _gemm_default(M: int, N: int, K: int, epi: int):
+    """Fewest tile-columns x waves: cost(bn) = ceil(tiles / 256 CUs) * bn (ties -> 256), with
+    the 4-phase schedule (fastest on most serving shapes with weights streamed from HBM:
+    profiles/r2_gemm.md)."""
+    tm = (M + 255) // 256
+    best = None
+    for _, bn in _gemm_configs(N, epi):
+        n_cols = N // 2 // 128 if epi == 1 else N // bn
+        cost = -(-tm * n_cols // 256) * (256 if epi == 1 else bn)
+        if best is None or cost < best[0]:
+            best = (cost, bn)
+    if best is None:
+        return None
+    return (0, best[1])
+
+
+def _gemm_ok(x, w) -> bool:
+    return (use_hip(x) and x.dim() == 2 and w.dim() == 2 and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and x.stride(1) == 1 and x.stride(0) % 8 == 0
+            and w.is_contiguous() and x.data_ptr() % 16 == 0)
+
+
+def gemm(x, w, b=None, epi: int = 0, out=None):
+    """epi(x w^T (+ b)) on the hand-written kernel; None if the shape is unsupported."""
+    M, K = x.shape
+    N = w.shape[0]
+    key = _gemm_key(M, N, K, epi)
+    cfg = _GEMM_TABLE.get(key)
+    if cfg is None:
+        cfg = _gemm_default(M, N, K, epi)
+        if cfg is None or not lib().gemm_supported(M, N, K, epi, cfg[1]):
+            return None
+    return lib().gemm(x, w, b, epi, cfg[1], out, cfg[0])
+
+
+def _library(x, w, b, act, key):
+    LIBRARY_FALLBACKS[key] = LIBRARY_FALLBACKS.get(key, 0) + 1
+    y = torch.nn.functional.linear(x, w, b)
+    if act == "gelu":
+        gelu_(y)
+    elif act == "relu":
+        relu_(y)
+    return y
+
+
+def tune_gemm(weights, max_m: int, min_m: int = 512, iters: int = 6, cold_bytes: int = 600 << 20) -> dict:
+    """Time every (schedule, column tile) of the kernel for each 256-row M bucket in
+    [min_m, max_m] and each (weight, epilogue) pair; keep the fastest.  As in serving, the
+    weights arrive from HBM: each launch reads the next of enough weight copies to overflow
+    the 256 MB MALL (a warm-weight tuning picks the 2-phase schedule for the SwiGLU
+    projection, which is 3 % slower in situ).  Candidates are timed round-robin so clock drift
+    hits all alike.  ``weights``: [(w [N, K] bf16 CUDA tensor, epi)].  Returns {key: {cfg: us}}."""
     import statistics
 
     L = lib()
@@ -302,57 +354,76 @@ def tune_big_gemm(weights, max_m: int, min_m: int = 512, iters: int = 8, margin:
         b.synchronize()
         return a.elapsed_time(b) * 1e3
 
-    for w, swiglu in weights:
+    for w, epi in weights:
         N, K = w.shape
-        if K % 64 or N % 256:
+        cfgs = [c for c in _gemm_configs(N, epi) if L.gemm_supported(max_m, N, K, epi, c[1])]
+        if not cfgs:
             continue
+        copies = [w] + [w.clone() for _ in range(max(0, -(-cold_bytes // (N * K * 2)) - 1))]
+        rot = [0]
+
+        def wn():
+            rot[0] = (rot[0] + 1) % len(copies)
+            return copies[rot[0]]
+
+        bias = torch.zeros(N, device=w.device, dtype=torch.bfloat16) if epi >= 2 else None
+        xmax = torch.randn(max_m, K, device=w.device, dtype=torch.bfloat16)
         for mb in range(max(min_m, 256) // 256, max_m // 256 + 1):
-            M = mb * 256
-            x = torch.randn(M, K, device=w.device, dtype=torch.bfloat16)
-            big = lambda: L.big_linear(x, w, swiglu, None, BIG_VARIANT)  # noqa: E731
-            ref = (lambda: silu_mul(torch.nn.functional.linear(x, w))) if swiglu else \
-                (lambda: torch.nn.functional.linear(x, w))
-            for _ in range(2):
-                big()
-                ref()
-            tbs, tls = [], []
+            x = xmax[: mb * 256]
+            fns = {c: (lambda c=c: L.gemm(x, wn(), bias, epi, c[1], None, c[0])) for c in cfgs}
+            for f in fns.values():
+                f()
+            ts = {c: [] for c in cfgs}
             for _ in range(iters):
-                tbs.append(once(big))
-                tls.append(once(ref))
-            tb, tl = statistics.median(tbs), statistics.median(tls)
-            key = (mb, N, K, swiglu)
-            _BIG_TABLE[key] = tb < margin * tl
-            out[key] = (round(tb, 1), round(tl, 1))
+                for c, f in fns.items():
+                    ts[c].append(once(f))
+            med = {c: statistics.median(v) for c, v in ts.items()}
+            key = _gemm_key(mb * 256, N, K, epi)
+            _GEMM_TABLE[key] = min(med, key=med.get)
+            out[key] = {f"s{c[0]}/{c[1]}": round(t, 1) for c, t in med.items()}
+        del copies
     return out
 
 
-def linear(x, w, b=None):
-    """Projection GEMM: decode-sized batches on the hand-written weight-streaming MFMA
-    kernels (skinny / ws), prefill-sized ones on hipBLASLt or the big-tile MFMA kernel
-    where tuned faster."""
-    if b is None:
+def linear(x, w, b=None, act: Optional[str] = None):
+    """Projection GEMM (+ bias, + GELU / ReLU): decode-sized batches without an epilogue on
+    the weight-streaming MFMA kernels (skinny / ws), everything else on the prefill kernel
+    with the epilogue fused."""
+    if not use_hip(x):
+        y = torch.nn.functional.linear(x, w, b)
+        if act is not None:
+            y = ref.activation_(y, None, 0 if act == "gelu" else 2)
+        return y
+    if b is None and act is None:
         kind = _decode_gemm_kind(x, w, False)
         if kind == "skinny":
             return lib().skinny_linear(x, w)
         if kind == "ws":
             return lib().ws_linear(x, w)
-        if kind is None and x.shape[0] > WS_MAX_M and _use_big(x, w, False):
-            return lib().big_linear(x, w, False, None, BIG_VARIANT)
-    return torch.nn.functional.linear(x, w, b)
+    epi = EPI["bias" if act is None else act] if b is not None else 0
+    if act is not None and b is None:
+        b = torch.zeros(w.shape[0], device=x.device, dtype=x.dtype)
+        epi = EPI[act]
+    y = gemm(x, w, b, epi) if _gemm_ok(x, w) and not GEMM_LIBRARY else None
+    if y is None:
+        y = _library(x, w, b, act, (x.shape[0] > WS_MAX_M, w.shape[0], w.shape[1], epi))
+    return y
 
 
 def linear_swiglu(x, w_gate_up):
     """silu(x Wg^T) * (x Wu^T) for a fused [Wg; Wu] weight: one kernel (GEMM with the
-    SwiGLU epilogue) in the decode regime and where the big-tile kernel was tuned
-    faster, hipBLASLt + silu_mul otherwise."""
+    SwiGLU epilogue) in every regime."""
+    if not use_hip(x):
+        return silu_mul(linear(x, w_gate_up))
     kind = _decode_gemm_kind(x, w_gate_up, True)
     if kind == "skinny":
         return lib().skinny_linear(x, w_gate_up, True)
     if kind == "ws":
         return lib().ws_linear(x, w_gate_up, True)
-    if x.shape[0] > WS_SWIGLU_MAX_M and _use_big(x, w_gate_up, True):
-        return lib().big_linear(x, w_gate_up, True, None, BIG_VARIANT)
-    return silu_mul(linear(x, w_gate_up))
+    y = gemm(x, w_gate_up, None, 1) if _gemm_ok(x, w_gate_up) and not GEMM_LIBRARY else None
+    if y is None:
+        y = silu_mul(_library(x, w_gate_up, None, None, (True, w_gate_up.shape[0], w_gate_up.shape[1], 1)))
+    return y
 
 
 # Decode-step fusions: when the weight-streaming GEMM splits K (S >= 2 partial slabs),

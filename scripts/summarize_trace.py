@@ -7,7 +7,10 @@ call count, mean duration, GPU busy fraction and the idle-gap histogram.
 """
 import collections
 import csv
+import os
 import sys
+
+BY_GRID = os.environ.get("SUMMARY_BY_GRID") == "1"
 
 
 def main(path, window_s, top=25):
@@ -21,7 +24,11 @@ def main(path, window_s, top=25):
         if s < t0:
             continue
         ev.append((s, e))
-        a = agg[r["Kernel_Name"].replace("(anonymous namespace)", "anon").split("(")[0][:100]]
+        name = r["Kernel_Name"].replace("(anonymous namespace)", "anon").split("(")[0][:100]
+        if BY_GRID:  # one row per (kernel, grid): separates the GEMM shapes of one template
+            grid = r.get("Grid_Size") or "x".join(r.get(f"Grid_Size_{a}", "?") for a in "XYZ")
+            name += f" grid={grid}"
+        a = agg[name]
         a[0] += e - s
         a[1] += 1
     ev.sort()

@@ -391,30 +391,85 @@ def test_ws_swiglu(hip, M, IK):
     _close(hip.ws_linear(x, w, True, 64, 2), a_ref, 0.03, 0.01, "ws swiglu bn64 S2")
 
 
-@pytest.mark.parametrize("M", [257, 512, 1000, 3584])
-@pytest.mark.parametrize("NK", [(6144, 4096), (4096, 14336), (768, 768), (1280, 8192)])
-def test_big_linear(hip, M, NK):
-    """Prefill-regime 256x256 MFMA GEMM (LDS-DMA staged, XCD-grouped tiles) vs an fp32
-    matmul, including an M tail (masked rows)."""
+GEMM_CFGS = [(0, 256), (1, 256), (0, 192), (1, 192)]
+
+
+@pytest.mark.parametrize("M", [1, 257, 1000, 3584])
+@pytest.mark.parametrize("NK", [(6144, 4096), (4096, 14336), (768, 768), (1280, 8192), (1152, 384)])
+def test_gemm(hip, M, NK):
+    """Prefill-regime 256 x {256, 192} MFMA GEMM (csrc/gemm.hip), both K-loop schedules, vs an
+    fp32 matmul, including M tails (rows past M read as zeros by the buffer descriptor)."""
     N, K = NK
     torch.manual_seed(M + N)
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
     y_ref = x.float() @ w.float().t()
-    for v in (0, 1, 2):
-        _close(hip.big_linear(x, w, False, None, v), y_ref, 0.02, 0.01, f"big v{v} M{M} N{N} K{K}")
+    ran = 0
+    for sched, bn in GEMM_CFGS:
+        if hip.gemm_supported(M, N, K, 0, bn):
+            _close(hip.gemm(x, w, None, 0, bn, None, sched), y_ref, 0.02, 0.01, f"gemm s{sched}/{bn} M{M} N{N} K{K}")
+            ran += 1
+    assert ran >= 2
+
+
+def test_gemm_asymmetric_layout(hip):
+    """A = I with an asymmetric B catches a transposed C write (CDNA4 playbook §3)."""
+    M = N = K = 256
+    x = torch.eye(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K) % 97 - 48).to(torch.bfloat16)
+    for sched, bn in [(0, 256), (1, 256)]:
+        y = hip.gemm(x, w, None, 0, bn, None, sched)
+        assert torch.equal(y.float().cpu(), w.float().t().cpu()), f"s{sched}/{bn}"
 
 
 @pytest.mark.parametrize("M", [300, 2048])
 @pytest.mark.parametrize("IK", [(14336, 4096), (3584, 8192), (1536, 768)])
-def test_big_swiglu_matches_unfused(hip, M, IK):
+def test_gemm_swiglu_matches_unfused(hip, M, IK):
     I, K = IK
     torch.manual_seed(3)
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(2 * I, K, device=DEV, dtype=torch.bfloat16) * 0.05
     a_ref = ref.silu_mul((x.float() @ w.float().t()).to(torch.bfloat16))
-    for v in (0, 1, 2):
-        _close(hip.big_linear(x, w, True, None, v), a_ref, 0.03, 0.01, f"big v{v} swiglu M{M} I{I}")
+    for sched in (0, 1):
+        _close(hip.gemm(x, w, None, 1, 256, None, sched), a_ref, 0.03, 0.01, f"gemm s{sched} swiglu M{M} I{I}")
+
+
+@pytest.mark.parametrize("M", [7, 300, 4000])
+@pytest.mark.parametrize("NK", [(2304, 768), (3072, 768), (768, 3072), (1536, 384)])
+@pytest.mark.parametrize("epi", [2, 3, 4])
+def test_gemm_bias_epilogues(hip, M, NK, epi):
+    """bias / bias+GELU(erf) / bias+ReLU epilogues vs fp32 linear -> bf16 -> activation."""
+    N, K = NK
+    torch.manual_seed(M * 7 + N + epi)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    y = (x.float() @ w.float().t() + b.float()).to(torch.bfloat16).float()
+    if epi == 3:
+        y = torch.nn.functional.gelu(y)
+    elif epi == 4:
+        y = torch.relu(y)
+    for sched, bn in GEMM_CFGS:
+        if hip.gemm_supported(M, N, K, epi, bn):
+            _close(hip.gemm(x, w, b, epi, bn, None, sched), y, 0.03, 0.01, f"gemm epi{epi} s{sched}/{bn} M{M} N{N}")
+
+
+def test_serving_gemms_never_reach_the_library(hip):
+    """Every Llama-3 / bge / OPT projection shape the engine runs goes to the hand-written
+    kernels (no hipBLASLt fallback counted)."""
+    ops.LIBRARY_FALLBACKS.clear()
+    shapes = [(4096, 6144, 4096, None, None), (4096, 4096, 4096, None, None), (3328, 4096, 14336, None, None),
+              (2000, 2304, 768, "b", None), (2000, 3072, 768, "b", "gelu"), (2000, 768, 3072, "b", None),
+              (300, 3072, 768, "b", "relu"), (160, 2304, 768, "b", None)]
+    for M, N, K, b, act in shapes:
+        x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+        w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+        bias = torch.zeros(N, device=DEV, dtype=torch.bfloat16) if b else None
+        ops.linear(x, w, bias, act=act)
+    x = torch.randn(3000, 4096, device=DEV, dtype=torch.bfloat16)
+    ops.linear_swiglu(x, torch.randn(28672, 4096, device=DEV, dtype=torch.bfloat16) * 0.05)
+    torch.cuda.synchronize()
+    assert not ops.LIBRARY_FALLBACKS, ops.LIBRARY_FALLBACKS
 
 
 @pytest.mark.parametrize("M", [33, 64, 100, 128, 200, 256])
