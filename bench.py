@@ -105,6 +105,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world % args.tp:
         raise SystemExit(f"--tp {args.tp} must divide the world size {world}")
+    if args.device == "cuda" and os.environ.get("LK_FORCE_REFERENCE", "0") not in ("", "0", "false", "False"):
+        # the flag routes GPU tensors to the torch reference ops: never measure that as the framework
+        raise SystemExit("bench.py: LK_FORCE_REFERENCE is set -- refusing to time the torch reference path "
+                         "instead of the HIP kernels")
     t_setup = time.perf_counter()
 
     # ---- corpus chunks (CPU, before any GPU init: the pool forks)

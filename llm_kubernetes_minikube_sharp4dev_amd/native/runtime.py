@@ -6,6 +6,7 @@
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
 import subprocess
 import sys
@@ -21,16 +22,25 @@ def so_path() -> Path:
     return Path(__file__).resolve().parent / f"_runtime{sysconfig.get_config_var('EXT_SUFFIX') or '.so'}"
 
 
-def build(verbose: bool = False) -> Path:
+def sanitized_so_path() -> Path:
+    return ROOT / "build" / "asan" / so_path().name
+
+
+def build(verbose: bool = False, sanitize: bool = False) -> Path:
+    """Compile csrc/runtime/*.cpp into the package (``sanitize=True``: an ASan + UBSan build
+    under build/asan/, loaded by setting LK_NATIVE_RUNTIME_SO and preloading libasan)."""
     import pybind11
 
-    out = so_path()
+    out = sanitized_so_path() if sanitize else so_path()
+    out.parent.mkdir(parents=True, exist_ok=True)
     srcs = sorted(SRC.glob("*.cpp"))
     deps = srcs + sorted(SRC.glob("*.h"))
     if out.exists() and all(s.stat().st_mtime <= out.stat().st_mtime for s in deps):
         return out
     cxx = os.environ.get("CXX", "g++")
-    cmd = [cxx, "-O3", "-shared", "-fPIC", "-std=c++17", "-Wall", "-pthread", f"-I{pybind11.get_include()}",
+    opt = (["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
+           if sanitize else ["-O3"])
+    cmd = [cxx, *opt, "-shared", "-fPIC", "-std=c++17", "-Wall", "-pthread", f"-I{pybind11.get_include()}",
            f"-I{sysconfig.get_paths()['include']}", *map(str, srcs), "-o", str(out)]
     if verbose:
         print(" ".join(cmd))
@@ -44,7 +54,13 @@ def build(verbose: bool = False) -> Path:
 def load():
     global _mod
     if _mod is None:
-        _mod = importlib.import_module("llm_kubernetes_minikube_sharp4dev_amd.native._runtime")
+        alt = os.environ.get("LK_NATIVE_RUNTIME_SO")  # e.g. the ASan/UBSan build
+        if alt:
+            spec = importlib.util.spec_from_file_location("llm_kubernetes_minikube_sharp4dev_amd.native._runtime", alt)
+            _mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_mod)
+        else:
+            _mod = importlib.import_module("llm_kubernetes_minikube_sharp4dev_amd.native._runtime")
     return _mod
 
 

@@ -56,3 +56,11 @@ def test_bench_two_rank_dp():
 def test_bench_two_rank_tp():
     d = _run(["--tp", "2"], nproc=2)
     assert d["config"]["parallelism"] == "tp2" and d["config"]["global_batch"] == 2 and d["value"] > 0
+
+
+def test_bench_refuses_forced_reference_on_gpu_device():
+    """--device cuda with LK_FORCE_REFERENCE=1 would time the torch reference ops: refused
+    before any GPU or corpus work."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1"], capture_output=True,
+                       text=True, timeout=120, cwd="/tmp", env=dict(os.environ, LK_FORCE_REFERENCE="1"))
+    assert r.returncode != 0 and "LK_FORCE_REFERENCE" in r.stderr

@@ -1,6 +1,8 @@
 """End-to-end GPU paths (every op on the HIP kernel library): Llama / BERT forwards vs
 HuggingFace fp32 on the CPU, hipGraph decode == eager decode, the RAG pipeline on a
 GPU index, and the loud failure when the kernel library is forced off."""
+import os
+
 import pytest
 import torch
 
@@ -182,11 +184,23 @@ def test_rag_pipeline_on_gpu_index():
     assert len(out) >= 12 and all(r.status in (200, 400, 404, 500) for r in out)
 
 
-def test_forced_reference_fails_loudly_not_silently(monkeypatch):
+def test_forced_reference_fails_loudly_not_silently():
     """LK_FORCE_REFERENCE routes ops to the torch reference; the bench entry point must
-    refuse to run without the HIP library rather than measure a fallback."""
-    from llm_kubernetes_minikube_sharp4dev_amd.ops import _ext
+    refuse to run rather than measure that fallback, and without the flag a GPU op must
+    go through the HIP library (the forced path really changes the dispatch)."""
+    import subprocess
+    import sys
 
-    assert _ext.available()
-    lib = _ext.lib()
-    assert hasattr(lib, "paged_decode") and hasattr(lib, "ws_linear")
+    from llm_kubernetes_minikube_sharp4dev_amd import ops
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "0", "--docs", "10"], cwd=root,
+                       env=dict(os.environ, LK_FORCE_REFERENCE="1"), capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "LK_FORCE_REFERENCE" in (r.stderr + r.stdout)
+    x = torch.randn(4, 768, device="cuda", dtype=torch.bfloat16)
+    assert ops.use_hip(x)
+    os.environ["LK_FORCE_REFERENCE"] = "1"
+    try:
+        assert not ops.use_hip(x)
+    finally:
+        del os.environ["LK_FORCE_REFERENCE"]

@@ -1,4 +1,5 @@
 """C++ block allocator == Python block allocator, operation by operation."""
+import os
 import random
 
 import pytest
@@ -11,8 +12,9 @@ from llm_kubernetes_minikube_sharp4dev_amd.native import runtime
 def native():
     try:
         runtime.build()
-    except Exception as e:  # toolchain missing: the Python allocator is the fallback
-        pytest.skip(f"native build unavailable: {e}")
+    except (ImportError, FileNotFoundError) as e:  # toolchain missing (pybind11 / g++): Python fallback
+        pytest.skip(f"native build toolchain unavailable: {e}")
+    # a RuntimeError from a failed compile of csrc/runtime/*.cpp is NOT skipped: it fails the tests
     return runtime
 
 
@@ -153,3 +155,29 @@ def test_native_decode_rows_matches_python(native):
         assert slots[i] == t[starts[i] // 16] * 16 + starts[i] % 16
         assert list(bt[i, : len(t)]) == list(t) and not bt[i, len(t):].any()
     assert list(slots[4:]) == [-1] * 4 and list(ctx[4:]) == [1] * 4 and list(ids[:4]) == toks
+
+
+@pytest.mark.skipif(bool(os.environ.get("LK_NATIVE_RUNTIME_SO")), reason="already running under the sanitizer build")
+def test_runtime_under_asan_ubsan(native):
+    """Every test of this file again, against an ASan + UBSan build of csrc/runtime/*.cpp
+    (bpe.cpp's Unicode scanners, the block allocator, the decode-row packer)."""
+    import subprocess
+    import sys
+
+    try:
+        so = native.build(sanitize=True)
+    except (ImportError, FileNotFoundError) as e:
+        pytest.skip(f"sanitizer toolchain unavailable: {e}")
+    # libstdc++ is preloaded too: python itself does not link it, so ASan's __cxa_throw
+    # interceptor would otherwise find no real symbol and abort on the first C++ exception
+    libs = [subprocess.run(["gcc", f"-print-file-name={n}"], capture_output=True, text=True).stdout.strip()
+            for n in ("libasan.so", "libstdc++.so")]
+    if not all(os.path.isabs(x) for x in libs):
+        pytest.skip("libasan / libstdc++ not found")
+    env = dict(os.environ, LK_NATIVE_RUNTIME_SO=str(so), LD_PRELOAD=" ".join(libs),
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", __file__],
+                       capture_output=True, text=True, env=env, timeout=900,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "passed" in r.stdout

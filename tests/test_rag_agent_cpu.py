@@ -19,17 +19,32 @@ from llm_kubernetes_minikube_sharp4dev_amd.rag.chunking import (chunk_sliding, s
 from llm_kubernetes_minikube_sharp4dev_amd.rag.embedder import HashEmbedder, parse_embedding_response
 from llm_kubernetes_minikube_sharp4dev_amd.rag.index import RagHit, RagIndex, cosine_exact
 
+# the reference knowledge base, shipped byte-for-byte (Minimal_RAG/knowledge/runbook_scaling.md:1-28)
+RUNBOOK = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "knowledge", "runbook_scaling.md")
 REF_RUNBOOK = "/root/reference/Minimal_Agent_RAG/Minimal_RAG/knowledge/runbook_scaling.md"
 
 
-@pytest.mark.skipif(not os.path.exists(REF_RUNBOOK), reason="reference checkout not mounted")
 def test_reference_runbook_split_lengths():
-    text = open(REF_RUNBOOK, encoding="utf-8").read()
+    text = open(RUNBOOK, encoding="utf-8").read()
     secs = split_by_markdown_headers(text)
     assert [len(s) for s in secs] == [562, 73, 359, 88]
     assert secs[0].startswith("---") and secs[1].startswith("## Obiettivo")
     assert extract_allowed_namespaces(secs[0]) == ["dev", "staging", "sharp4dev", "test-ns-giovanni"]
     assert extract_allowed_namespaces(secs[1]) == []
+
+
+@pytest.mark.skipif(not os.path.exists(REF_RUNBOOK), reason="reference checkout not mounted")
+def test_shipped_runbook_is_the_reference_file():
+    assert open(RUNBOOK, "rb").read() == open(REF_RUNBOOK, "rb").read()
+
+
+def test_knowledge_folder_index_has_the_reference_chunks():
+    """RagIndex over ./knowledge yields the reference runbook's 4 chunks (ids file#i, i over
+    non-empty sanitized sections), plus the extra logs runbook."""
+    idx = RagIndex(HashEmbedder(64))
+    idx.build_from_folder(os.path.dirname(RUNBOOK))
+    ids = [c.id for c in idx.chunks]
+    assert [i for i in ids if i.startswith("runbook_scaling.md#")] == [f"runbook_scaling.md#{i}" for i in range(4)]
 
 
 def test_split_and_resplit():
