@@ -533,6 +533,26 @@ at::Tensor select_allowed(const at::Tensor& logits, const at::Tensor& plan, cons
   return out;
 }
 
+// Fused Ollama-default sampler (csrc/sampling.hip lk_sample): see kernels.h
+at::Tensor sample(at::Tensor& logits, const at::Tensor& prm, at::Tensor& hist, at::Tensor& hist_len, int64_t seed,
+                  const c10::optional<at::Tensor>& out_) {
+  CHECK_CUDA(logits); CHECK_F32(logits); CHECK_LASTDIM(logits);
+  TORCH_CHECK(logits.dim() == 2, "logits [B, V]");
+  const int B = logits.size(0), V = logits.size(1);
+  CHECK_I32(prm); CHECK_CONTIG(prm); TORCH_CHECK(prm.dim() == 2 && prm.size(0) == B && prm.size(1) == 8, "prm [B, 8]");
+  CHECK_I32(hist); CHECK_CONTIG(hist); TORCH_CHECK(hist.dim() == 2, "hist [slots, W]");
+  CHECK_I32(hist_len); CHECK_CONTIG(hist_len); TORCH_CHECK(hist_len.numel() == hist.size(0), "hist_len [slots]");
+  TORCH_CHECK(prm.is_cuda() && hist.is_cuda() && hist_len.is_cuda(), "sampler state must be on the GPU");
+  // slot ids / top_k are read by the kernel: checked here (one small D2H of the parameter rows is
+  // avoided by the caller, which validates the host copy it uploads: ops.sample)
+  at::Tensor out = out_ ? *out_ : at::empty({B}, logits.options().dtype(at::kInt));
+  CHECK_I32(out);
+  int rc = lk_sample(logits.data_ptr<float>(), logits.stride(0), B, V, ip(prm), hist.data_ptr<int>(),
+                     hist_len.data_ptr<int>(), hist.size(1), (unsigned long long)seed, out.data_ptr<int>(), cur_stream());
+  CHECK_RC(rc, "sample");
+  return out;
+}
+
 void repeat_penalty_(at::Tensor& logits, const at::Tensor& window, const at::Tensor& penalty) {
   CHECK_CUDA(logits); CHECK_I32(window); CHECK_F32(penalty); CHECK_CONTIG(window);
   const bool is_bf16 = logits.scalar_type() == at::kBFloat16;
@@ -664,4 +684,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seed") = 0, py::arg("step") = 0);
   m.def("select_tokens", &select_tokens, "", py::arg("logits"), py::arg("temps") = py::none(), py::arg("seed") = 0, py::arg("step") = 0, py::arg("out") = py::none());
   m.def("repeat_penalty_", &repeat_penalty_);
+  m.def("sample", &sample, "", py::arg("logits"), py::arg("prm"), py::arg("hist"), py::arg("hist_len"),
+        py::arg("seed") = 0, py::arg("out") = py::none());
 }

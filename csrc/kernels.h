@@ -107,3 +107,9 @@ int lk_select_tokens(const void* logits, int is_bf16, long ls, int B, int V, con
                      unsigned long long seed, int step, int* out, hipStream_t st);
 int lk_repeat_penalty(void* logits, int is_bf16, long ls, int B, const int* window, int W,
                       const float* penalty, hipStream_t st);
+// Ollama-default sampling (repeat penalty from a device history ring, top-k, top-p,
+// temperature; greedy rows = argmax).  prm: int32 [B, 8] = temperature, top_p, penalty (f32
+// bits), top_k, last_n, slot, reset, seed.  hist: int32 [slots, W] ring, hist_len: [slots].
+// logits (f32, modified in place by the penalty) -> out int32 [B]; the token is appended to the ring.
+int lk_sample(float* logits, long ls, int B, int V, const int* prm, int* hist, int* hist_len, int W,
+              unsigned long long seed, int* out, hipStream_t st);

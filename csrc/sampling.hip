@@ -168,3 +168,260 @@ int lk_repeat_penalty(void* logits, int is_bf16, long ls, int B, const int* wind
   else repeat_penalty_kernel<false><<<B, 64, 0, st>>>(logits, ls, window, W, penalty);
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------
+// Ollama-default sampling on the device (temperature 0.8, top-k 40, top-p 0.9, repeat
+// penalty 1.1 over the last 64 generated tokens): two launches per step, no host work
+// beyond one per-row parameter row.
+//
+//   sample_penalty_kernel: per row, the window of the sequence's device history ring
+//     (hist[slot][*], the last min(len, last_n) tokens) is de-duplicated and applied to
+//     the f32 logits in place (l > 0 ? l / p : l * p).
+//   sample_topkp_kernel (1024 threads per row):
+//     1. each thread's max over its strided slice of the row; the K-th largest of the 1024
+//        maxima (bitonic sort in LDS) is a lower bound T0 of the row's K-th largest value;
+//     2. every element >= T0 is appended to an LDS candidate list (typically ~K of them;
+//        more than kCand -> exact radix select over the row in LDS histograms instead);
+//     3. bitonic sort of the candidates by (value desc, index asc) -> the top K;
+//     4. p_i = exp((v_i - v_0) / T), inclusive scan; keep i while the mass before it is
+//        <= top_p * total (so the token crossing top_p is kept); draw u from a counter-based
+//        hash of (request seed, generated-token position) and pick the first kept i with
+//        prefix > u * kept_total;
+//     5. the token goes to out[row] and is appended to the ring (len + 1).
+//   Greedy rows (T <= 0) take K = 1: the argmax with the lowest index among ties.
+// Row parameters (8 x 32-bit): temperature, top_p, repeat_penalty (f32), top_k, last_n,
+// slot, reset (1 = new sequence: its ring restarts empty), seed (i32).
+constexpr int kSampThreads = 1024, kSampKMax = 1024, kCand = 4096;
+
+LK_DEVICE unsigned fkey(float f) {  // order-preserving float -> uint
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+LK_DEVICE float keyf(unsigned k) { return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k); }
+
+__global__ __launch_bounds__(256) void sample_penalty_kernel(float* __restrict__ logits, long ls,
+                                                             const int* __restrict__ prm,
+                                                             const int* __restrict__ hist,
+                                                             const int* __restrict__ hist_len, int W) {
+  const int row = blockIdx.x;
+  const int* p = prm + row * 8;
+  const float pen = __int_as_float(p[2]);
+  const int last_n = p[4], slot = p[5], reset = p[6];
+  if (pen == 1.f || last_n == 0) return;
+  const int hl = reset ? 0 : hist_len[slot];
+  const int n = min(min(hl, last_n > 0 ? last_n : W), W);
+  const int* h = hist + (long)slot * W;
+  float* lp = logits + (long)row * ls;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    const int tok = h[(hl - 1 - j) % W];
+    bool dup = false;
+    for (int i = 0; i < j; ++i) dup |= (h[(hl - 1 - i) % W] == tok);
+    if (dup || tok < 0) continue;
+    const float l = lp[tok];
+    lp[tok] = l > 0.f ? l / pen : l * pen;
+  }
+}
+
+// block-wide inclusive scan (1024 threads = 16 waves)
+LK_DEVICE float block_scan(float v, float* wsum) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  __syncthreads();
+  if (lane == 63) wsum[w] = v;
+  __syncthreads();
+  float add = 0.f;
+  for (int i = 0; i < w; ++i) add += wsum[i];
+  return v + add;
+}
+
+// bitonic sort of n (power of two <= 4 * 1024) (key desc, idx asc) pairs in LDS
+LK_DEVICE bool before(unsigned ka, int ia, unsigned kb, int ib) { return ka > kb || (ka == kb && ia < ib); }
+LK_DEVICE void bitonic(unsigned* key, int* idx, int n) {
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n; i += kSampThreads) {
+        const int l = i ^ j;
+        if (l > i) {
+          const bool up = (i & k) == 0;  // this run sorted "before"-first
+          const bool swap = up ? before(key[l], idx[l], key[i], idx[i]) : before(key[i], idx[i], key[l], idx[l]);
+          if (swap) {
+            const unsigned tk = key[i];
+            key[i] = key[l];
+            key[l] = tk;
+            const int ti = idx[i];
+            idx[i] = idx[l];
+            idx[l] = ti;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ __launch_bounds__(kSampThreads) void sample_topkp_kernel(const float* __restrict__ logits, long ls, int V,
+                                                                   const int* __restrict__ prm,
+                                                                   int* __restrict__ hist,
+                                                                   int* __restrict__ hist_len, int W,
+                                                                   unsigned long long seed, int* __restrict__ out) {
+  __shared__ unsigned ckey[kCand];
+  __shared__ int cidx[kCand];
+  __shared__ float wsum[16];
+  __shared__ int ncand_s, thr_s, above_s;
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int* p = prm + row * 8;
+  const float temp = __int_as_float(p[0]), top_p = __int_as_float(p[1]);
+  const int top_k = p[3], slot = p[5], reset = p[6], rseed = p[7];
+  const bool greedy = temp <= 0.f;
+  const int K = greedy ? 1 : min(top_k > 0 ? top_k : kSampKMax, min(V, kSampKMax));
+  const float* lp = logits + (long)row * ls;
+
+  // 1. per-thread maxima -> lower bound of the K-th largest
+  unsigned tmax = 0;
+  for (int i = tid; i < V; i += kSampThreads) tmax = max(tmax, fkey(lp[i]));
+  ckey[tid] = tmax;
+  cidx[tid] = tid;
+  if (tid == 0) ncand_s = 0;
+  __syncthreads();
+  bitonic(ckey, cidx, kSampThreads);
+  const unsigned t0 = ckey[K - 1];
+  __syncthreads();
+  // 2. gather every element >= t0
+  for (int i = tid; i < V; i += kSampThreads) {
+    const unsigned k = fkey(lp[i]);
+    if (k >= t0) {
+      const int s = atomicAdd(&ncand_s, 1);
+      if (s < kCand) {
+        ckey[s] = k;
+        cidx[s] = i;
+      }
+    }
+  }
+  __syncthreads();
+  int nc = ncand_s;
+  if (nc > kCand) {
+    // adversarial row (huge tie / plateau above t0): exact K-th key by a 3-digit MSB radix
+    // select with LDS histograms, then gather > threshold plus the lowest-index ties
+    unsigned* hst = ckey;  // reuse the candidate buffer as a 2048-bin histogram
+    unsigned prefix = 0, mask = 0;
+    int kr = K;
+    const int shifts[3] = {21, 10, 0}, bits[3] = {11, 11, 10};
+    for (int d = 0; d < 3; ++d) {
+      const int nb = 1 << bits[d];
+      for (int b = tid; b < 2048; b += kSampThreads) hst[b] = 0;
+      __syncthreads();
+      for (int i = tid; i < V; i += kSampThreads) {
+        const unsigned k = fkey(lp[i]);
+        if ((k & mask) == prefix) atomicAdd(&hst[(k >> shifts[d]) & (nb - 1)], 1u);
+      }
+      __syncthreads();
+      // thread t owns bins 2t', 2t'+1 counted from the top (t' = 1023 - t)
+      const int hi = 2047 - 2 * tid;
+      const float mine = (hi < nb ? (float)hst[hi] : 0.f) + (hi - 1 < nb && hi >= 1 ? (float)hst[hi - 1] : 0.f);
+      const float incl = block_scan(mine, wsum);
+      const float excl = incl - mine;
+      if (excl < kr && incl >= kr) {
+        const float c_hi = hi < nb ? (float)hst[hi] : 0.f;
+        const int b = (excl + c_hi >= kr) ? hi : hi - 1;
+        thr_s = b;
+        above_s = (int)(excl + (b == hi ? 0.f : c_hi));  // elements strictly above bin b
+      }
+      __syncthreads();
+      kr -= above_s;
+      prefix |= (unsigned)thr_s << shifts[d];
+      mask |= (unsigned)(nb - 1) << shifts[d];
+      __syncthreads();
+    }
+    // gather: key > prefix (K - kr of them), then the first kr ties in index order
+    if (tid == 0) ncand_s = 0;
+    __syncthreads();
+    for (int i = tid; i < V; i += kSampThreads) {
+      const unsigned k = fkey(lp[i]);
+      if (k > prefix) {
+        const int s = atomicAdd(&ncand_s, 1);
+        ckey[s] = k;
+        cidx[s] = i;
+      }
+    }
+    __syncthreads();
+    int base = ncand_s, need = kr;
+    for (int c0 = 0; c0 < V && need > 0; c0 += kSampThreads) {
+      const int i = c0 + tid;
+      const bool tie = i < V && fkey(lp[i]) == prefix;
+      const int pos = (int)block_scan(tie ? 1.f : 0.f, wsum);  // ties up to and including this lane
+      if (tie && pos <= need) {
+        ckey[base + pos - 1] = prefix;
+        cidx[base + pos - 1] = i;
+      }
+      if (tid == kSampThreads - 1) thr_s = pos;  // ties in this chunk
+      __syncthreads();
+      const int taken = min(need, thr_s);
+      base += taken;
+      need -= taken;
+      __syncthreads();
+    }
+    nc = base;
+  }
+  // 3. sort the candidates; the first K are the top K
+  int n2 = 1;
+  while (n2 < nc) n2 <<= 1;
+  for (int i = nc + tid; i < n2; i += kSampThreads) {
+    ckey[i] = 0;
+    cidx[i] = 0x7fffffff;
+  }
+  __syncthreads();
+  bitonic(ckey, cidx, n2);
+  const int k_eff = min(K, nc);
+  // 4. temperature softmax over the top K, top-p cut, inverse-CDF draw
+  int tok;
+  if (greedy || k_eff == 1) {
+    tok = cidx[0];
+  } else {
+    const float v0 = keyf(ckey[0]);
+    const float invt = 1.f / temp;
+    const float e = tid < k_eff ? __expf((keyf(ckey[tid]) - v0) * invt) : 0.f;
+    const float incl = block_scan(e, wsum);
+    __shared__ float tot_s, keep_s;
+    __shared__ int nkeep_s;
+    if (tid == k_eff - 1) tot_s = incl;
+    if (tid == 0) nkeep_s = 0;
+    __syncthreads();
+    const bool keep = tid < k_eff && (incl - e) <= top_p * tot_s;
+    if (keep) atomicMax(&nkeep_s, tid + 1);
+    __syncthreads();
+    if (tid == nkeep_s - 1) keep_s = incl;
+    __syncthreads();
+    const int hl = reset ? 0 : hist_len[slot];
+    // one draw per (request seed, generated-token position): reproducible per request, independent
+    // of which batch row or engine step the sequence lands in
+    const unsigned hsh = hash3((unsigned)(seed ^ (seed >> 32)), (unsigned)rseed, (unsigned)hl);
+    const float u = ((float)(hsh >> 8) + 0.5f) * (1.f / 16777216.f) * keep_s;
+    // the first kept i whose inclusive prefix exceeds u
+    __shared__ int pick_s;
+    if (tid == 0) pick_s = nkeep_s - 1;
+    __syncthreads();
+    if (tid < nkeep_s && incl > u && (tid == 0 || incl - e <= u)) atomicMin(&pick_s, tid);
+    __syncthreads();
+    tok = cidx[pick_s];
+  }
+  // 5. emit + append to the history ring
+  if (tid == 0) {
+    const int hl = reset ? 0 : hist_len[slot];
+    out[row] = tok;
+    hist[(long)slot * W + hl % W] = tok;
+    hist_len[slot] = hl + 1;
+  }
+}
+
+int lk_sample(float* logits, long ls, int B, int V, const int* prm, int* hist, int* hist_len, int W,
+              unsigned long long seed, int* out, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (V < 1 || W < 1) return -1;
+  sample_penalty_kernel<<<B, 256, 0, st>>>(logits, ls, prm, hist, hist_len, W);
+  sample_topkp_kernel<<<B, kSampThreads, 0, st>>>(logits, ls, V, prm, hist, hist_len, W, seed, out);
+  return 0;
+}

@@ -149,7 +149,8 @@ class LLMEngine:
         host = ev = ids = None
         if rows:
             seqs = [s for s, _ in rows]
-            ids = out if greedy else self.sampler(out, [s.params for s in seqs], [s.output_ids for s in seqs])
+            ids = out if greedy else self.sampler(out, [s.params for s in seqs], [s.output_ids for s in seqs],
+                                                  [s.req_id for s in seqs])
             if ids.is_cuda:
                 host = torch.empty(ids.shape, dtype=ids.dtype, pin_memory=True)
                 host.copy_(ids, non_blocking=True)
@@ -218,6 +219,7 @@ class LLMEngine:
         if reason:
             seq.step_finish = self.launches
             self.scheduler.finish(seq, reason)
+            self.sampler.release(seq.req_id)
             M.GEN_TOKENS.inc(n)
         if seq.on_token is not None:
             try:

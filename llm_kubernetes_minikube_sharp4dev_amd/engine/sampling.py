@@ -1,9 +1,14 @@
 """Sampling parameters (Ollama ``options`` semantics) and the batched sampler.
 
 Fast paths: an all-greedy batch is one HIP argmax kernel over the logits; a batch
-with temperatures but no top-k/top-p is one HIP Gumbel-max kernel; top-k / top-p
-(Ollama's defaults 40 / 0.9) go through a partial top-k on the GPU.  Repetition
-penalty (Ollama default 1.1 over the last 64 tokens) is a HIP kernel on the logits.
+with temperatures but no top-k/top-p/penalty is one HIP Gumbel-max kernel.  Anything
+else -- Ollama's defaults (temperature 0.8, top-k 40, top-p 0.9, repeat penalty 1.1 over
+the last 64 tokens, which is what an OllamaSharp client gets: it sends no options) -- is
+``ops.sample``: two HIP launches (csrc/sampling.hip lk_sample) driven by one int32
+parameter row per sequence, with each sequence's generated tokens kept in a device
+history ring that the kernel itself appends to (the host never builds a penalty
+window, and with pipelined steps the ring already holds the token the host has not
+collected yet).
 """
 from __future__ import annotations
 
@@ -108,11 +113,76 @@ class Sampler:
         plan = np.concatenate([flags, offs.astype(np.int32), ids.astype(np.int32)])
         return torch.from_numpy(plan).to(dev, non_blocking=True)
 
-    def __call__(self, logits: torch.Tensor, params: list, histories: list) -> torch.Tensor:
-        """logits [B, V] (f32) -> int32 token ids [B] (on logits.device)."""
+    # ---------------------------------------------------------------- device sampler state
+    RING = 256        # history window per sequence (repeat_last_n is clamped to it)
+    SLOTS = 1024      # sequences with a live ring (>= 2x max_num_seqs; LRU-evicted beyond)
+
+    def _ring(self, dev):
+        if getattr(self, "_hist", None) is None or self._hist.device != dev:
+            self._hist = torch.zeros((self.SLOTS, self.RING), dtype=torch.int32, device=dev)
+            self._hist_len = torch.zeros(self.SLOTS, dtype=torch.int32, device=dev)
+            self._slot_of: dict = {}   # key -> (slot, request salt)
+            self._lru: dict = {}       # key -> last step seen
+            self._free = list(range(self.SLOTS - 1, -1, -1))
+            self._assigned = 0
+        return self._hist, self._hist_len
+
+    def _slot(self, key, live: set):
+        """(slot, reset, request salt) of sequence ``key``; a new key takes a free slot or,
+        with none left, the least recently used one not in this batch."""
+        hit = self._slot_of.get(key)
+        if hit is not None:
+            self._lru[key] = self.step
+            return hit[0], 0, hit[1]
+        if self._free:
+            slot = self._free.pop()
+        else:
+            victim = min((k for k in self._lru if k not in live), key=self._lru.get)
+            slot = self._slot_of.pop(victim)[0]
+            self._lru.pop(victim)
+        self._assigned += 1
+        self._slot_of[key] = (slot, self._assigned)
+        self._lru[key] = self.step
+        return slot, 1, self._assigned
+
+    def release(self, key):
+        """Forget a finished sequence's ring (its slot is reused)."""
+        hit = getattr(self, "_slot_of", {}).pop(key, None)
+        if hit is not None:
+            self._lru.pop(key, None)
+            self._free.append(hit[0])
+
+    def _device_sample(self, logits, params, keys):
+        dev = logits.device
+        hist, hist_len = self._ring(dev)
+        B = logits.shape[0]
+        prm = np.zeros((B, 8), dtype=np.int32)
+        f = prm.view(np.float32)
+        live = set(keys)
+        seed = self.seed
+        for i, (p, key) in enumerate(zip(params, keys)):
+            slot, reset, salt = self._slot(key, live)
+            f[i, 0] = 0.0 if p.is_greedy else p.temperature
+            f[i, 1] = p.top_p
+            f[i, 2] = p.repeat_penalty
+            prm[i, 3] = p.top_k
+            prm[i, 4] = min(p.repeat_last_n, self.RING) if p.repeat_last_n >= 0 else self.RING
+            prm[i, 5] = slot
+            prm[i, 6] = reset
+            prm[i, 7] = (int(p.seed) if p.seed is not None else salt) & 0x7FFFFFFF
+        prm_t = torch.from_numpy(prm)
+        if dev.type == "cuda":
+            prm_t = prm_t.pin_memory().to(dev, non_blocking=True)
+        lg = logits if logits.dtype == torch.float32 and logits.is_contiguous() else logits.float().contiguous()
+        return ops.sample(lg, prm_t, hist, hist_len, seed)
+
+    def __call__(self, logits: torch.Tensor, params: list, histories: list, keys: Optional[list] = None) -> torch.Tensor:
+        """logits [B, V] (f32) -> int32 token ids [B] (on logits.device).  ``keys``: a stable
+        id per row's sequence (its history ring); default the row index."""
         self.step += 1
         B = logits.shape[0]
         dev = logits.device
+        keys = list(keys) if keys is not None else list(range(B))
         # constrained decoding: on the GPU the select kernel scans only each row's allowed
         # ids (one host->device copy of the id lists); otherwise everything outside the
         # allowed set is masked -- one copy of the flat (row * V + token) positions and one
@@ -127,8 +197,9 @@ class Sampler:
                 if allowed is not None:
                     rows[i] = self._as_array(allowed, V)
         need_filter = any((not p.is_greedy) and (0 < p.top_k < V or p.top_p < 1.0) for p in params)
+        need_penalty = any(p.repeat_penalty != 1.0 and p.repeat_last_n != 0 for p in params)
         plan = None
-        if rows and not need_filter and SPARSE_SELECT and ops.use_hip(logits):
+        if rows and not need_filter and not need_penalty and SPARSE_SELECT and ops.use_hip(logits):
             # selection straight over each row's allowed ids (HIP select_allowed): no mask
             plan = self._plan(rows, B, dev)
         elif rows:
@@ -139,18 +210,9 @@ class Sampler:
             mask.view(-1).index_fill_(0, idx, 0.0)
             sel = torch.from_numpy(np.asarray(crow, dtype=np.int64)).to(dev, non_blocking=True)
             logits.index_add_(0, sel, mask)
-        # repetition penalty
-        if any(p.repeat_penalty != 1.0 and p.repeat_last_n != 0 for p in params):
-            W = max(max((p.repeat_last_n if p.repeat_last_n > 0 else len(h)) for p, h in zip(params, histories)), 1)
-            win = torch.full((B, W), -1, dtype=torch.int32)
-            pen = torch.ones(B, dtype=torch.float32)
-            for i, (p, h) in enumerate(zip(params, histories)):
-                if p.repeat_penalty != 1.0 and p.repeat_last_n != 0 and h:
-                    n = p.repeat_last_n if p.repeat_last_n > 0 else len(h)
-                    tail = h[-n:]
-                    win[i, : len(tail)] = torch.tensor(tail, dtype=torch.int32)
-                    pen[i] = p.repeat_penalty
-            ops.repeat_penalty_(logits, win.to(dev, non_blocking=True), pen.to(dev, non_blocking=True))
+        if need_filter or need_penalty:
+            # Ollama's chain (penalty -> top-k -> temperature -> top-p -> draw) in one fused kernel
+            return self._device_sample(logits, params, keys)
         if all(p.is_greedy for p in params):
             if plan is not None:
                 return ops.lib().select_allowed(logits, plan)
@@ -161,27 +223,6 @@ class Sampler:
             if p.seed is not None:
                 seed = int(p.seed)
                 break
-        if not need_filter:
-            if plan is not None:
-                return ops.lib().select_allowed(logits, plan, temps.to(dev), seed, self.step)
-            return ops.select_tokens(logits, temps.to(dev), seed=seed, step=self.step)
-        return self._filtered(logits, params, temps.to(dev), seed)
-
-    def _filtered(self, logits, params, temps, seed):
-        kmax = max(p.top_k if p.top_k > 0 else 0 for p in params)
-        kmax = kmax if kmax > 0 else 1024
-        kmax = min((kmax + 7) // 8 * 8, logits.shape[1])  # 32-B aligned rows for the HIP select
-        vals, idx = torch.topk(logits, kmax, dim=-1)
-        B = logits.shape[0]
-        for i, p in enumerate(params):
-            if p.is_greedy:
-                continue
-            if 0 < p.top_k < kmax:
-                vals[i, p.top_k:] = float("-inf")
-            if p.top_p < 1.0:
-                probs = torch.softmax(vals[i] / max(p.temperature, 1e-6), -1)
-                cum = probs.cumsum(-1)
-                cut = (cum - probs) > p.top_p
-                vals[i].masked_fill_(cut, float("-inf"))  # a boolean-index store would sync
-        pick = ops.select_tokens(vals.contiguous(), temps, seed=seed, step=self.step)
-        return idx.gather(1, pick.long()[:, None]).squeeze(1).int()
+        if plan is not None:
+            return ops.lib().select_allowed(logits, plan, temps.to(dev), seed, self.step)
+        return ops.select_tokens(logits, temps.to(dev), seed=seed, step=self.step)

@@ -18,7 +18,7 @@ from ._ext import available, force_reference, lib, use_hip  # noqa: F401
 __all__ = [
     "rmsnorm", "layernorm", "embed_layernorm", "silu_mul", "gelu_", "relu_", "rope_kv_",
     "kv_write", "paged_decode", "flash_prefill", "prefill_tiles", "knn_topk", "knn_merge",
-    "pool_normalize", "row_norms", "select_tokens", "repeat_penalty_", "linear", "linear_swiglu",
+    "pool_normalize", "row_norms", "select_tokens", "repeat_penalty_", "sample", "linear", "linear_swiglu",
     "decode_splits", "rope_cos_sin", "tune_gemm", "gemm", "linear_add_rmsnorm", "linear_rope_kv",
 ]
 
@@ -221,6 +221,14 @@ def select_tokens(logits, temps=None, seed: int = 0, step: int = 0, out=None):
     if use_hip(logits):
         return lib().select_tokens(logits, temps, int(seed) & ((1 << 63) - 1), int(step), out)
     return ref.select_tokens(logits, temps, seed, step)
+
+
+def sample(logits, prm, hist, hist_len, seed: int = 0, out=None):
+    """Ollama-default sampling of every row (repeat penalty from the device history ring,
+    top-k, top-p, temperature; greedy rows = argmax); appends the tokens to the ring."""
+    if use_hip(logits):
+        return lib().sample(logits, prm, hist, hist_len, int(seed) & ((1 << 63) - 1), out)
+    return ref.sample(logits, prm, hist, hist_len, seed)
 
 
 def repeat_penalty_(logits, window, penalty):

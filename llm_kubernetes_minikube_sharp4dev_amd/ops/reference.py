@@ -254,3 +254,59 @@ def repeat_penalty_(logits, window, penalty):
         l = logits[b, idx].float()
         logits[b, idx] = torch.where(l > 0, l / p, l * p).to(logits.dtype)
     return logits
+
+
+SAMPLE_KMAX = 1024  # csrc/sampling.hip kSampKMax
+
+
+def sample(logits, prm, hist, hist_len, seed=0):
+    """fp32 reference of lk_sample (csrc/sampling.hip): per row the repeat penalty over the
+    unique tokens of the last min(len, last_n) ring entries, top-k by (value desc, index asc),
+    softmax at the row's temperature, the top-p prefix (a token is kept while the mass before
+    it is <= top_p), one draw; the token is appended to the ring.  Same distribution as the
+    kernel (the random stream differs: torch's generator seeded per (seed, request seed,
+    position))."""
+    B, V = logits.shape
+    W = hist.shape[1]
+    out = torch.empty(B, dtype=torch.int32)
+    P = prm.cpu()
+    for r in range(B):
+        row = P[r]
+        temp = float(row[0:1].view(torch.float32)[0])
+        top_p = float(row[1:2].view(torch.float32)[0])
+        pen = float(row[2:3].view(torch.float32)[0])
+        top_k, last_n, slot, reset, rseed = (int(x) for x in row[3:8])
+        hl = 0 if reset else int(hist_len[slot])
+        l = logits[r].float().clone()
+        if pen != 1.0 and last_n != 0:
+            n = min(hl, last_n if last_n > 0 else W, W)
+            toks = {int(hist[slot, (hl - 1 - j) % W]) for j in range(n)}
+            for t in toks:
+                if t >= 0:
+                    l[t] = l[t] / pen if l[t] > 0 else l[t] * pen
+            logits[r] = l.to(logits.dtype)
+        greedy = temp <= 0.0
+        K = 1 if greedy else min(top_k if top_k > 0 else SAMPLE_KMAX, V, SAMPLE_KMAX)
+        order = _topk_stable(l, K)
+        if greedy or K == 1:
+            tok = order[0]
+        else:
+            v = l[torch.tensor(order)].double()
+            e = torch.exp((v - v[0]) / temp)
+            incl = torch.cumsum(e, 0)
+            keep = (incl - e) <= top_p * incl[-1]
+            nkeep = int(keep.sum())
+            g = torch.Generator().manual_seed((int(seed) * 1000003 + rseed * 7919 + hl) & ((1 << 62) - 1))
+            u = float(torch.rand((), generator=g, dtype=torch.float64)) * float(incl[nkeep - 1])
+            pick = int((incl[:nkeep] > u).nonzero()[0]) if bool((incl[:nkeep] > u).any()) else nkeep - 1
+            tok = order[pick]
+        out[r] = tok
+        hist[slot, hl % W] = tok
+        hist_len[slot] = hl + 1
+    return out.to(logits.device)
+
+
+def _topk_stable(l, K):
+    """indices of the K largest (value desc, index asc)."""
+    vals, idx = torch.sort(l, descending=True, stable=True)
+    return idx[:K].tolist()

@@ -1,0 +1,63 @@
+"""Sampler semantics on the CPU (ops.reference.sample, the oracle of csrc/sampling.hip):
+Ollama's default chain, the per-sequence history ring, slot reuse and seeds."""
+import numpy as np
+import torch
+
+from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import Sampler, SamplingParams
+from llm_kubernetes_minikube_sharp4dev_amd.ops import reference as ref
+
+
+def _support(row, temp, top_k, top_p):
+    v, idx = torch.sort(row.double(), descending=True, stable=True)
+    v, idx = v[:top_k], idx[:top_k]
+    e = torch.exp((v - v[0]) / temp)
+    incl = torch.cumsum(e, 0)
+    return set(idx[(incl - e) <= top_p * incl[-1]].tolist())
+
+
+def test_default_params_are_ollamas():
+    p = SamplingParams()
+    assert (p.temperature, p.top_k, p.top_p, p.repeat_penalty, p.repeat_last_n) == (0.8, 40, 0.9, 1.1, 64)
+    assert SamplingParams.from_ollama(None).top_k == 40
+
+
+def test_sampler_support_ring_and_release():
+    torch.manual_seed(0)
+    s = Sampler(500, seed=1)
+    base = torch.randn(500) * 3
+    p = SamplingParams()
+    keys = ["x", "y"]
+    for step in range(5):
+        logits = base.repeat(2, 1).clone()
+        ids = s(logits, [p, p], [[], []], keys)
+        for t in ids.tolist():
+            assert t in _support(base, 0.8, 40, 0.9) or step > 0  # later steps: penalised row
+    slots = [s._slot_of[k][0] for k in keys]
+    assert s._hist_len[slots].tolist() == [5, 5]
+    s.release("x")
+    assert "x" not in s._slot_of and slots[0] in s._free
+
+
+def test_repeat_penalty_counts_generated_tokens_once():
+    """Duplicates in the window are penalised once (llama.cpp / Ollama semantics)."""
+    V = 10
+    logits = torch.zeros(1, V)
+    logits[0, 3] = 4.0
+    hist = torch.tensor([[3, 3, 3, 3] + [0] * 60], dtype=torch.int32)
+    hl = torch.tensor([4], dtype=torch.int32)
+    prm = np.zeros((1, 8), dtype=np.int32)
+    f = prm.view(np.float32)
+    f[0, 0], f[0, 1], f[0, 2] = 0.0, 1.0, 2.0
+    prm[0, 3:8] = [0, 64, 0, 0, 0]
+    ref.sample(logits, torch.from_numpy(prm), hist, hl)
+    assert float(logits[0, 3]) == 2.0  # 4 / 2 once, not 4 / 16
+
+
+def test_seeded_requests_are_reproducible():
+    base = torch.randn(1, 300) * 2
+    outs = []
+    for _ in range(2):
+        s = Sampler(300, seed=9)
+        p = SamplingParams(seed=42)
+        outs.append([int(s(base.clone(), [p], [[]], ["r"])[0]) for _ in range(4)])
+    assert outs[0] == outs[1]
