@@ -89,6 +89,13 @@ def parse():
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: BASELINE config 1 plumbing run (fp32 torch reference ops, gloo), e.g. "
                          "--device cpu --model opt-125m --embedder minilm-l6 --docs 1000")
+    ap.add_argument("--sampling", choices=["greedy", "ollama"], default="greedy",
+                    help="greedy (default; with the tool-call grammar unless --unconstrained) or Ollama's server "
+                         "defaults (temperature 0.8, top-k 40, top-p 0.9, repeat penalty 1.1: what the .NET client "
+                         "gets, no grammar) -- the in-process arm of the --via-http comparison")
+    ap.add_argument("--via-http", action="store_true",
+                    help="the .NET-facing path: Ollama-compatible server + Minimal_RAG app as separate processes, "
+                         "/agent_rag driven over HTTP at concurrency 1, 8, 128 (benchmarks/http_bench.py)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -100,6 +107,13 @@ def log(rank, *a):
 
 def main():
     args = parse()
+    if args.via_http:  # before any GPU use: the servers are child processes
+        import subprocess
+
+        cmd = [sys.executable, os.path.join(ROOT, "benchmarks", "http_bench.py"), "--docs", str(args.docs),
+               "--max-new-tokens", str(args.max_new_tokens), "--model", args.model, "--embedder", args.embedder,
+               "--kv-gb", str(args.kv_gb)] + (["--json-out", args.json_out] if args.json_out else [])
+        raise SystemExit(subprocess.call(cmd))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -206,7 +220,11 @@ def main():
         runner_kw["num_blocks"] = max(256, args.batch * 80)
     engine_kw = dict(max_num_batched_tokens=mbt, enable_prefix_caching=not args.no_prefix_cache, eos_ids=set(),
                      token_align=args.token_align)
-    params = SamplingParams.greedy(args.max_new_tokens, ignore_eos=True)
+    if args.sampling == "ollama":
+        params = SamplingParams(max_tokens=args.max_new_tokens, ignore_eos=True)  # Ollama defaults
+        args.constrained = False
+    else:
+        params = SamplingParams.greedy(args.max_new_tokens, ignore_eos=True)
     if args.constrained:
         from llm_kubernetes_minikube_sharp4dev_amd.engine.constrained import tool_call_processor
 
@@ -225,11 +243,11 @@ def main():
         if args.tp > 1:
             engine = make_tp_engine(llm, tpg, tok, engine_kw=engine_kw, **runner_kw)
             if runner_kw["use_graphs"]:
-                tp_capture_all(engine, max_batch=max(args.batch, 1), variants=(not args.constrained,))
+                tp_capture_all(engine, max_batch=max(args.batch, 1), variants=(args.sampling == "greedy" and not args.constrained,))
         else:
             engine = LLMEngine(llm, tok, **runner_kw, **engine_kw)
             if runner_kw["use_graphs"]:
-                engine.runner.capture_all(max_batch=max(args.batch, 1), variants=(not args.constrained,))
+                engine.runner.capture_all(max_batch=max(args.batch, 1), variants=(args.sampling == "greedy" and not args.constrained,))
         k8s = FakeCluster.default()
         rag = RagAgentPipeline(index, engine, tok, k8s, cfg)
         agent = AgentPipeline(engine, tok, k8s, cfg)
@@ -387,7 +405,9 @@ def main():
                 "admit_chunk": args.admit_chunk if args.mode == "continuous" else None,
                 "corpus_chunks": n,
                 "max_new_tokens": args.max_new_tokens,
-                "decoding": "greedy, ignore_eos" + (", tool-call grammar" if args.constrained else ""),
+                "decoding": ("Ollama defaults (T 0.8, top-k 40, top-p 0.9, repeat penalty 1.1), ignore_eos"
+                             if args.sampling == "ollama" else
+                             "greedy, ignore_eos" + (", tool-call grammar" if args.constrained else "")),
                 "prefix_caching": not args.no_prefix_cache,
                 "hip_graphs": not args.no_graphs,
                 "avg_cached_prefix_tokens": round(statistics.mean(pre), 1) if pre else 0,

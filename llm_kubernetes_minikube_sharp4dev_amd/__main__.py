@@ -109,8 +109,46 @@ def cmd_rag_app(args):
     if args.ollama_url:
         cfg.agent.ollama_url = cfg.agent.embedder_url = args.ollama_url
     emb, llm, k8s = _backends(args, cfg)
+    if args.synthetic_docs:
+        idx = _synthetic_index(args, emb)
+        _uvicorn(create_rag_app(cfg, idx, llm, k8s, build_index=False), args.host, args.port)
+        return
     idx = RagIndex(emb, backend=cfg.rag.index_backend)
     _uvicorn(create_rag_app(cfg, idx, llm, k8s), args.host, args.port)
+
+
+def _synthetic_index(args, query_embedder):
+    """Benchmark bootstrap (benchmarks/http_bench.py): the synthetic runbook corpus of
+    bench.py, bulk-embedded ONCE on this process's GPU by an in-process encoder of the same
+    preset and seed as the serving process's embedder (the batched replacement of the
+    reference's serial per-chunk HTTP embedding, ``RagIndex.cs:47``), kNN on the GPU; every
+    request's query embedding still goes through ``query_embedder`` (HTTP /api/embeddings)."""
+    import torch
+
+    from .config import Config
+    from .engine.embed_engine import EmbeddingEngine
+    from .models import build_encoder
+    from .models.tokenizer import builtin_tokenizer
+    from .rag.corpus import build_chunks
+    from .rag.index import RagChunk, RagIndex
+
+    chunks = build_chunks(args.synthetic_docs, 0, workers=8)
+    dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    enc = build_encoder(args.bulk_embed, device=dev, seed=Config().engine.seed,
+                        dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32)
+    eng = EmbeddingEngine(enc, builtin_tokenizer(), name=args.bulk_embed, max_tokens_per_batch=131072)
+    corpus = eng.embed([c[2] for c in chunks]).to(torch.bfloat16 if dev.type == "cuda" else torch.float32)
+    idx = RagIndex(query_embedder, backend="gpu" if dev.type == "cuda" else "exact", device=str(dev))
+    idx.chunks = [RagChunk(i, s, t) for i, s, t in chunks]
+    if dev.type == "cuda":
+        idx.set_gpu_corpus(corpus.contiguous())
+    else:
+        idx._emb = list(corpus.float().numpy())
+    del enc, eng
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
+    print(f"[rag-app] synthetic index: {len(chunks)} chunks", flush=True)
+    return idx
 
 
 def cmd_agent_app(args):
@@ -200,6 +238,11 @@ def main(argv=None):
         p.add_argument("--knowledge", default=None)
         p.add_argument("--kubeconfig", default=None)
         p.add_argument("--index-cache", default=None)
+        if name == "rag-app":
+            p.add_argument("--synthetic-docs", type=int, default=0,
+                           help="index bench.py's synthetic corpus of this many documents instead of --knowledge")
+            p.add_argument("--bulk-embed", default="bge-base",
+                           help="encoder preset for the one-off bulk index build (same seed as the server's)")
         p.set_defaults(fn=fn)
     p = common(sub.add_parser("all"), 0)
     p.add_argument("--device", default=None)

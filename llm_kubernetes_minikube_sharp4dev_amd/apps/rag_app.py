@@ -53,6 +53,13 @@ def create_rag_app(cfg: Optional[Config] = None, index=None, llm=None, k8s=None,
     if cfg.server.https_redirection:
         add_https_redirection(app, cfg.server.rag_https_port)
 
+    import numpy as np
+
+    from ..serving.batcher import MicroBatcher
+
+    knn_batcher = MicroBatcher(lambda qs: index.search_vectors(np.stack([np.asarray(q, dtype=np.float32) for q in qs]),
+                                                               r.agent_topk), max_items=64)
+
     @app.get("/health")
     async def health():
         return NetJSONResponse({"status": "ok"})
@@ -97,7 +104,18 @@ def create_rag_app(cfg: Optional[Config] = None, index=None, llm=None, k8s=None,
         if is_blank(prompt):
             return NetJSONResponse({"error": "Prompt mancante"}, status_code=400)
         with tracer.span("rag.retrieve"):
-            hits = await asyncio.to_thread(index.query, prompt, r.agent_topk)
+            if hasattr(index, "search_vectors") and hasattr(index, "embedder"):
+                with tracer.span("rag.embed"):
+                    if hasattr(index.embedder, "aembed_one"):  # HTTP embedder: no worker thread
+                        qv = (await index.embedder.aembed_one(prompt))[None]
+                    else:
+                        qv = await asyncio.to_thread(index.embedder.embed, [prompt])
+                with tracer.span("rag.knn"):
+                    # concurrent requests' queries share one kNN launch (one corpus pass)
+                    res = await knn_batcher.submit([qv[0]])
+                hits = index.hits(res[0])
+            else:
+                hits = await asyncio.to_thread(index.query, prompt, r.agent_topk)
         if not hits:
             return NetJSONResponse({"result": None, "citations": [], "note": "Nessuna evidenza trovata nei runbook."})
         citations, evidence = select_citations(hits, r.evidence_min_score, r.citation_best_ratio)
@@ -109,6 +127,13 @@ def create_rag_app(cfg: Optional[Config] = None, index=None, llm=None, k8s=None,
             status, out = await asyncio.to_thread(dispatch_rag_tool, app.state.k8s, tool_json, citations, evidence, cfg)
         M.HTTP_LAT.labels("/agent_rag").observe(time.perf_counter() - t0)
         return respond(status, out)
+
+    @app.get("/debug/spans")
+    async def spans(since: float = 0.0):
+        """Per-span latency summary (count / mean / p50 / p99) since a time.time() stamp."""
+        from ..utils import tracing
+
+        return NetJSONResponse(tracing.summary(since))
 
     @app.get("/metrics")
     async def metrics():

@@ -14,7 +14,7 @@ import json
 import os
 from dataclasses import dataclass, field, fields
 from pathlib import Path
-from typing import Any
+from typing import Any, Optional
 
 
 @dataclass
@@ -85,11 +85,13 @@ class EngineConfig:
     dtype: str = "bfloat16"
     kv_block_size: int = 16
     gpu_memory_fraction: float = 0.85                  # of the 288 GB HBM3E
+    kv_cache_gb: Optional[float] = None                # explicit KV budget (overrides the fraction)
     max_num_seqs: int = 256
     max_num_batched_tokens: int = 65536
     max_model_len: int = 8192
     enable_prefix_caching: bool = True
     use_hip_graphs: bool = True
+    capture_graphs_at_load: bool = True                # serve: capture every decode bucket up front
     graph_batch_sizes: tuple = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)
     tp_size: int = 1
     seed: int = 0
@@ -139,6 +141,13 @@ class Config:
 
 
 def _coerce(cur: Any, val: Any) -> Any:
+    if cur is None and isinstance(val, str):  # Optional numeric knobs (e.g. engine.kv_cache_gb)
+        for t in (int, float):
+            try:
+                return t(val)
+            except ValueError:
+                pass
+        return None if val.lower() in ("", "none", "null") else val
     if isinstance(cur, bool):
         if isinstance(val, str):
             return val.strip().lower() in ("1", "true", "yes", "on")

@@ -89,6 +89,28 @@ class EmbeddingEngine:
             self._run(flat, lens, out, g0)
         return out
 
+    def embed_cpu(self, texts: list[str]) -> torch.Tensor:
+        """Host f32 [n, D] embeddings computed on this engine's own HIP stream, copied back on
+        it and synchronised there: a serving process's query embeddings do not queue behind
+        the LLM engine's pipelined steps on the default stream."""
+        if self.device.type != "cuda":
+            return self.embed(texts).float()
+        t0 = time.perf_counter()
+        with self.lock:
+            if getattr(self, "_stream", None) is None:
+                self._stream = torch.cuda.Stream(self.device)
+            with torch.cuda.stream(self._stream):
+                r = self._embed_texts(list(texts)) if texts else torch.zeros((0, self.dim), device=self.device)
+                n = r.numel()
+                if getattr(self, "_pinned", None) is None or self._pinned.numel() < n:  # grown, then reused
+                    self._pinned = torch.empty(max(n, 1 << 16), dtype=torch.float32, pin_memory=True)
+                host = self._pinned[:n].view(r.shape)
+                host.copy_(r, non_blocking=True)
+            self._stream.synchronize()
+            host = host.clone()
+        M.EMBED_LAT.observe(time.perf_counter() - t0)
+        return host
+
     def embed(self, texts: list[str]) -> torch.Tensor:
         t0 = time.perf_counter()
         with self.lock:

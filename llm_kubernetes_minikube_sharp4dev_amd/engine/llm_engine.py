@@ -242,12 +242,45 @@ class LLMEngine:
         return seqs
 
 
+class _LoopMux:
+    """Token hand-off from the engine thread to one asyncio loop: the tokens of a whole
+    engine step (one per running stream) are queued under a lock and delivered by ONE
+    ``call_soon_threadsafe`` wake-up, not one self-pipe write and loop wake-up per stream
+    per token (128 per step at the serving point)."""
+
+    def __init__(self, loop):
+        self.loop = loop
+        self.lock = threading.Lock()
+        self.pending: list = []
+        self.scheduled = False
+
+    def push(self, q, item):
+        with self.lock:
+            self.pending.append((q, item))
+            if self.scheduled:
+                return
+            self.scheduled = True
+        self.loop.call_soon_threadsafe(self._drain)
+
+    def _drain(self):
+        with self.lock:
+            items, self.pending, self.scheduled = self.pending, [], False
+        for q, it in items:
+            q.put_nowait(it)
+
+
 class AsyncLLMEngine:
     """Background step loop + asyncio streaming for the HTTP front-end."""
 
     def __init__(self, engine: LLMEngine, request_timeout_s: Optional[float] = None, stall_s: float = 120.0):
+        import sys
+
         from ..utils.watchdog import StepWatchdog
 
+        # the step loop shares the GIL with the HTTP event loop: a short switch interval lets
+        # it take the GIL back within ~0.2 ms of its GPU waits instead of the default 5 ms
+        sys.setswitchinterval(min(sys.getswitchinterval(), 2e-4))
+        self._muxes: dict = {}
         self.engine = engine
         self.request_timeout_s = request_timeout_s
         self._wake = threading.Event()
@@ -302,9 +335,12 @@ class AsyncLLMEngine:
         q: asyncio.Queue = asyncio.Queue()
         timeout_s = timeout_s if timeout_s is not None else self.request_timeout_s
         deadline = loop.time() + timeout_s if timeout_s else None
+        mux = self._muxes.get(id(loop))
+        if mux is None or mux.loop is not loop:
+            mux = self._muxes[id(loop)] = _LoopMux(loop)
 
         def cb(seq, tid, fin):
-            loop.call_soon_threadsafe(q.put_nowait, (tid, fin, seq))
+            mux.push(q, (tid, fin, seq))
 
         seq = self.engine.add_request(prompt_ids, params, req_id, cb)
         self._wake.set()

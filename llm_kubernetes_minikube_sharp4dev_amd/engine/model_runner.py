@@ -433,7 +433,9 @@ class ModelRunner:
         if self._graph_pool is None:
             self._graph_pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self._graph_pool):
+        # thread-local capture: a serving process's other threads (HTTP handlers, the
+        # embedding engine's own stream) may touch the device while a bucket is captured
+        with torch.cuda.graph(g, pool=self._graph_pool, capture_error_mode="thread_local"):
             h = self.model(st["ids"], st["meta"], self.kv_caches)
             st["logits"] = self.model.greedy(h) if greedy else self.model.logits(h)
         st["graph"] = g

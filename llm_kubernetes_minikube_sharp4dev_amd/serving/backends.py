@@ -29,7 +29,11 @@ class OllamaHTTPGenerate:
 
         self.model = model
         self.options = options
-        self.client = client or httpx.AsyncClient(base_url=base_url, timeout=timeout)
+        # no pool cap: every concurrent /agent_rag session holds one streaming /api/generate
+        # (httpx's default of 100 connections queued the 101st..128th sessions behind others)
+        self.client = client or httpx.AsyncClient(base_url=base_url, timeout=timeout,
+                                                  limits=httpx.Limits(max_connections=None,
+                                                                      max_keepalive_connections=512))
 
     async def generate(self, prompt: str) -> str:
         body = {"model": self.model, "prompt": prompt, "stream": True}
@@ -47,6 +51,15 @@ class OllamaHTTPGenerate:
                 if msg.get("error"):
                     raise GenerateError(msg["error"])
                 parts.append(msg.get("response") or "")
+                if msg.get("done") and "total_duration" in msg:
+                    # the server's own timing of this request (Ollama's done-chunk fields)
+                    from ..utils import tracing
+
+                    pe, ev, tot = (msg.get(k, 0) / 1e9 for k in ("prompt_eval_duration", "eval_duration",
+                                                                  "total_duration"))
+                    tracing.record("ollama", "prompt_eval", pe)
+                    tracing.record("ollama", "eval", ev)
+                    tracing.record("ollama", "server_total", tot)
         return "".join(parts)
 
 

@@ -103,11 +103,15 @@ class ModelManager:
             kw = dict(block_size=e.kv_block_size, max_model_len=min(e.max_model_len, model.cfg.max_position),
                       max_num_seqs=e.max_num_seqs, max_num_batched_tokens=e.max_num_batched_tokens,
                       enable_prefix_caching=e.enable_prefix_caching, use_graphs=e.use_hip_graphs,
-                      gpu_memory_fraction=e.gpu_memory_fraction, seed=e.seed)
+                      gpu_memory_fraction=e.gpu_memory_fraction, kv_cache_gb=e.kv_cache_gb, seed=e.seed)
             if self.device.type == "cpu":
                 kw["num_blocks"] = 2048
             kw.update(self.engine_overrides)
             eng = LLMEngine(model, tok, **kw)
+            if eng.runner.use_graphs and e.capture_graphs_at_load:
+                # every decode bucket (sampled-logits and greedy-ids variants) before the first
+                # request: no capture ever runs concurrently with serving traffic
+                eng.runner.capture_all(max_batch=e.max_num_seqs)
             h = GeneratorHandle(name, preset, eng, AsyncLLMEngine(eng, request_timeout_s=self.cfg.agent.request_timeout_s),
                                 tok, style,
                                 load_s=time.perf_counter() - t0)

@@ -40,8 +40,17 @@ log = get_logger("serving.ollama")
 OLLAMA_VERSION = "0.6.8"
 
 
+_now_cache = [0.0, ""]
+
+
 def _now() -> str:
-    return datetime.now(timezone.utc).isoformat().replace("+00:00", "Z")
+    """RFC 3339 timestamp of the chunk (cached for 1 ms: hundreds of streams emit a chunk per
+    engine step)."""
+    t = time.time()
+    if t - _now_cache[0] >= 1e-3:
+        _now_cache[0] = t
+        _now_cache[1] = datetime.fromtimestamp(t, timezone.utc).isoformat().replace("+00:00", "Z")
+    return _now_cache[1]
 
 
 def _chat_to_prompt(messages: list) -> tuple[Optional[str], str]:
@@ -53,6 +62,8 @@ def _chat_to_prompt(messages: list) -> tuple[Optional[str], str]:
 
 
 def create_app(manager: Optional[ModelManager] = None, cfg=None):
+    from .batcher import MicroBatcher
+
     from fastapi import FastAPI, Request
     from fastapi.responses import JSONResponse, PlainTextResponse, Response, StreamingResponse
 
@@ -182,6 +193,9 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
             d.update(stats)
             return d
 
+        from ..utils import tracing
+
+        tracing.record("server", "generate_admit", time.perf_counter() - t_req)
         r = await run_stream(h, ids, sp, chunk, final, stream)
         M.HTTP_LAT.labels("/api/generate").observe(time.perf_counter() - t_req)
         return r
@@ -222,10 +236,16 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
         return await run_stream(h, ids, sp, chunk, final, stream)
 
     # ------------------------------------------------------------------ embeddings
+    batchers: dict = {}
+
     async def _embed(model: str, texts: list[str]):
+        """Concurrent requests for one model share packed encoder passes (MicroBatcher)."""
         h = await asyncio.to_thread(mgr.embedder, model)
-        vec = await asyncio.to_thread(h.engine.embed, texts)
-        return h, vec.float().cpu().tolist()
+        b = batchers.get(h.name)
+        if b is None:
+            b = batchers[h.name] = MicroBatcher(h.engine.embed_cpu)
+        vec = await b.submit(texts) if texts else h.engine.embed_cpu(texts)
+        return h, vec.tolist()
 
     @app.post("/api/embeddings")
     async def embeddings(request: Request):
@@ -296,6 +316,12 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
                 "details": {k: d[k] for k in ("format", "family", "families", "parameter_size", "quantization_level")},
                 "model_info": {"general.architecture": d["family"], "general.parameter_count": d["params"]},
                 "capabilities": caps}
+
+    @app.get("/debug/spans")
+    async def spans(since: float = 0.0):
+        from ..utils import tracing
+
+        return JSONResponse(tracing.summary(since))
 
     @app.get("/health")
     async def health():

@@ -81,16 +81,26 @@ class Tracer:
             _export(rec)
 
 
+def record(component: str, span: str, dur_s: float, **attrs):
+    """Add an externally timed span (e.g. durations an upstream server reported)."""
+    rec = {"ts": time.time(), "component": component, "span": span, "dur_s": dur_s, **attrs}
+    with _lock:
+        _buffer.append(rec)
+    _export(rec)
+
+
 def recent(n: int = 100) -> list:
     with _lock:
         return list(_buffer)[-n:]
 
 
-def summary() -> dict:
-    """Per-span count / mean / p50 / p99 over the buffer."""
+def summary(since: float = 0.0) -> dict:
+    """Per-span count / mean / p50 / p99 over the buffer (spans that ended after ``since``,
+    a ``time.time()`` stamp)."""
     by: dict = {}
     for r in recent(len(_buffer)):
-        by.setdefault(f"{r['component']}.{r['span']}", []).append(r["dur_s"])
+        if r["ts"] >= since:
+            by.setdefault(f"{r['component']}.{r['span']}", []).append(r["dur_s"])
     out = {}
     for k, v in by.items():
         v = sorted(v)

@@ -64,3 +64,16 @@ def test_bench_refuses_forced_reference_on_gpu_device():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1"], capture_output=True,
                        text=True, timeout=120, cwd="/tmp", env=dict(os.environ, LK_FORCE_REFERENCE="1"))
     assert r.returncode != 0 and "LK_FORCE_REFERENCE" in r.stderr
+
+
+def test_http_bench_cpu_plumbing():
+    """bench.py --via-http plumbing: Ollama-compatible server + Minimal_RAG app processes,
+    /agent_rag driven over HTTP at two concurrency levels (tiny CPU models)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "http_bench.py"), "--docs", "8",
+                        "--concurrency", "1,2", "--requests", "2,4", "--model", "llama-tiny", "--embedder", "bert-tiny",
+                        "--max-new-tokens", "3"], capture_output=True, text=True, timeout=600, cwd="/tmp",
+                       env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert set(d["config"]["levels"]) == {"1", "2"} and d["value"] > 0
+    assert sum(d["config"]["levels"]["2"]["http_status_counts"].values()) == 4
