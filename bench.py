@@ -234,7 +234,7 @@ def main():
             tok, max_str=16, enums={"namespace": list(cfg.agent.allowed_namespaces) + ["default"],
                                     "name": ["echoserver", "api", "web", "worker"]})
     results, trace, elapsed, tim_setup = [], [], 0.0, 0.0
-    load, load_host = None, {}
+    load, load_host, tp_ctrl = None, {}, {}
 
     if not leader:
         # TP follower: execute the driver's steps (and its barriers) until it says stop
@@ -296,6 +296,7 @@ def main():
         sync()
         engine.step_trace = []
         load_host0 = dict(load.host_s) if load is not None else {}
+        ctrl0 = (engine.tp_ctrl.seconds, engine.tp_ctrl.messages) if args.tp > 1 else None
         prof = None
         if os.environ.get("LK_PROFILE_TIMED"):  # host-side cProfile of the timed window only
             import cProfile
@@ -316,6 +317,11 @@ def main():
             prof.disable()
             prof.dump_stats(f"{os.environ['LK_PROFILE_TIMED']}.rank{rank}")
         trace, engine.step_trace = engine.step_trace, None
+        if ctrl0 is not None:  # driver -> TP worker control hop inside the timed window
+            tp_ctrl = {"tp_ctrl_s": round(engine.tp_ctrl.seconds - ctrl0[0], 4),
+                       "tp_ctrl_us_per_msg": round((engine.tp_ctrl.seconds - ctrl0[0]) * 1e6
+                                                   / max(1, engine.tp_ctrl.messages - ctrl0[1]), 1),
+                       "tp_ctrl_transport": "shm" if engine.tp_ctrl.shm is not None else "gloo"}
         if load is not None:
             load_host = {k: v - load_host0[k] for k, v in load.host_s.items()}
             load.drain()
@@ -357,6 +363,7 @@ def main():
                     (("schedule_s", 3), ("prepare_launch_s", 4), ("sample_sync_s", 5), ("post_s", 6))}
         if load is not None:
             host.update({f"load_{k}_s": round(v, 3) for k, v in load_host.items()})
+        host.update(tp_ctrl)
         step_mix = {
             "host_breakdown": host,
             "steps": len(trace),

@@ -2,7 +2,8 @@
 
 One process per GPU.  Rank 0 owns the scheduler, the block allocator and the
 sampler; every step it broadcasts the host-side :class:`StepInputs` to the other
-ranks over a small CPU (gloo) control group, then all ranks run the same forward
+ranks over a small CPU (gloo) control group -- a fixed-layout int64 header plus one
+int32 payload, block tables trimmed to their live width (``encode_msg``) -- then all ranks run the same forward
 in lockstep — weights and KV heads sharded, two RCCL all-reduces per layer, vocab
 all-gather for the logits.  Decode hipGraphs are captured on every rank for the
 same batch buckets (RCCL calls inside the graph), so a TP decode step is one graph
@@ -17,8 +18,11 @@ replay per GPU.
 """
 from __future__ import annotations
 
+import os
+import time
 from typing import Optional
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -29,9 +33,179 @@ from .tp import TPGroup
 log = get_logger("tp")
 
 
+_CMDS = ("stop", "step", "capture", "barrier")
+# StepInputs array fields in wire order (lists travel as int32 arrays; gather = (dst, src))
+_FIELDS = ("ids", "positions", "slots", "q_lens", "ctx_lens", "tables_p", "ctx_d", "tables_d", "logits_rows",
+           "gather_dst", "gather_src")
+_NF = 5                                   # header slots per field: present, dtype, dim0, dim1, sent dim1
+_HDR = 10 + _NF * len(_FIELDS)
+
+
+def _live_width(t: np.ndarray) -> int:
+    """Columns up to the last non-zero one: block tables are zero-padded to the bucket's
+    full width (up to max_model_len / block_size); only the live part travels."""
+    if t.size == 0:
+        return 0
+    nz = np.flatnonzero(t.any(axis=0))
+    return int(nz[-1]) + 1 if nz.size else 0
+
+
+def encode_msg(cmd: str, arg=None) -> tuple[np.ndarray, np.ndarray]:
+    """(int64 header [_HDR], int32 payload) of a control message: a fixed-layout tensor
+    pair instead of a pickled object (no pickling, no per-step Python object graph)."""
+    h = np.zeros(_HDR, dtype=np.int64)
+    h[0] = _CMDS.index(cmd)
+    parts = []
+    if cmd == "capture":
+        h[7], h[8] = int(arg[0]), int(bool(arg[1]))
+    elif cmd == "step":
+        si = arg
+        h[2], h[3], h[4], h[5], h[6] = si.num_decode, si.decode_graph, int(si.greedy), si.shared_len, si.prev_bcast
+        vals = {f: getattr(si, f, None) for f in _FIELDS[:9]}
+        vals["gather_dst"], vals["gather_src"] = si.gather if si.gather is not None else (None, None)
+        for k, f in enumerate(_FIELDS):
+            v = vals[f]
+            b = 10 + _NF * k
+            if v is None:
+                continue
+            a = np.asarray(v)
+            h[b], h[b + 1] = 1, 1 if a.dtype == np.int64 else 0
+            h[b + 2] = a.shape[0] if a.ndim else 0
+            if a.ndim == 2:
+                w = _live_width(a) if f in ("tables_p", "tables_d") else a.shape[1]
+                h[b + 3], h[b + 4] = a.shape[1], w
+                a = a[:, :w]
+            parts.append(np.ascontiguousarray(a, dtype=np.int32).reshape(-1))
+    payload = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int32)
+    h[1] = payload.size
+    return h, payload
+
+
+def decode_msg(h: np.ndarray, payload: np.ndarray):
+    from ..engine.model_runner import StepInputs
+
+    cmd = _CMDS[int(h[0])]
+    if cmd == "capture":
+        return cmd, (int(h[7]), bool(h[8]))
+    if cmd != "step":
+        return cmd, None
+    out, off = {}, 0
+    for k, f in enumerate(_FIELDS):
+        b = 10 + _NF * k
+        if not h[b]:
+            out[f] = None
+            continue
+        dt = np.int64 if h[b + 1] else np.int32
+        d0, d1, w = int(h[b + 2]), int(h[b + 3]), int(h[b + 4])
+        if d1:
+            a = np.zeros((d0, d1), dtype=dt)
+            a[:, :w] = payload[off:off + d0 * w].reshape(d0, w)
+            off += d0 * w
+        else:
+            a = payload[off:off + d0].astype(dt)
+            off += d0
+        out[f] = a
+    gather = (out.pop("gather_dst"), out.pop("gather_src"))
+    si = StepInputs(ids=out["ids"], positions=out["positions"], slots=out["slots"], num_decode=int(h[2]),
+                    decode_graph=int(h[3]), q_lens=out["q_lens"].tolist() if out["q_lens"] is not None else [],
+                    ctx_lens=out["ctx_lens"].tolist() if out["ctx_lens"] is not None else [],
+                    tables_p=out["tables_p"], ctx_d=out["ctx_d"], tables_d=out["tables_d"],
+                    logits_rows=out["logits_rows"] if out["logits_rows"] is not None else np.zeros(0, np.int64),
+                    greedy=bool(h[4]), gather=gather if gather[0] is not None else None,
+                    shared_len=int(h[5]), prev_bcast=int(h[6]))
+    return cmd, si
+
+
+class _ShmChannel:
+    """Single-producer / multi-consumer message slots in POSIX shared memory for the TP
+    ranks of one node (TP never spans nodes here: one process per GPU, TP within the
+    node's xGMI mesh).  Two slots alternate; the driver writes a message's bytes, then its
+    sequence number; a worker spins on the sequence number, copies the message out and
+    acknowledges it; the driver reuses a slot only once every worker acknowledged the
+    message two back.  x86 keeps stores (and loads) in program order, so a worker that
+    sees the new sequence number sees the complete message.  Idle workers back off from
+    spinning to 50 us - 1 ms sleeps."""
+
+    SLOT = 8 << 20
+    ACKS = 64
+
+    def __init__(self, name: str, create: bool, worker_index: int = -1, n_workers: int = 0):
+        import mmap
+
+        size = 64 + 8 * self.ACKS + 2 * self.SLOT
+        self.path = os.path.join("/dev/shm", name)
+        fd = os.open(self.path, (os.O_CREAT | os.O_EXCL | os.O_RDWR) if create else os.O_RDWR, 0o600)
+        try:
+            if create:
+                os.ftruncate(fd, size)
+            self.mm = mmap.mmap(fd, size)
+        finally:
+            os.close(fd)
+        buf = self.mm
+        self.seq = np.ndarray((1,), dtype=np.uint64, buffer=buf, offset=0)
+        self.acks = np.ndarray((self.ACKS,), dtype=np.uint64, buffer=buf, offset=64)
+        self.slots = [np.ndarray((self.SLOT,), dtype=np.uint8, buffer=buf, offset=64 + 8 * self.ACKS + i * self.SLOT)
+                      for i in range(2)]
+        if create:
+            self.seq[0] = 0
+            self.acks[:] = 0
+        self.me, self.n_workers, self.next = worker_index, n_workers, 1
+        self.created = create
+
+    def send(self, h: np.ndarray, payload: np.ndarray):
+        n = int(self.seq[0]) + 1
+        nbytes = h.nbytes + payload.nbytes
+        if nbytes > self.SLOT:
+            raise ValueError(f"control message of {nbytes} B exceeds the {self.SLOT} B slot")
+        spins = 0
+        while n > 2 and int(self.acks[: self.n_workers].min()) < n - 2:  # slot still being read
+            spins += 1
+            if spins > 2000:
+                time.sleep(5e-5)
+        slot = self.slots[n & 1]
+        slot[: h.nbytes] = h.view(np.uint8)
+        slot[h.nbytes: nbytes] = payload.view(np.uint8)
+        self.seq[0] = n  # publish last
+
+    def recv(self) -> tuple[np.ndarray, np.ndarray]:
+        spins, sleep = 0, 5e-5
+        while int(self.seq[0]) < self.next:
+            spins += 1
+            if spins > 20000:
+                time.sleep(sleep)
+                sleep = min(sleep * 1.5, 1e-3)
+        slot = self.slots[self.next & 1]
+        h = slot[: _HDR * 8].view(np.int64).copy()
+        n = int(h[1])
+        payload = slot[_HDR * 8: _HDR * 8 + 4 * n].view(np.int32).copy()
+        self.acks[self.me] = self.next
+        self.next += 1
+        return h, payload
+
+    def close(self):
+        self.seq = self.acks = self.slots = None  # drop the views before unmapping
+        try:
+            self.mm.close()
+        except BufferError:
+            pass
+        if self.created:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
+
+
 class _Ctrl:
+    """Driver -> worker control channel of one TP group.  Messages are a fixed int64 header
+    plus an exact-size int32 payload (``encode_msg``).  Transport: a shared-memory slot
+    pair (``_ShmChannel``) when the group's ranks share a host, else two gloo broadcasts.
+    ``LK_TP_CTRL=gloo`` forces the broadcasts."""
+
     def __init__(self, tp: TPGroup):
         self.tp = tp
+        self.seconds = 0.0   # driver-side time spent in the control hop
+        self.messages = 0
+        self.shm = None
         if tp.size > 1 and tp.ctrl is not None:
             self.group, self.src = tp.ctrl, tp.ranks[0]
         elif tp.size > 1:
@@ -40,13 +214,76 @@ class _Ctrl:
             self.src = ranks[0]
         else:
             self.group, self.src = None, 0
+        self._h = torch.zeros(_HDR, dtype=torch.int64)
+        if tp.size > 1 and os.environ.get("LK_TP_CTRL", "shm") == "shm":
+            self._setup_shm()
 
-    def bcast(self, obj=None):
-        if self.tp.size == 1:
-            return obj
-        box = [obj]
+    def _setup_shm(self):
+        import socket
+        import uuid
+
+        box = [None, socket.gethostname()]
+        if self.tp.rank == 0:
+            import atexit
+
+            name = f"lk_tpctrl_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+            self.shm = _ShmChannel(name, True, n_workers=self.tp.size - 1)
+            box[0] = name
+            path = self.shm.path
+            atexit.register(lambda: os.path.exists(path) and os.unlink(path))  # a driver that dies
         dist.broadcast_object_list(box, src=self.src, group=self.group)
-        return box[0]
+        same = [None] * self.tp.size
+        dist.all_gather_object(same, socket.gethostname() == box[1], group=self.group)
+        if not all(same):  # ranks on another host: broadcasts
+            if self.shm is not None:
+                self.shm.close()
+                self.shm = None
+            return
+        if self.tp.rank > 0:
+            self.shm = _ShmChannel(box[0], False, worker_index=self.tp.rank - 1)
+        dist.barrier(group=self.group)  # every worker attached before the driver may unlink
+
+    def send(self, cmd: str, arg=None):
+        if self.tp.size == 1:
+            return
+        t0 = time.perf_counter()
+        h, payload = encode_msg(cmd, arg)
+        if self.shm is not None:
+            self.shm.send(h, payload)
+        else:
+            self._h.copy_(torch.from_numpy(h))
+            dist.broadcast(self._h, src=self.src, group=self.group)
+            if payload.size:
+                dist.broadcast(torch.from_numpy(payload), src=self.src, group=self.group)
+        self.seconds += time.perf_counter() - t0
+        self.messages += 1
+        if cmd == "stop":
+            self.close()
+
+    def recv(self):
+        if self.shm is not None:
+            h, payload = self.shm.recv()
+        else:
+            dist.broadcast(self._h, src=self.src, group=self.group)
+            h = self._h.numpy().copy()
+            payload = np.zeros(int(h[1]), dtype=np.int32)
+            if payload.size:
+                dist.broadcast(torch.from_numpy(payload), src=self.src, group=self.group)
+        msg = decode_msg(h, payload)
+        if msg[0] == "stop":
+            self.close()
+        return msg
+
+    def close(self):
+        if self.shm is not None:
+            # the driver unlinks only after the workers saw "stop" (their ack of it)
+            if self.shm.created:
+                n = int(self.shm.seq[0])
+                t0 = time.time()
+                while int(self.shm.acks[: self.shm.n_workers].min()) < n and time.time() - t0 < 30:
+                    time.sleep(1e-4)
+            self.shm.close()
+            self.shm = None
 
 
 def _agree_num_blocks(model, tp: TPGroup, **kw) -> int:
@@ -80,7 +317,7 @@ def make_tp_engine(model, tp: TPGroup, tokenizer=None, engine_kw: Optional[dict]
     LLMEngine.__init__(eng, model, tokenizer, block_size=runner.bs, max_model_len=runner.max_model_len,
                        max_num_seqs=runner.max_num_seqs, num_blocks=runner.num_blocks, use_graphs=runner.use_graphs,
                        _runner=runner, **ekw)
-    runner.step_hook = lambda si: ctrl.bcast(("step", si))
+    runner.step_hook = lambda si: ctrl.send("step", si)
     eng.tp_ctrl = ctrl
     return eng
 
@@ -91,12 +328,12 @@ def tp_capture_all(engine, max_batch: Optional[int] = None, variants=(False, Tru
     for B in r.graph_sizes:
         for v in variants:
             if (max_batch is None or B <= max_batch) and (B, v) not in r.graphs:
-                engine.tp_ctrl.bcast(("capture", (B, v)))
+                engine.tp_ctrl.send("capture", (B, v))
                 r.capture(B, v)
 
 
 def shutdown_tp(engine):
-    engine.tp_ctrl.bcast(("stop", None))
+    engine.tp_ctrl.send("stop")
 
 
 def tp_barrier(engine):
@@ -104,7 +341,7 @@ def tp_barrier(engine):
     run_tp_worker: they receive a "barrier" command and join the same barrier."""
     ctrl = getattr(engine, "tp_ctrl", None)
     if ctrl is not None:
-        ctrl.bcast(("barrier", None))
+        ctrl.send("barrier")
     if torch.cuda.is_available() and engine.model.device.type == "cuda":
         torch.cuda.synchronize()
     dist.barrier()
@@ -121,7 +358,7 @@ def run_tp_worker(model, tp: TPGroup, **runner_kw):
     n = 0
     pending: list = []
     while True:
-        cmd, arg = ctrl.bcast(None)  # idle wait for the driver: not a stall
+        cmd, arg = ctrl.recv()  # idle wait for the driver: not a stall
         wd.beat()
         if cmd == "stop":
             for ev in pending:

@@ -73,3 +73,40 @@ def test_xgmi_allreduce_two_processes():
         for r in range(2):
             ok = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)
             assert all(ok), f"rank {r}: {ok}"
+
+
+def _timeout_worker(rank, world, port, out_dir):
+    """Rank 1 skips the call (a dead / desynchronised peer): rank 0's kernel must give up
+    after its bounded spin, set the error word and return -- no hung device."""
+    import time
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp import TPGroup
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.xgmi_ar import XgmiAllReduce
+
+    tp = TPGroup(rank, world, dist.group.WORLD, ctrl=dist.group.WORLD, ranks=list(range(world)))
+    ar = XgmiAllReduce(tp, 1 << 20)
+    x = _vals(4096, rank).cuda()
+    ar.all_reduce_(x)  # one good call first
+    torch.cuda.synchronize()
+    res = {"first_ok": ar.error() == 0}
+    dist.barrier()
+    if rank == 0:
+        t0 = time.time()
+        ar.all_reduce_(x)  # the peer never arrives
+        torch.cuda.synchronize()
+        res.update(seconds=time.time() - t0, error=ar.error())
+    torch.save(res, os.path.join(out_dir, f"t{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_xgmi_allreduce_missing_peer_times_out_with_error():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_timeout_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        r0 = torch.load(os.path.join(d, "t0.pt"), weights_only=True)
+        r1 = torch.load(os.path.join(d, "t1.pt"), weights_only=True)
+    assert r0["first_ok"] and r1["first_ok"]
+    assert r0["error"] == 1 and r0["seconds"] < 60, r0
