@@ -81,6 +81,9 @@ def parse():
                          "(reduce-scatter / all-gather around the norms); default off")
     ap.add_argument("--token-align", type=int, default=256,
                     help="trim mixed steps' prefill chunks to a multiple of this many rows (0: off)")
+    ap.add_argument("--deferred-admission", action="store_true",
+                    help="launch retrieval without waiting on the device; admit its requests one "
+                         "engine step later (ContinuousLoad deferred=True)")
     ap.add_argument("--threaded-admission", action="store_true",
                     help="continuous mode: plan admissions on a planner thread (default: inline on the engine "
                          "thread between pipelined steps; measured 1%% faster)")
@@ -283,7 +286,7 @@ def main():
             # warm-up fills the pipeline and reaches the steady prefill/decode mix; the timed
             # window continues the same stream (in-flight requests carry over)
             load = ContinuousLoad(pipe, next_queries, params, args.batch, admit_chunk=args.admit_chunk,
-                                  threaded=args.threaded_admission)
+                                  threaded=args.threaded_admission, deferred=args.deferred_admission)
             load.run(max(args.warmup, 1) * args.batch)
         else:
             for _ in range(args.warmup):
@@ -379,7 +382,8 @@ def main():
                 (t[0] + t[1] + 255) // 256 for t in mixed).items())},
         }
         tim = {k: statistics.mean(r.timings.get(k, 0.0) for r in results if r.timings)
-               for k in ("embed_s", "knn_s", "prompt_s")} if results else {}
+               for k in ("embed_s", "knn_s", "knn_gpu_s", "prompt_s")
+               if any(r.timings and k in r.timings for r in results)} if results else {}
         steps_acct = {k: round(statistics.mean(r.timings[k] for r in results if r.timings and r.timings.get(k) is not None), 2)
                       for k in ("steps_queued", "steps_in_system", "steps_run")
                       if any(r.timings and r.timings.get(k) is not None for r in results)}
@@ -410,6 +414,8 @@ def main():
                          else f"synchronous batches of {args.batch}"),
                 "max_batched_tokens": mbt,
                 "admit_chunk": args.admit_chunk if args.mode == "continuous" else None,
+                "admission": ("threaded" if args.threaded_admission else "deferred" if args.deferred_admission
+                              else "inline") if args.mode == "continuous" else None,
                 "corpus_chunks": n,
                 "max_new_tokens": args.max_new_tokens,
                 "decoding": ("Ollama defaults (T 0.8, top-k 40, top-p 0.9, repeat penalty 1.1), ignore_eos"

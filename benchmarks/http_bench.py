@@ -60,18 +60,21 @@ def _wait(url, proc, timeout):
 
 
 async def _drive(url, queries, concurrency, n):
-    import httpx
+    """Closed-loop clients over aiohttp (httpx's pool rescans every connection per request:
+    at 128 clients the driver itself became the bottleneck)."""
+    import aiohttp
 
     lat, status = [], {}
     it = iter(range(n))
-    limits = httpx.Limits(max_connections=concurrency + 4, max_keepalive_connections=concurrency + 4)
-    async with httpx.AsyncClient(base_url=url, timeout=600.0, limits=limits) as c:
+    conn = aiohttp.TCPConnector(limit=concurrency + 4, keepalive_timeout=60.0)
+    async with aiohttp.ClientSession(connector=conn, timeout=aiohttp.ClientTimeout(total=600.0)) as c:
         async def worker():
             for i in it:
                 t0 = time.perf_counter()
-                r = await c.post("/agent_rag", json={"prompt": queries[i % len(queries)]})
+                async with c.post(url + "/agent_rag", json={"prompt": queries[i % len(queries)]}) as r:
+                    await r.read()
                 lat.append(time.perf_counter() - t0)
-                status[r.status_code] = status.get(r.status_code, 0) + 1
+                status[r.status] = status.get(r.status, 0) + 1
 
         t0 = time.perf_counter()
         await asyncio.gather(*(worker() for _ in range(concurrency)))
@@ -130,7 +133,13 @@ def main():
         for c, n in zip(levels, counts):
             since = time.time()
             cpu0 = {k: sum(p.cpu_times()[:2]) for k, p in procs.items()}
-            res[str(c)] = asyncio.run(_drive(url, queries, c, n))
+            try:
+                res[str(c)] = asyncio.run(_drive(url, queries, c, n))
+            except Exception:
+                # name which process went away (a negative code is the signal that ended it)
+                print(f"[http_bench] concurrency {c} failed: server exit={srv.poll()} "
+                      f"rag-app exit={app.poll()}", file=sys.stderr, flush=True)
+                raise
             wall = res[str(c)]["wall_s"]
             res[str(c)]["process_cpu_frac"] = {k: round((sum(p.cpu_times()[:2]) - cpu0[k]) / wall, 2)
                                                for k, p in procs.items()}

@@ -20,6 +20,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -214,7 +216,11 @@ class BpeTokenizer {
   std::vector<int> encode(const std::string& text) {
     std::vector<int> out;
     Local lc;
-    encode_into(text, out, lc);
+    {
+      py::gil_scoped_release nogil;
+      std::shared_lock<std::shared_mutex> rd(mu_);
+      encode_into(text, out, lc);
+    }
     merge_cache(lc);
     return out;
   }
@@ -225,6 +231,9 @@ class BpeTokenizer {
     std::vector<Local> locals(T);
     {
       py::gil_scoped_release nogil;
+      // several Python threads may encode at once (server event loop + engine thread):
+      // batches read the shared cache under a shared lock, merges take it exclusively
+      std::shared_lock<std::shared_mutex> rd(mu_);
       if (T == 1) {
         for (size_t i = 0; i < texts.size(); ++i) encode_into(texts[i], out[i], locals[0]);
       } else {
@@ -240,7 +249,10 @@ class BpeTokenizer {
     return out;
   }
 
-  size_t cache_size() const { return cache_.size(); }
+  size_t cache_size() {
+    std::shared_lock<std::shared_mutex> rd(mu_);
+    return cache_.size();
+  }
 
  private:
   using Local = std::unordered_map<std::string, std::vector<int>>;
@@ -263,6 +275,9 @@ class BpeTokenizer {
   }
 
   void merge_cache(Local& lc) {
+    if (lc.empty()) return;
+    py::gil_scoped_release nogil;  // a batch in another thread may hold the read lock
+    std::unique_lock<std::shared_mutex> wr(mu_);
     if (cache_.size() > (1u << 20)) cache_.clear();
     for (auto& kv : lc) cache_.emplace(std::move(kv.first), std::move(kv.second));
   }
@@ -270,7 +285,7 @@ class BpeTokenizer {
   // one pre-token (raw bytes [b, e) of text) -> ids appended to out
   void bpe_piece(const std::string& text, size_t b, size_t e, std::vector<int>& out, Local& lc) {
     const std::string raw = text.substr(b, e - b);
-    auto it = cache_.find(raw);  // read-only during a batch (writes happen after join)
+    auto it = cache_.find(raw);  // under mu_ (shared); merges happen after join, exclusively
     if (it != cache_.end()) {
       out.insert(out.end(), it->second.begin(), it->second.end());
       return;
@@ -357,6 +372,7 @@ class BpeTokenizer {
   std::vector<std::pair<std::string, int>> added_;
   bool added_first_[256] = {};
   std::unordered_map<std::string, std::vector<int>> cache_;
+  std::shared_mutex mu_;
 };
 
 }  // namespace

@@ -42,10 +42,19 @@ def _cfg(args):
     return cfg
 
 
-def _uvicorn(app, host, port):
+def _uvicorn(app, host, port, name="http"):
     import uvicorn
 
-    uvicorn.run(app, host=host, port=port, log_level="warning")
+    from .utils.pyprof import thread_profile
+
+    with thread_profile(f"loop_{name}") as dump:  # LK_PYPROFILE=<dir>: the event loop's profile
+        if getattr(app, "router", None) is not None:
+            app.router.on_shutdown.append(dump)
+        # keep-alive well past a long generation (uvicorn's 5 s default closes pooled client
+        # connections mid-burst), a deep accept queue for bursts of concurrent clients, and a
+        # bounded graceful shutdown so a SIGTERM always returns
+        uvicorn.run(app, host=host, port=port, log_level="warning", timeout_keep_alive=120,
+                    backlog=4096, timeout_graceful_shutdown=5)
 
 
 def cmd_serve(args):
@@ -59,7 +68,7 @@ def cmd_serve(args):
     for m in args.preload or []:
         kind, _ = mgr.resolve(m)
         (mgr.generator if kind == "generate" else mgr.embedder)(m)
-    _uvicorn(create_app(mgr), args.host, args.port)
+    _uvicorn(create_app(mgr), args.host, args.port, "server")
 
 
 def _serve_replicas(args):
@@ -111,10 +120,10 @@ def cmd_rag_app(args):
     emb, llm, k8s = _backends(args, cfg)
     if args.synthetic_docs:
         idx = _synthetic_index(args, emb)
-        _uvicorn(create_rag_app(cfg, idx, llm, k8s, build_index=False), args.host, args.port)
+        _uvicorn(create_rag_app(cfg, idx, llm, k8s, build_index=False), args.host, args.port, "rag_app")
         return
     idx = RagIndex(emb, backend=cfg.rag.index_backend)
-    _uvicorn(create_rag_app(cfg, idx, llm, k8s), args.host, args.port)
+    _uvicorn(create_rag_app(cfg, idx, llm, k8s), args.host, args.port, "rag_app")
 
 
 def _synthetic_index(args, query_embedder):
@@ -216,6 +225,11 @@ def cmd_router(args):
 
 
 def main(argv=None):
+    # a long-running server that dies in native code (a HIP runtime abort, a segfault in an
+    # extension thread) leaves every thread's Python stack in its log
+    import faulthandler
+
+    faulthandler.enable(all_threads=True)
     ap = argparse.ArgumentParser(prog="llm_kubernetes_minikube_sharp4dev_amd")
     sub = ap.add_subparsers(dest="cmd", required=True)
 

@@ -52,8 +52,10 @@ class RagAgentPipeline:
         self.cfg = cfg
         self.chat_style = chat_style
 
-    def plan(self, prompts: list[str]):
-        """Retrieval + gating + prompt construction for a batch of user prompts."""
+    def plan_launch(self, prompts: list[str]) -> dict:
+        """Enqueue retrieval for a batch of user prompts without waiting on the device: the
+        query encoder and the kNN kernel run on the current stream, the top-k lands in
+        pinned memory behind an event (:meth:`RagIndex.search_vectors_async`)."""
         t0 = time.perf_counter()
         r = self.cfg.rag
         embedder = self.index.embedder
@@ -62,11 +64,27 @@ class RagAgentPipeline:
         else:
             qv = embedder.embed(prompts)
         t1 = time.perf_counter()
-        res = self.index.search_vectors(qv, r.agent_topk)
-        t2 = time.perf_counter()
+        ev0 = ev1 = None
+        if isinstance(qv, torch.Tensor) and qv.is_cuda:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        pending = self.index.search_vectors_async(qv, r.agent_topk)
+        if ev1 is not None:
+            ev1.record()
+        return {"prompts": prompts, "pending": pending, "t": (t0, t1, time.perf_counter()), "ev": (ev0, ev1)}
+
+    def plan_ready(self, h: dict) -> bool:
+        return h["pending"].ready()
+
+    def plan_finish(self, h: dict):
+        """Gating + prompt construction once the launched search has landed."""
+        t0, t1, t2 = h["t"]
+        res = h["pending"].result()
+        t2w = time.perf_counter()
+        r = self.cfg.rag
         plans = []
         texts = []
-        for p, rr in zip(prompts, res):
+        for p, rr in zip(h["prompts"], res):
             hits = self.index.hits(rr)
             if not hits:
                 plans.append((p, None, [], []))
@@ -80,12 +98,28 @@ class RagAgentPipeline:
         for p, full, cit, ev in plans:
             out.append((p, next(ids) if full is not None else None, cit, ev))
         t3 = time.perf_counter()
-        return out, {"embed_s": t1 - t0, "knn_s": t2 - t1, "prompt_s": t3 - t2}
+        # embed_s / knn_s: host time blocked in each stage (launch, plus the wait for the
+        # top-k); knn_gpu_s: the kNN's device time in situ (event to event on its stream,
+        # including any wait for CUs held by a concurrent engine step)
+        tim = {"embed_s": t1 - t0, "knn_s": (t2 - t1) + h["pending"].wait_s,
+               "prompt_s": t3 - t2w}
+        ev0, ev1 = h["ev"]
+        if ev0 is not None:
+            ev1.synchronize()
+            tim["knn_gpu_s"] = ev0.elapsed_time(ev1) / 1e3
+        return out, tim
+
+    def plan(self, prompts: list[str]):
+        """Retrieval + gating + prompt construction for a batch of user prompts."""
+        return self.plan_finish(self.plan_launch(prompts))
 
     # ---- request-level interface used by ContinuousLoad (shared with AgentPipeline)
     def plan_requests(self, prompts: list[str]):
         """[(prompt, token ids or None (no evidence -> answered without the LLM), ctx)], timings"""
-        plans, tim = self.plan(prompts)
+        return self.requests_of(*self.plan(prompts))
+
+    @staticmethod
+    def requests_of(plans, tim):
         return [(p, ids, (cit, ev)) for p, ids, cit, ev in plans], tim
 
     def finish_request(self, prompt: str, out_ids: list, ctx) -> RagAgentResult:
@@ -149,12 +183,17 @@ class ContinuousLoad:
     hand-offs cost the engine thread more than the overlap gains."""
 
     def __init__(self, pipe: RagAgentPipeline, next_queries, params, concurrency: int, admit_chunk: int = 16,
-                 threaded: bool = False):
+                 threaded: bool = False, deferred: Optional[bool] = None):
         self.pipe, self.next_queries, self.params = pipe, next_queries, params
         self.concurrency, self.admit_chunk = concurrency, admit_chunk
         self.inflight: dict = {}
         self.host_s = {"plan": 0.0, "step": 0.0, "finish": 0.0}  # wall time by phase
         self.threaded = threaded
+        # deferred=True: retrieval is launched without waiting; its requests are admitted at
+        # the first loop iteration after its top-k landed (no host block on the device, one
+        # engine step later than a blocking plan).  LK_ADMIT_DEFERRED=1 selects it.
+        self.deferred = (os.environ.get("LK_ADMIT_DEFERRED", "0") == "1") if deferred is None else deferred
+        self._launched: list = []  # (t_adm, plan handle) in launch order
         self._todo: "queue.Queue" = queue.Queue()
         self._ready: "queue.Queue" = queue.Queue()
         self._planning = 0  # queries submitted to the planner and not yet admitted
@@ -162,20 +201,45 @@ class ContinuousLoad:
         self._error = None
 
     # ---- planner
-    def _plan(self, qs):
+    def _side_stream(self):
         dev = getattr(getattr(self.pipe.llm, "model", None), "device", None)
+        if dev is None or dev.type != "cuda":
+            return None
+        if getattr(self, "_side", None) is None:
+            # stream priority knob for the retrieval kernels: a high-priority stream
+            # (-1) measured slower on MI355X (98.7 vs 100.8 q/s, kNN 10.4 vs 5.5 ms)
+            prio = int(os.environ.get("LK_ADMIT_STREAM_PRIORITY", "0"))
+            self._side = torch.cuda.Stream(dev, priority=prio)
+        return self._side
+
+    def _plan(self, qs):
+        side = self._side_stream()
         t_adm = time.perf_counter()
-        if dev is not None and dev.type == "cuda":
-            if getattr(self, "_side", None) is None:
-                # stream priority knob for the retrieval kernels: a high-priority stream
-                # (-1) measured slower on MI355X (98.7 vs 100.8 q/s, kNN 10.4 vs 5.5 ms)
-                prio = int(os.environ.get("LK_ADMIT_STREAM_PRIORITY", "0"))
-                self._side = torch.cuda.Stream(dev, priority=prio)
-            with torch.cuda.stream(self._side):
+        if side is not None:
+            with torch.cuda.stream(side):
                 reqs, tim = self.pipe.plan_requests(qs)
         else:
             reqs, tim = self.pipe.plan_requests(qs)
         return t_adm, time.perf_counter() - t_adm, reqs, tim
+
+    def _launch_plan(self, qs):
+        side = self._side_stream()
+        t_adm = time.perf_counter()
+        if side is not None:
+            with torch.cuda.stream(side):
+                h = self.pipe.plan_launch(qs)
+        else:
+            h = self.pipe.plan_launch(qs)
+        self.host_s["plan"] += time.perf_counter() - t_adm
+        self._launched.append((t_adm, h))
+
+    def _finish_launched(self, block: bool):
+        """Plans whose top-k landed (all of them when ``block``), in launch order."""
+        while self._launched and (block or self.pipe.plan_ready(self._launched[0][1])):
+            t_adm, h = self._launched.pop(0)
+            t0 = time.perf_counter()
+            reqs, tim = self.pipe.requests_of(*self.pipe.plan_finish(h))
+            self._ready.put((t_adm, time.perf_counter() - t0, reqs, tim))
 
     def _planner(self):
         while True:
@@ -190,6 +254,9 @@ class ContinuousLoad:
 
     def _submit(self, qs):
         self._planning += len(qs)
+        if self.deferred and not self.threaded:
+            self._launch_plan(qs)
+            return
         if not self.threaded:
             self._ready.put(self._plan(qs))
             return
@@ -199,6 +266,8 @@ class ContinuousLoad:
         self._todo.put(qs)
 
     def _admit_ready(self, done, block: bool):
+        if self._launched:
+            self._finish_launched(block)
         while True:
             try:
                 item = self._ready.get(block=block)
@@ -268,6 +337,7 @@ class ContinuousLoad:
             self._thread = None
         while not self._ready.empty():
             self._ready.get()
+        self._launched.clear()
         self._planning = 0
         for seq, *_ in self.inflight.values():
             self.pipe.llm.abort(seq.req_id)

@@ -90,15 +90,17 @@ class EmbeddingEngine:
         return out
 
     def embed_cpu(self, texts: list[str]) -> torch.Tensor:
-        """Host f32 [n, D] embeddings computed on this engine's own HIP stream, copied back on
-        it and synchronised there: a serving process's query embeddings do not queue behind
-        the LLM engine's pipelined steps on the default stream."""
+        """Host f32 [n, D] embeddings computed on this engine's own high-priority HIP stream,
+        copied back on it and synchronised there: a serving process's query embeddings do not
+        queue behind the LLM engine's pipelined steps."""
         if self.device.type != "cuda":
             return self.embed(texts).float()
         t0 = time.perf_counter()
         with self.lock:
             if getattr(self, "_stream", None) is None:
-                self._stream = torch.cuda.Stream(self.device)
+                # high priority: a query embedding (a few ms of small kernels) is dispatched
+                # ahead of the queued kernels of the LLM engine's step instead of behind them
+                self._stream = torch.cuda.Stream(self.device, priority=-1)
             with torch.cuda.stream(self._stream):
                 r = self._embed_texts(list(texts)) if texts else torch.zeros((0, self.dim), device=self.device)
                 n = r.numel()

@@ -5,6 +5,7 @@ for the HTTP server (one engine per GPU / TP group; DP replicas are routed by
 from __future__ import annotations
 
 import asyncio
+import collections
 import threading
 import time
 from typing import Callable, Optional
@@ -45,6 +46,10 @@ class LLMEngine:
             eos_ids = set(tokenizer.eos_ids) if tokenizer is not None else set(model.cfg.eos_token_ids)
         self.eos_ids = set(eos_ids)
         self.lock = threading.RLock()
+        # new requests land here without the engine lock (the lock is held across a step's
+        # device wait: an HTTP event loop admitting a request must not stall behind it);
+        # the step loop moves them into the scheduler at its next launch
+        self._inbox: collections.deque = collections.deque()
         self.steps = 0
         self.launches = 0
         self._inflight = None  # the launched-and-sampled step not yet collected (step_pipelined)
@@ -64,17 +69,22 @@ class LLMEngine:
         if budget <= 0:
             raise ValueError("prompt longer than max_model_len")
         params.max_tokens = min(params.max_tokens, budget)
-        with self.lock:
-            self.scheduler.add(seq)
+        self._inbox.append(seq)  # deque.append is atomic: no lock on the caller's thread
         M.REQUESTS.inc()
         return seq
 
+    def _drain_inbox(self):
+        """Move newly added requests into the scheduler (caller holds ``self.lock``)."""
+        while self._inbox:
+            self.scheduler.add(self._inbox.popleft())
+
     def abort(self, req_id: str) -> bool:
         with self.lock:
+            self._drain_inbox()
             return self.scheduler.abort(req_id)
 
     def has_work(self) -> bool:
-        return self.scheduler.has_work()
+        return bool(self._inbox) or self.scheduler.has_work()
 
     # ------------------------------------------------------------------ step
     # A step is three phases: _launch (schedule, build the inputs, enqueue the forward),
@@ -123,6 +133,7 @@ class LLMEngine:
     def _launch(self):
         with self.lock:
             ts = time.perf_counter()
+            self._drain_inbox()
             batch = self.scheduler.schedule()
             # requests that could never fit were finished by the scheduler
             if batch.empty:
@@ -166,12 +177,12 @@ class LLMEngine:
 
     def _collect(self, pending) -> list:
         batch, rows, host, ev, ts, t0, t1, t1s, ev0 = pending
+        t2 = time.perf_counter()
+        if rows and ev is not None:
+            ev.synchronize()  # outside the lock: aborts and admissions never wait on the device
         with self.lock:
             out = []
-            t2 = time.perf_counter()
             if rows:
-                if ev is not None:
-                    ev.synchronize()
                 ids = host.tolist()
                 now = t2 = time.perf_counter()
                 for (seq, _), tid in zip(rows, ids):
@@ -296,6 +307,7 @@ class AsyncLLMEngine:
     def _fail_all(self, why: str):
         """Finish every in-flight request with an error token (-1) so no client hangs."""
         with self.engine.lock:
+            self.engine._drain_inbox()
             for s in list(self.engine.scheduler.running) + list(self.engine.scheduler.waiting):
                 self.engine.scheduler.abort(s.req_id)
                 s.error = why
@@ -303,6 +315,12 @@ class AsyncLLMEngine:
                     s.on_token(s, -1, True)
 
     def _loop(self):
+        from ..utils.pyprof import thread_profile
+
+        with thread_profile("engine"):
+            self._loop_body()
+
+    def _loop_body(self):
         while not self._stop:
             if not self.engine.has_work():
                 if self.engine._inflight is not None:
@@ -324,6 +342,8 @@ class AsyncLLMEngine:
         self._stop = True
         self._wake.set()
         self.watchdog.stop()
+        if self._thread.is_alive() and self._thread is not threading.current_thread():
+            self._thread.join(timeout=10)
 
     async def stream(self, prompt_ids: list, params: SamplingParams, req_id: Optional[str] = None,
                      timeout_s: Optional[float] = None):

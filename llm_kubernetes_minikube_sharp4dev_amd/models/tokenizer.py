@@ -99,14 +99,10 @@ class Tokenizer:
         self.cls_id = v.get("[CLS]", self.bos_id)
         self.sep_id = v.get("[SEP]", self.eot_id)
         self._piece_cache: Optional[list] = None
-        # the native encoder merges its word cache after each call (GIL released inside):
-        # serialise callers (admission planner thread vs request threads)
-        self._native_lock = threading.Lock()
 
     def encode(self, text: str, add_bos: bool = False) -> list[int]:
         if self.native is not None:
-            with self._native_lock:
-                ids = self.native.encode(text)
+            ids = self.native.encode(text)  # thread-safe: its word cache sits behind a shared mutex
         else:
             ids = self.tok.encode(text, add_special_tokens=False).ids
         return ([self.bos_id] + ids) if add_bos else ids
@@ -114,8 +110,7 @@ class Tokenizer:
     def encode_batch(self, texts: Iterable[str]) -> list[list[int]]:
         texts = list(texts)
         if self.native is not None:
-            with self._native_lock:
-                return self.native.encode_batch(texts, min(8, max(1, len(texts) // 4)))
+            return self.native.encode_batch(texts, min(8, max(1, len(texts) // 4)))
         return [e.ids for e in self.tok.encode_batch(texts, add_special_tokens=False)]
 
     def encode_for_embedding(self, texts: list[str], max_len: int = 512) -> list[list[int]]:

@@ -58,26 +58,26 @@ class OllamaEmbedder:
 
     async def aembed_one(self, text: str) -> np.ndarray:
         """Async twin of :meth:`embed_one` for an event-loop front-end (same payload order,
-        one pooled connection per concurrent request, no worker thread)."""
-        import httpx
+        one pooled aiohttp connection per concurrent request, no worker thread)."""
+        from ..serving.backends import AioSession
 
         if self._aclient is None:
-            self._aclient = httpx.AsyncClient(base_url=self.base_url, timeout=self.timeout,
-                                              limits=httpx.Limits(max_connections=None, max_keepalive_connections=512))
+            self._aclient = AioSession(self.base_url, self.timeout)
+        sess = self._aclient.get()
         for payload in ({"model": self.model, "input": text},
                         {"model": self.model, "input": [text]},
                         {"model": self.model, "prompt": text}):
             self.attempts += 1
-            r = await self._aclient.post("/api/embeddings",
-                                         content=json.dumps(payload, ensure_ascii=False).encode("utf-8"),
-                                         headers={"Content-Type": "application/json; charset=utf-8"})
-            if 200 <= r.status_code < 300:
-                try:
-                    e = parse_embedding_response(r.json())
-                except ValueError:
-                    e = None
-                if e:
-                    return np.asarray(e, dtype=np.float32)
+            async with sess.post(self._aclient.url("/api/embeddings"),
+                                 data=json.dumps(payload, ensure_ascii=False).encode("utf-8"),
+                                 headers={"Content-Type": "application/json; charset=utf-8"}) as r:
+                if 200 <= r.status < 300:
+                    try:
+                        e = parse_embedding_response(json.loads(await r.read()))
+                    except ValueError:
+                        e = None
+                    if e:
+                        return np.asarray(e, dtype=np.float32)
         raise EmbeddingError(self.MESSAGE)
 
     def _try(self, payload: dict) -> Optional[list]:

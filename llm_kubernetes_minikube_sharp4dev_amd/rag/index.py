@@ -33,6 +33,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..utils import metrics as M
 from ..utils.logging import get_logger
 from .chunking import chunk_document, chunk_sliding, is_blank, sanitize, split_by_markdown_headers
 
@@ -160,6 +161,30 @@ class RagIndex:
         """Attach a corpus matrix produced directly on the GPU (bulk index builds)."""
         self._gpu = (corpus_bf16.contiguous(), norms if norms is not None else ops.row_norms(corpus_bf16))
 
+    def search_vectors_async(self, q: np.ndarray | torch.Tensor, top_k: int) -> "PendingSearch":
+        """Launch a batched search without blocking the host: on the GPU the kNN kernel and
+        one non-blocking copy of its (scores, ids) into pinned memory are enqueued on the
+        current stream behind an event; :meth:`PendingSearch.result` waits for that event
+        only (an engine thread collects it after its next step, when it has long completed).
+        Elsewhere the search runs synchronously."""
+        k = max(1, top_k)
+        n = len(self.chunks)
+        if n == 0 or not self._use_gpu():
+            return PendingSearch(done=self.search_vectors(q, top_k) if n else [[] for _ in range(len(q))])
+        corpus, norms = self.gpu_tensors()
+        qt = torch.as_tensor(q).to(self.device, torch.bfloat16).reshape(-1, corpus.shape[1]).contiguous()
+        qn = ops.row_norms(qt) if qt.is_cuda else qt.float().norm(dim=-1)
+        s, i = ops.knn_topk(corpus, norms, qt, qn, min(k, 64))
+        if not s.is_cuda:
+            return PendingSearch(done=_rows(s.tolist(), i.tolist(), min(k, n)))
+        hs = torch.empty(s.shape, dtype=s.dtype, pin_memory=True)
+        hi = torch.empty(i.shape, dtype=i.dtype, pin_memory=True)
+        hs.copy_(s, non_blocking=True)
+        hi.copy_(i, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return PendingSearch(host=(hs, hi, min(k, n)), event=ev)
+
     def search_vectors(self, q: np.ndarray | torch.Tensor, top_k: int) -> list[list[tuple[int, float]]]:
         """Batched: q [nq, D] -> per query [(chunk_index, score)] (stable order)."""
         k = max(1, top_k)
@@ -167,12 +192,7 @@ class RagIndex:
         if n == 0:
             return [[] for _ in range(len(q))]
         if self._use_gpu():
-            corpus, norms = self.gpu_tensors()
-            qt = torch.as_tensor(q).to(self.device, torch.bfloat16).reshape(-1, corpus.shape[1]).contiguous()
-            qn = ops.row_norms(qt) if qt.is_cuda else qt.float().norm(dim=-1)
-            s, i = ops.knn_topk(corpus, norms, qt, qn, min(k, 64))
-            s, i = s.cpu().tolist(), i.cpu().tolist()
-            return [[(ii, ss) for ss, ii in zip(sr, ir) if ii >= 0][: min(k, n)] for sr, ir in zip(s, i)]
+            return self.search_vectors_async(q, top_k).result()
         mat = self.matrix()
         qa = np.asarray(q.float().cpu().numpy() if isinstance(q, torch.Tensor) else q, dtype=np.float32)
         if qa.ndim == 1:
@@ -267,3 +287,30 @@ class RagIndex:
 
 __all__ = ["RagIndex", "RagChunk", "RagHit", "cosine_exact", "enumerate_files", "split_by_markdown_headers",
            "chunk_sliding", "sanitize", "is_blank"]
+
+
+def _rows(s, i, k):
+    return [[(ii, ss) for ss, ii in zip(sr, ir) if ii >= 0][:k] for sr, ir in zip(s, i)]
+
+
+class PendingSearch:
+    """A launched :meth:`RagIndex.search_vectors_async`: ``ready()`` polls its event,
+    ``result()`` waits for it (not for the device) and decodes the rows once."""
+
+    def __init__(self, host=None, event=None, done=None):
+        self._host, self._event, self._done = host, event, done
+        self.wait_s = 0.0  # host time spent blocked in result()
+
+    def ready(self) -> bool:
+        return self._done is not None or self._event is None or self._event.query()
+
+    def result(self) -> list:
+        if self._done is None:
+            t0 = time.perf_counter()
+            if self._event is not None:
+                self._event.synchronize()
+            self.wait_s = time.perf_counter() - t0
+            hs, hi, k = self._host
+            self._done = _rows(hs.tolist(), hi.tolist(), k)
+            M.KNN_LAT.observe(self.wait_s)
+        return self._done

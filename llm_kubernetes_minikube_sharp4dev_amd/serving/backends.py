@@ -22,44 +22,83 @@ class GenerateError(RuntimeError):
     pass
 
 
+class AioSession:
+    """One aiohttp session per event loop for a front-end's calls to the model server.
+
+    httpx/httpcore rescans its whole pool for every request (``_assign_requests_to_
+    connections``): at 128 concurrent sessions -- 128 streaming generates plus 128 embeds
+    in flight -- that scan was the RAG app's largest CPU cost (24 M ``is_idle`` calls in
+    16 s, measured with LK_PYPROFILE).  aiohttp's connector keeps idle connections in a
+    per-host deque.  No connection cap (every concurrent session holds one stream)."""
+
+    def __init__(self, base_url: str, timeout: float):
+        self.base_url = base_url.rstrip("/")
+        self.timeout = timeout
+        self._loop = self._session = None
+
+    def get(self):
+        import aiohttp
+
+        loop = asyncio.get_running_loop()
+        if self._session is None or self._loop is not loop or self._session.closed:
+            self._loop = loop
+            self._session = aiohttp.ClientSession(
+                connector=aiohttp.TCPConnector(limit=0, keepalive_timeout=60.0),
+                timeout=aiohttp.ClientTimeout(total=self.timeout))
+        return self._session
+
+    def url(self, path: str) -> str:
+        return self.base_url + path
+
+
 class OllamaHTTPGenerate:
     def __init__(self, base_url: str = "http://127.0.0.1:11434", model: str = "llama3.1:8b", client=None,
                  timeout: float = 300.0, options: Optional[dict] = None):
-        import httpx
-
         self.model = model
         self.options = options
-        # no pool cap: every concurrent /agent_rag session holds one streaming /api/generate
-        # (httpx's default of 100 connections queued the 101st..128th sessions behind others)
-        self.client = client or httpx.AsyncClient(base_url=base_url, timeout=timeout,
-                                                  limits=httpx.Limits(max_connections=None,
-                                                                      max_keepalive_connections=512))
+        # ``client``: an httpx.AsyncClient (tests drive the ASGI app in-process through one);
+        # otherwise aiohttp to the server
+        self.client = client
+        self.aio = AioSession(base_url, timeout) if client is None else None
+
+    def _done_chunk(self, msg: dict):
+        if msg.get("done") and "total_duration" in msg:
+            # the server's own timing of this request (Ollama's done-chunk fields)
+            from ..utils import tracing
+
+            pe, ev, tot = (msg.get(k, 0) / 1e9 for k in ("prompt_eval_duration", "eval_duration", "total_duration"))
+            tracing.record("ollama", "prompt_eval", pe)
+            tracing.record("ollama", "eval", ev)
+            tracing.record("ollama", "server_total", tot)
+
+    def _line(self, line, parts: list):
+        if not line.strip():
+            return
+        msg = json.loads(line)
+        if msg.get("error"):
+            raise GenerateError(msg["error"])
+        parts.append(msg.get("response") or "")
+        self._done_chunk(msg)
 
     async def generate(self, prompt: str) -> str:
         body = {"model": self.model, "prompt": prompt, "stream": True}
         if self.options:
             body["options"] = self.options
-        parts = []
+        parts: list = []
+        if self.aio is not None:
+            async with self.aio.get().post(self.aio.url("/api/generate"), json=body) as r:
+                if r.status >= 300:
+                    text = (await r.read()).decode("utf-8", "replace")
+                    raise GenerateError(f"Ollama /api/generate returned {r.status}: {text}")
+                async for line in r.content:  # NDJSON: one chunk per line
+                    self._line(line, parts)
+            return "".join(parts)
         async with self.client.stream("POST", "/api/generate", json=body) as r:
             if r.status_code >= 300:
                 text = (await r.aread()).decode("utf-8", "replace")
                 raise GenerateError(f"Ollama /api/generate returned {r.status_code}: {text}")
             async for line in r.aiter_lines():
-                if not line.strip():
-                    continue
-                msg = json.loads(line)
-                if msg.get("error"):
-                    raise GenerateError(msg["error"])
-                parts.append(msg.get("response") or "")
-                if msg.get("done") and "total_duration" in msg:
-                    # the server's own timing of this request (Ollama's done-chunk fields)
-                    from ..utils import tracing
-
-                    pe, ev, tot = (msg.get(k, 0) / 1e9 for k in ("prompt_eval_duration", "eval_duration",
-                                                                  "total_duration"))
-                    tracing.record("ollama", "prompt_eval", pe)
-                    tracing.record("ollama", "eval", ev)
-                    tracing.record("ollama", "server_total", tot)
+                self._line(line, parts)
         return "".join(parts)
 
 

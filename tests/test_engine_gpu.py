@@ -46,6 +46,7 @@ def test_llama_gpu_logits_match_hf_fp32():
     eng = _engine(m, use_graphs=False)
     for p in PROMPTS:
         eng.add_request(p, SamplingParams.greedy(1))
+    eng._drain_inbox()
     batch = eng.scheduler.schedule()
     rows, lg = eng.runner.forward_logits(batch.items)
     for (seq, _), got in zip(rows, lg):

@@ -41,6 +41,7 @@ def test_llama_matches_hf():
     # logits of the first step
     eng2 = _engine(m)
     s2 = eng2.add_request(prompt, SamplingParams.greedy(1))
+    eng2._drain_inbox()
     batch = eng2.scheduler.schedule()
     rows, lg = eng2.runner.forward_logits(batch.items)
     assert torch.allclose(lg[0], hf_logits, atol=1e-4, rtol=1e-4)

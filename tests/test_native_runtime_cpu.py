@@ -117,6 +117,39 @@ def test_native_bpe_matches_hf_builtin(native):
     assert [enc.encode(t) for t in texts[:200]] == ref[:200]
 
 
+def test_native_bpe_concurrent_callers(native):
+    """Several Python threads encoding through ONE encoder at once (a server's event loop,
+    its engine thread and the embedding batcher): the shared word cache is read under a
+    shared lock and merged exclusively, so every thread gets the serial result."""
+    import threading
+
+    from llm_kubernetes_minikube_sharp4dev_amd.models.tokenizer import builtin_tokenizer, native_encoder
+
+    hf = builtin_tokenizer().tok
+    enc = native_encoder(hf)
+    texts = _corpus_texts() + _adversarial_texts()
+    ref = [e.ids for e in hf.encode_batch(texts, add_special_tokens=False)]
+    errs = []
+
+    def work(t):
+        try:
+            for r in range(6):
+                part = texts[(t * 37 + r * 11) % len(texts):][:64]
+                exp = ref[(t * 37 + r * 11) % len(texts):][:64]
+                got = enc.encode_batch(part, 2) if (t + r) % 2 else [enc.encode(x) for x in part]
+                if got != exp:
+                    errs.append((t, r))
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs[:3]
+
+
 def test_native_bpe_matches_hf_llama3_pretokenizer(native):
     """Llama-3 layout: Split(llama-3 regex, isolated) + ByteLevel(no regex), ignore_merges."""
     from tokenizers import Regex, Tokenizer, decoders, models, pre_tokenizers, trainers
