@@ -193,6 +193,7 @@ class ContinuousLoad:
         # the first loop iteration after its top-k landed (no host block on the device, one
         # engine step later than a blocking plan).  LK_ADMIT_DEFERRED=1 selects it.
         self.deferred = (os.environ.get("LK_ADMIT_DEFERRED", "0") == "1") if deferred is None else deferred
+        self.deferred = self.deferred and hasattr(pipe, "plan_launch")  # pipelines without retrieval: inline
         self._launched: list = []  # (t_adm, plan handle) in launch order
         self._todo: "queue.Queue" = queue.Queue()
         self._ready: "queue.Queue" = queue.Queue()

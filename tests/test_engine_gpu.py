@@ -179,10 +179,14 @@ def test_rag_pipeline_on_gpu_index():
         counter[0] += 1
         return make_queries(k, seed=counter[0])
 
-    load = ContinuousLoad(pipe, nq, SamplingParams.greedy(6, ignore_eos=True), concurrency=6, admit_chunk=3)
-    out = load.run(12)
-    load.drain()
-    assert len(out) >= 12 and all(r.status in (200, 400, 404, 500) for r in out)
+    for deferred in (False, True):
+        load = ContinuousLoad(pipe, nq, SamplingParams.greedy(6, ignore_eos=True), concurrency=6, admit_chunk=3,
+                              deferred=deferred)
+        out = load.run(12)
+        load.drain()
+        assert len(out) >= 12 and all(r.status in (200, 400, 404, 500) for r in out)
+        # the kNN's device time was measured in situ (events on the side stream)
+        assert all("knn_gpu_s" in r.timings for r in out if r.timings)
 
 
 def test_forced_reference_fails_loudly_not_silently():

@@ -273,10 +273,10 @@ def _tiny_stack():
     return tok, idx, eng, FakeCluster.default(), Config()
 
 
-@pytest.mark.parametrize("threaded", [False, True])
-def test_continuous_load_rag_agent_mixed(threaded):
+@pytest.mark.parametrize("mode", ["inline", "threaded", "deferred"])
+def test_continuous_load_rag_agent_mixed(mode):
     """Closed-loop continuous batching over the three workloads of bench.py (configs 2/3/5),
-    admission planned inline or on the planner thread."""
+    admission planned inline, on the planner thread, or launched and admitted once landed."""
     from llm_kubernetes_minikube_sharp4dev_amd.agent.agent_pipeline import AgentPipeline, MixedPipeline
     from llm_kubernetes_minikube_sharp4dev_amd.agent.rag_pipeline import ContinuousLoad, RagAgentPipeline
     from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import SamplingParams
@@ -293,7 +293,8 @@ def test_continuous_load_rag_agent_mixed(threaded):
 
     params = SamplingParams.greedy(4, ignore_eos=True)
     for pipe in (rag, agent, MixedPipeline(rag, agent)):
-        load = ContinuousLoad(pipe, nq, params, concurrency=4, admit_chunk=2, threaded=threaded)
+        load = ContinuousLoad(pipe, nq, params, concurrency=4, admit_chunk=2, threaded=mode == "threaded",
+                              deferred=mode == "deferred")
         out = load.run(6)
         out += load.run(3)  # continues the same stream
         load.drain()
