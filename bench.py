@@ -238,7 +238,7 @@ def main():
             tok, max_str=16, enums={"namespace": list(cfg.agent.allowed_namespaces) + ["default"],
                                     "name": ["echoserver", "api", "web", "worker"]})
     results, trace, elapsed, tim_setup = [], [], 0.0, 0.0
-    load, load_host, tp_ctrl = None, {}, {}
+    load, load_host, tp_ctrl, prompt_len = None, {}, {}, {}
 
     if not leader:
         # TP follower: execute the driver's steps (and its barriers) until it says stop
@@ -301,6 +301,7 @@ def main():
         sync()
         engine.step_trace = []
         load_host0 = dict(load.host_s) if load is not None else {}
+        chars0 = (rag.planned_chars, rag.planned_tokens, rag.planned_requests, rag.planned_evidence)
         ctrl0 = (engine.tp_ctrl.seconds, engine.tp_ctrl.messages) if args.tp > 1 else None
         prof = None
         if os.environ.get("LK_PROFILE_TIMED"):  # host-side cProfile of the timed window only
@@ -327,6 +328,11 @@ def main():
                        "tp_ctrl_us_per_msg": round((engine.tp_ctrl.seconds - ctrl0[0]) * 1e6
                                                    / max(1, engine.tp_ctrl.messages - ctrl0[1]), 1),
                        "tp_ctrl_transport": "shm" if engine.tp_ctrl.shm is not None else "gloo"}
+        dc, dt, dn, de = (a - b for a, b in zip(
+            (rag.planned_chars, rag.planned_tokens, rag.planned_requests, rag.planned_evidence), chars0))
+        if dn:  # RAG prompts planned inside the timed window
+            prompt_len = {"prompt_chars": round(dc / dn, 1), "prompt_tokens": round(dt / dn, 1),
+                          "chars_per_token": round(dc / dt, 3), "evidence_chunks": round(de / dn, 2)}
         if load is not None:
             load_host = {k: v - load_host0[k] for k, v in load.host_s.items()}
             load.drain()
@@ -410,6 +416,9 @@ def main():
                 "workload": args.workload,
                 "global_batch": args.batch * n_replicas,
                 "seq_len": round(avg_prompt, 1),
+                # RAG prompt bodies planned in the timed window: characters, tokens (chat template
+                # included) and their ratio under the built-in tokenizer (models/tokenizer.py)
+                **prompt_len,
                 "parallelism": par,
                 "load": (f"continuous batching, closed loop, {args.batch} requests in flight per replica, "
                          f"step = {args.batch} completions per replica" if args.mode == "continuous"

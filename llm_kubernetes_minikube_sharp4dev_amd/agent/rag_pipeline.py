@@ -51,6 +51,12 @@ class RagAgentPipeline:
         self.k8s = k8s
         self.cfg = cfg
         self.chat_style = chat_style
+        # running totals over planned LLM requests: prompt-body characters and prompt tokens
+        # (chat template included) -- bench.py reports their ratio as chars_per_token
+        self.planned_chars = 0
+        self.planned_tokens = 0
+        self.planned_requests = 0
+        self.planned_evidence = 0  # evidence chunks that passed the citation gate
 
     def plan_launch(self, prompts: list[str]) -> dict:
         """Enqueue retrieval for a batch of user prompts without waiting on the device: the
@@ -96,7 +102,13 @@ class RagAgentPipeline:
         ids = iter(self.tok.chat_prompt_batch(texts, style=self.chat_style)) if texts else iter(())
         out = []
         for p, full, cit, ev in plans:
-            out.append((p, next(ids) if full is not None else None, cit, ev))
+            pid = next(ids) if full is not None else None
+            if pid is not None:
+                self.planned_chars += len(full)
+                self.planned_tokens += len(pid)
+                self.planned_requests += 1
+                self.planned_evidence += len(ev)
+            out.append((p, pid, cit, ev))
         t3 = time.perf_counter()
         # embed_s / knn_s: host time blocked in each stage (launch, plus the wait for the
         # top-k); knn_gpu_s: the kNN's device time in situ (event to event on its stream,

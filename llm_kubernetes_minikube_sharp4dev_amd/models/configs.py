@@ -74,10 +74,10 @@ DECODERS = {
                               max_position=2048, norm_eps=1e-5, tie_word_embeddings=True,
                               bos_token_id=2, eos_token_ids=(2,), activation="relu", bias=True),
     # small shapes for tests / smoke runs (same code paths, tiny weights)
-    # (vocab = the built-in tokenizer's 16384 so text round-trips through the servers)
-    "llama-tiny": DecoderConfig("llama-tiny", "llama", 2, 256, 4, 2, 64, 512, 16384,
+    # (vocab = the built-in tokenizer's 32768 so text round-trips through the servers)
+    "llama-tiny": DecoderConfig("llama-tiny", "llama", 2, 256, 4, 2, 64, 512, 32768,
                                 max_position=4096, rope_theta=10000.0),
-    "opt-tiny": DecoderConfig("opt-tiny", "opt", 2, 128, 2, 2, 64, 256, 16384, max_position=512,
+    "opt-tiny": DecoderConfig("opt-tiny", "opt", 2, 128, 2, 2, 64, 256, 32768, max_position=512,
                               tie_word_embeddings=True, activation="relu", bias=True,
                               bos_token_id=2, eos_token_ids=(2,)),
 }
@@ -88,8 +88,8 @@ ENCODERS = {
     "nomic-embed-text": EncoderConfig("nomic-embed-text", "nomic_bert", 12, 768, 12, 3072, 30528,
                                       max_position=8192, pooling="mean", activation="swiglu",
                                       rotary=True, rope_theta=1000.0, bias=False),
-    "bert-tiny": EncoderConfig("bert-tiny", "bert", 2, 128, 2, 256, 16384, max_position=512),
-    "nomic-tiny": EncoderConfig("nomic-tiny", "nomic_bert", 2, 128, 2, 256, 16384,
+    "bert-tiny": EncoderConfig("bert-tiny", "bert", 2, 128, 2, 256, 32768, max_position=512),
+    "nomic-tiny": EncoderConfig("nomic-tiny", "nomic_bert", 2, 128, 2, 256, 32768,
                                 max_position=2048, activation="swiglu", rotary=True, bias=False),
 }
 
