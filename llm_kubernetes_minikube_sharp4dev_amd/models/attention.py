@@ -62,6 +62,11 @@ class AttnMeta:
     pp_ml: Optional[torch.Tensor] = None
     # rows whose hidden state feeds the LM head (last token of each prefill + decode rows)
     logits_idx: Optional[torch.Tensor] = None
+    # context parallelism (paged_attention's cp_group): the block tables / ctx_lens above
+    # describe THIS rank's contiguous shard of every sequence's keys, whose first key sits
+    # at global position cp_key_start_{p,d}[b] (host ints); queries are replicated
+    cp_key_start_p: Optional[list] = None
+    cp_key_start_d: Optional[list] = None
 
     @property
     def num_tokens(self) -> int:
@@ -76,11 +81,17 @@ class AttnMeta:
 
 
 def paged_attention(qkv: torch.Tensor, k_cache, v_cache, meta: AttnMeta, Hq: int, Hkv: int, D: int,
-                    scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """qkv: [T, (Hq+2Hkv)*D] after RoPE (K/V already written to the cache)."""
+                    scale: float, out: Optional[torch.Tensor] = None, cp_group=None) -> torch.Tensor:
+    """qkv: [T, (Hq+2Hkv)*D] after RoPE (K/V already written to the cache).
+
+    ``cp_group``: a context-parallel process group (default None = no CP).  Each of its
+    ranks holds a contiguous shard of every sequence's keys (``meta``'s tables and
+    ``cp_key_start_*``) and the same queries; see :func:`cp_paged_attention`."""
     T = qkv.shape[0]
     if out is None:
         out = torch.empty(T, Hq * D, dtype=qkv.dtype, device=qkv.device)
+    if cp_group is not None and torch.distributed.get_world_size(cp_group) > 1:
+        return cp_paged_attention(qkv, k_cache, v_cache, meta, Hq, Hkv, D, scale, out, cp_group)
     Tp = meta.num_prefill_tokens
     Bd = meta.num_decode
 
@@ -116,4 +127,84 @@ def paged_attention(qkv: torch.Tensor, k_cache, v_cache, meta: AttnMeta, Hq: int
         torch.cuda.current_stream(qkv.device).wait_stream(side)
     elif Bd:
         decode()
+    return out
+
+
+# ---------------------------------------------------------------- context parallelism
+def partial_attention(q, k, v, q_pos, k_pos0: int, scale: float, causal: bool = True):
+    """Attention of q [S, Hq, D] over one key shard k/v [n, Hkv, D] whose key j sits at
+    global position ``k_pos0 + j``; query i at ``q_pos[i]`` sees keys at positions <= its
+    own when ``causal``.  Returns (o f32 [S, Hq, D] normalised over the shard, lse f32
+    [S, Hq]); a query that sees no key of the shard gets o = 0, lse = -inf."""
+    S, Hq, D = q.shape
+    n, Hkv, _ = k.shape
+    if n == 0:
+        return (torch.zeros(S, Hq, D, dtype=torch.float32, device=q.device),
+                torch.full((S, Hq), float("-inf"), dtype=torch.float32, device=q.device))
+    g = Hq // Hkv
+    kf = k.float().repeat_interleave(g, dim=1)
+    vf = v.float().repeat_interleave(g, dim=1)
+    s = torch.einsum("qhd,khd->hqk", q.float(), kf) * scale
+    if causal:
+        kpos = k_pos0 + torch.arange(n, device=q.device)
+        s = s.masked_fill((kpos[None, :] > q_pos.to(q.device).long()[:, None])[None], float("-inf"))
+    lse = torch.logsumexp(s, dim=-1)                                 # [Hq, S]
+    p = torch.exp(s - torch.where(torch.isfinite(lse), lse, torch.zeros_like(lse))[..., None])
+    o = torch.einsum("hqk,khd->qhd", p, vf)
+    return o, lse.transpose(0, 1).contiguous()
+
+
+def merge_partials(o: torch.Tensor, lse: torch.Tensor) -> torch.Tensor:
+    """LSE-weighted merge of per-shard partials: o [C, S, Hq, D], lse [C, S, Hq] ->
+    [S, Hq, D] (exactly softmax attention over the union of the shards)."""
+    m = lse.max(dim=0).values
+    m = torch.where(torch.isfinite(m), m, torch.zeros_like(m))
+    w = torch.exp(lse - m[None])                                     # -inf -> 0
+    den = w.sum(dim=0).clamp_min(1e-30)
+    return (w[..., None] * o).sum(dim=0) / den[..., None]
+
+
+def cp_paged_attention(qkv, k_cache, v_cache, meta: AttnMeta, Hq: int, Hkv: int, D: int, scale: float,
+                       out: torch.Tensor, cp_group) -> torch.Tensor:
+    """Context-parallel attention: every rank attends the (replicated) queries over its
+    local key shard -- prefill rows causally by global position, decode rows over all
+    their keys -- then ONE all-gather of (o, lse) over ``cp_group`` and an LSE merge give
+    each rank the full result.  Collective volume per layer: T x Hq x (D + 1) f32 per
+    rank, independent of the context length (the KV shards never move)."""
+    import torch.distributed as dist
+
+    from ..ops import reference as ref
+
+    Tp, Bd = meta.num_prefill_tokens, meta.num_decode
+    T = Tp + Bd
+    q_all = qkv[:T, : Hq * D].reshape(T, Hq, D)
+    o_loc = torch.zeros(T, Hq, D, dtype=torch.float32, device=qkv.device)
+    l_loc = torch.full((T, Hq), float("-inf"), dtype=torch.float32, device=qkv.device)
+    pos = meta.positions[:T].long()
+    if Tp:
+        cu = [int(x) for x in meta.cu_q.tolist()]
+        starts = meta.cp_key_start_p or [0] * (len(cu) - 1)
+        for b in range(len(cu) - 1):
+            s0, e0 = cu[b], cu[b + 1]
+            n = int(meta.ctx_lens_p[b])
+            kb = ref.gather_paged(k_cache, meta.block_tables_p[b], n)
+            vb = ref.gather_paged(v_cache, meta.block_tables_p[b], n)
+            o_loc[s0:e0], l_loc[s0:e0] = partial_attention(q_all[s0:e0], kb, vb, pos[s0:e0], starts[b], scale)
+    if Bd:
+        starts = meta.cp_key_start_d or [0] * Bd
+        for i in range(Bd):
+            n = int(meta.ctx_lens_d[i])
+            kb = ref.gather_paged(k_cache, meta.block_tables_d[i], n)
+            vb = ref.gather_paged(v_cache, meta.block_tables_d[i], n)
+            r = Tp + i
+            o_loc[r:r + 1], l_loc[r:r + 1] = partial_attention(q_all[r:r + 1], kb, vb, pos[r:r + 1], starts[i],
+                                                               scale)
+    C = dist.get_world_size(cp_group)
+    packed = torch.cat([o_loc.reshape(T, -1), l_loc], dim=1)         # one collective
+    allp = [torch.empty_like(packed) for _ in range(C)]
+    dist.all_gather(allp, packed, group=cp_group)
+    allp = torch.stack(allp)
+    o = allp[..., : Hq * D].reshape(C, T, Hq, D)
+    lse = allp[..., Hq * D:]
+    out[:T] = merge_partials(o, lse).reshape(T, Hq * D).to(out.dtype)
     return out

@@ -54,6 +54,8 @@ class LlamaModel(nn.Module):
         self.hkv = max(1, cfg.num_kv_heads // tp.size)
         self.D = cfg.head_dim
         self.scale = 1.0 / math.sqrt(self.D)
+        # context-parallel group for attention (models/attention.py cp_paged_attention); None = off
+        self.cp_group = None
         self.vocab_lo, self.vocab_hi = tp.shard(cfg.vocab_size) if cfg.vocab_size % tp.size == 0 else (0, cfg.vocab_size)
         e = dict(dtype=dtype, device=device)
         vloc = self.vocab_hi - self.vocab_lo
@@ -109,7 +111,8 @@ class LlamaModel(nn.Module):
             kc, vc = kv_caches[li]
             qkv = ops.linear_rope_kv(x, L.qkv, meta.positions, self.cos_sin, self.hq, self.hkv, self.D, kc, vc,
                                      meta.slots, True, False)
-            attn_out = paged_attention(qkv, kc, vc, meta, self.hq, self.hkv, self.D, self.scale, attn_out)
+            attn_out = paged_attention(qkv, kc, vc, meta, self.hq, self.hkv, self.D, self.scale, attn_out,
+                                       cp_group=self.cp_group)
             nxt = self.layers[li + 1].input_norm if li + 1 < n else self.final_norm
             if fuse:
                 x = ops.linear_add_rmsnorm(attn_out, L.o, res, L.post_norm, cfg.norm_eps)
@@ -153,7 +156,8 @@ class LlamaModel(nn.Module):
             kc, vc = kv_caches[li]
             ops.rope_kv_(qkv, meta.positions, self.cos_sin, self.hq, self.hkv, self.D, kc, vc,
                          meta.slots, True, False)
-            attn_out = paged_attention(qkv, kc, vc, meta, self.hq, self.hkv, self.D, self.scale, attn_out)
+            attn_out = paged_attention(qkv, kc, vc, meta, self.hq, self.hkv, self.D, self.scale, attn_out,
+                                       cp_group=self.cp_group)
             o = tp.reduce_scatter_rows(padded(ops.linear(attn_out, L.o)))
             x = ops.rmsnorm(o, L.post_norm, cfg.norm_eps, residual=res)
             a = ops.linear_swiglu(tp.all_gather_rows(x)[:T], L.gate_up)

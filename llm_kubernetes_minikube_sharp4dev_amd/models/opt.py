@@ -44,6 +44,8 @@ class OPTModel(nn.Module):
         self.hq = self.hkv = cfg.num_heads // tp.size
         self.D = cfg.head_dim
         self.scale = 1.0 / math.sqrt(self.D)
+        # context-parallel group for attention (models/attention.py cp_paged_attention); None = off
+        self.cp_group = None
         e = dict(dtype=dtype, device=device)
         self.vocab_lo, self.vocab_hi = 0, cfg.vocab_size
         self.embed = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden, **e), requires_grad=False)
@@ -83,7 +85,7 @@ class OPTModel(nn.Module):
             k = qkv[:, hq * D:2 * hq * D].view(T, hq, D)
             v = qkv[:, 2 * hq * D:3 * hq * D].view(T, hq, D)
             ops.kv_write(k, v, kc, vc, meta.slots)
-            attn_out = paged_attention(qkv, kc, vc, meta, hq, hq, D, self.scale, attn_out)
+            attn_out = paged_attention(qkv, kc, vc, meta, hq, hq, D, self.scale, attn_out, cp_group=self.cp_group)
             o = ops.linear(attn_out, L.o, L.o_b if self.tp.rank == 0 else None)
             self.tp.all_reduce_(o)
             x = ops.layernorm(o, L.ffn_ln_w, L.ffn_ln_b, cfg.norm_eps, residual=res, write_residual=True)

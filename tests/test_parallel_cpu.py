@@ -405,3 +405,91 @@ def test_tp8_70b_shaped_plain_sp_pipelined_match_single_process():
     assert got["pipelined"] == [ref_plain, ref_c]
     assert got["sp"] == [ref_plain, ref_c]
     print(f"TP8 control hop: {got['ctrl_us_per_msg']:.0f} us per message")
+
+
+# ---- context parallelism: paged_attention(cp_group=...) over contiguous KV shards
+_CP_SEQS = [("prefill", 37, 9), ("prefill", 13, 13), ("decode", 50, 1), ("decode", 5, 1)]  # (kind, ctx, q)
+_CP_H = (4, 2, 16)  # Hq, Hkv, D
+_CP_BS = 4
+
+
+def _cp_problem(C: int, rank: int):
+    """The same attention problem on every rank; rank r's cache holds the r-th contiguous
+    shard of every sequence's keys (C = 1: the whole context)."""
+    from llm_kubernetes_minikube_sharp4dev_amd.models.attention import AttnMeta
+
+    Hq, Hkv, D = _CP_H
+    g = torch.Generator().manual_seed(7)
+    keys = [(torch.randn(n, Hkv, D, generator=g), torch.randn(n, Hkv, D, generator=g)) for _, n, _ in _CP_SEQS]
+    q = [torch.randn(ql, Hq, D, generator=g) for _, _, ql in _CP_SEQS]
+    kc = torch.zeros(64, Hkv, _CP_BS, D)
+    vc = torch.zeros_like(kc)
+    nxt = 0
+    tables, lens, starts = [], [], []
+    for (k, v), (_, n, _) in zip(keys, _CP_SEQS):
+        per = -(-n // C)
+        a, b = min(n, rank * per), min(n, (rank + 1) * per)
+        nb = max(1, -(-(b - a) // _CP_BS))
+        blocks = list(range(nxt, nxt + nb))
+        nxt += nb
+        for j in range(b - a):
+            kc[blocks[j // _CP_BS], :, j % _CP_BS] = k[a + j]
+            vc[blocks[j // _CP_BS], :, j % _CP_BS] = v[a + j]
+        tables.append(blocks + [0] * (16 - nb))
+        lens.append(b - a)
+        starts.append(a)
+    pre = [i for i, s in enumerate(_CP_SEQS) if s[0] == "prefill"]
+    dec = [i for i, s in enumerate(_CP_SEQS) if s[0] == "decode"]
+    qrows = torch.cat([q[i] for i in pre + dec])
+    T = qrows.shape[0]
+    qkv = torch.zeros(T, (Hq + 2 * Hkv) * D)
+    qkv[:, : Hq * D] = qrows.reshape(T, -1)
+    pos = []
+    for i in pre:
+        n, ql = _CP_SEQS[i][1], _CP_SEQS[i][2]
+        pos += list(range(n - ql, n))
+    pos += [_CP_SEQS[i][1] - 1 for i in dec]
+    cu = [0]
+    for i in pre:
+        cu.append(cu[-1] + _CP_SEQS[i][2])
+    meta = AttnMeta(positions=torch.tensor(pos, dtype=torch.int32), slots=torch.full((T,), -1, dtype=torch.int32),
+                    num_prefill_tokens=cu[-1], num_prefill_seqs=len(pre), num_decode=len(dec),
+                    cu_q=torch.tensor(cu, dtype=torch.int32),
+                    ctx_lens_p=torch.tensor([lens[i] for i in pre], dtype=torch.int32),
+                    block_tables_p=torch.tensor([tables[i] for i in pre], dtype=torch.int32),
+                    q_lens_cpu=[_CP_SEQS[i][2] for i in pre], ctx_lens_cpu=[lens[i] for i in pre],
+                    block_tables_d=torch.tensor([tables[i] for i in dec], dtype=torch.int32),
+                    ctx_lens_d=torch.tensor([lens[i] for i in dec], dtype=torch.int32),
+                    cp_key_start_p=[starts[i] for i in pre], cp_key_start_d=[starts[i] for i in dec])
+    return qkv, kc, vc, meta
+
+
+def _cp_worker(rank, world, port, out_path):
+    _init(rank, world, port)
+    from llm_kubernetes_minikube_sharp4dev_amd.models.attention import paged_attention
+
+    Hq, Hkv, D = _CP_H
+    qkv, kc, vc, meta = _cp_problem(world, rank)
+    out = paged_attention(qkv, kc, vc, meta, Hq, Hkv, D, D ** -0.5, cp_group=dist.group.WORLD)
+    torch.save(out, f"{out_path}.{rank}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_context_parallel_attention_matches_single_process(world):
+    """Every CP rank holds one contiguous shard of each sequence's keys (some shards empty
+    for the 5-key sequence at world 3); partial attention + one all-gather + LSE merge must
+    equal unsharded paged attention for chunked-prefill rows (causal by global position)
+    and decode rows."""
+    from llm_kubernetes_minikube_sharp4dev_amd.models.attention import paged_attention
+
+    Hq, Hkv, D = _CP_H
+    qkv, kc, vc, meta = _cp_problem(1, 0)
+    meta.cp_key_start_p = meta.cp_key_start_d = None
+    ref = paged_attention(qkv, kc, vc, meta, Hq, Hkv, D, D ** -0.5)
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "cp")
+        mp.spawn(_cp_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        for r in range(world):
+            got = torch.load(f"{out}.{r}", weights_only=True)
+            torch.testing.assert_close(got, ref, atol=2e-5, rtol=2e-5)
