@@ -18,6 +18,8 @@
 //  * K/V for tile t+1 are loaded into registers while tile t is computed and
 //    written to LDS after the barrier (issue-early / write-late staging).
 //  * online softmax in the exp2 domain with the scale folded into one multiply.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -63,16 +65,20 @@ struct PrefillParams {
   float* part_ml;
 };
 
-template <int D, bool CAUSAL, bool PAGED, int WH>
-__global__ __launch_bounds__(256, 2) void flash_prefill_kernel(PrefillParams p) {
+// NW waves per workgroup (4 or 8): WH of them share a row group (one head each), and
+// NW / WH row groups of 32 queries sit on top of each other, all fed by the same staged
+// K/V tile -- with NW = 8 each K/V byte brought into LDS serves 2x the MFMA work.
+template <int D, bool CAUSAL, bool PAGED, int WH, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillParams p) {
+  constexpr int NT = 64 * NW;      // threads
   constexpr int KK = D / 16;       // QK k-steps
   constexpr int ND = D / 32;       // O^T d tiles
   constexpr int CPR = D / 8;       // 16-byte chunks per row
   constexpr int NCH = KT * CPR;    // chunks per tile
-  constexpr int CPT = NCH / 256;   // chunks per thread per tile
-  constexpr int WR = 4 / WH;
+  constexpr int CPT = NCH / NT;    // chunks per thread per tile
+  constexpr int WR = NW / WH;
   constexpr int QB = 32 * WR;
-  static_assert(CPT >= 1, "tile too small");
+  static_assert(CPT >= 1 && NCH % NT == 0, "tile too small for the workgroup");
 
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * KT * D];
   bf16_t* Ks = lds;
@@ -97,6 +103,18 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(PrefillParams p) 
   const int qpos = past + qrow;        // absolute position
   const bool qvalid = qrow < qlen;
 
+  // Paged K/V: the 64 / (D / 8) rows one wave stages lie in ONE cache block (BS >= 512 / D,
+  // checked on the host), so the block-table lookup is wave-uniform: a scalar load and a
+  // scalar base per chunk, the lane part (row within block, 16-byte chunk) a constant.
+  // Rows past the context read the last block (masked later).
+  const int kvh_u = blockIdx.y * WH / G;  // == head / G for every wave of the workgroup
+  auto paged_base = [&](int kt, int row) -> long {
+    const int last = (ctx - 1) >> p.bs_shift;
+    const int bi = __builtin_amdgcn_readfirstlane(min((kt + row) >> p.bs_shift, last));
+    const long blk = p.block_tables[(long)b * p.bt_stride + bi];
+    return ((blk * p.Hkv + kvh_u) << p.bs_shift) * D;
+  };
+
   // Q^T fragments: lane holds Q[qrow][16kk + 8h + j]
   short8 qf[KK];
   {
@@ -119,15 +137,15 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(PrefillParams p) 
   auto gload = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int c = tid + 256 * i;
+      const int c = tid + NT * i;
       const int row = c / CPR, ch = c % CPR;
       const int key = min(kt + row, ctx - 1);  // clamp: masked later
       const bf16_t *kp, *vp;
       if constexpr (PAGED) {
-        const long blk = p.block_tables[(long)b * p.bt_stride + (key >> p.bs_shift)];
-        const long off = (((blk * p.Hkv + kvh) << p.bs_shift) + (key & (p.BS - 1))) * D + ch * 8;
-        kp = p.k + off;
-        vp = p.v + off;
+        const long base = paged_base(kt, row);
+        const int loff = (row & (p.BS - 1)) * D + ch * 8;
+        kp = p.k + base + loff;
+        vp = p.v + base + loff;
       } else {
         kp = p.k + (long)(qbeg + key) * p.ks + (long)kvh * D + ch * 8;
         vp = p.v + (long)(qbeg + key) * p.vs + (long)kvh * D + ch * 8;
@@ -139,7 +157,7 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(PrefillParams p) 
   auto swrite = [&]() {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int c = tid + 256 * i;
+      const int c = tid + NT * i;
       const int row = c / CPR, ch = c % CPR;
       *reinterpret_cast<short8*>(Ks + row * D + k_swz<D>(row, ch) * 8) = kreg[i];
       *reinterpret_cast<short8*>(Vs + row * D + v_swz<D>(row, ch) * 8) = vreg[i];
@@ -291,9 +309,22 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(PrefillParams p) 
   }
 }
 
+
 }  // namespace
 
-int lk_prefill_rows_per_tile(int G) { return G >= 4 ? 32 : 32 * (4 / G); }
+// LK_PREFILL_WAVES=8: 8-wave workgroups (64 query rows x 4 heads of a GQA group) for
+// G >= 4 at D >= 64.  Measured on MI355X (kernel_bench, 2 runs each): +3-5 % on long causal
+// prefill (B8 L4096: 873-889 vs 849 TF/s), -2 % on the serving chunk shape (B6 q643 ctx930:
+// 494 vs 503-507), so the 4-wave kernel is the default.
+static int prefill_waves(int G, int D) {
+  static const int env = [] {
+    const char* e = getenv("LK_PREFILL_WAVES");
+    return e ? atoi(e) : 4;
+  }();
+  return (G >= 4 && D >= 64 && env == 8) ? 8 : 4;
+}
+
+int lk_prefill_rows_per_tile(int G) { return G >= 4 ? 32 * (prefill_waves(G, 128) / 4) : 32 * (4 / G); }
 
 int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v, long ks, long vs,
                      const int* block_tables, int bt_stride, const int* cu_q, const int* ctx_lens,
@@ -306,17 +337,20 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
   if (!(G == 1 || G == 2 || G % 4 == 0)) return -2;
   if (paged && (BS <= 0)) return -4;
   if (paged && (BS & (BS - 1))) return -4;  // power-of-two cache blocks
+  if (paged && BS < 512 / D) return -4;     // a wave's staged rows must share one block
   int bs_shift = 0;
   while ((1 << bs_shift) < BS) ++bs_shift;
   PrefillParams pr{q, qs, k, v, ks, vs, block_tables, bt_stride, cu_q, ctx_lens, tile_seq,
                    tile_q0, out, os, Hq, Hkv, BS, bs_shift, scale * 1.4426950408889634f, part_o, part_ml};
   const int WH = G >= 4 ? 4 : G;
+  const int NW = prefill_waves(G, D);
   dim3 grid(ntiles, Hq / WH);
-#define L(DD, C, PG, W) flash_prefill_kernel<DD, C, PG, W><<<grid, 256, 0, st>>>(pr)
-#define BY_W(DD, C, PG)          \
-  if (WH == 4) L(DD, C, PG, 4);  \
-  else if (WH == 2) L(DD, C, PG, 2); \
-  else L(DD, C, PG, 1);
+#define L(DD, C, PG, W, N) flash_prefill_kernel<DD, C, PG, W, N><<<grid, 64 * N, 0, st>>>(pr)
+#define BY_W(DD, C, PG)                                 \
+  if (WH == 4 && NW == 8) L(DD, C, PG, 4, (DD >= 64 ? 8 : 4));   \
+  else if (WH == 4) L(DD, C, PG, 4, 4);                 \
+  else if (WH == 2) L(DD, C, PG, 2, 4);                 \
+  else L(DD, C, PG, 1, 4);
 #define BY_MODE(DD)                                    \
   if (causal && paged) { BY_W(DD, true, true) }        \
   else if (causal && !paged) { BY_W(DD, true, false) } \

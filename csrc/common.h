@@ -27,8 +27,12 @@ LK_DEVICE bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+// two f32 -> one dword of 2 x bf16 (lo in bits 0-15): a vector conversion lowers to ONE
+// v_cvt_pk_bf16_f32 (two scalar casts cost two converts + a shift + an or)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float floatx2_t __attribute__((ext_vector_type(2)));
 LK_DEVICE unsigned pack_bf2(float lo, float hi) {
-  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((floatx2_t){lo, hi}, bf16x2_t));
 }
 
 LK_DEVICE float wave_sum(float v) {

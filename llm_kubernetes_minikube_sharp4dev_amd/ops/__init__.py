@@ -129,7 +129,12 @@ def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_
 
 
 def prefill_rows_per_tile(G: int) -> int:
-    return 32 if G >= 4 else 32 * (4 // G)
+    """Query rows per flash-prefill tile: the HIP library's choice (8-wave 64-row
+    workgroups for GQA groups of >= 4 heads unless LK_PREFILL_WAVES=4), else 32 / 4-wave."""
+    try:
+        return int(lib().prefill_rows_per_tile(G))
+    except Exception:  # no extension (CPU): the tiles only matter to the HIP kernel
+        return 32 if G >= 4 else 32 * (4 // G)
 
 
 def prefill_tiles(q_lens: Sequence[int], ctx_lens: Sequence[int], G: int, causal: bool):
