@@ -245,11 +245,17 @@ def repeat_penalty_(logits, window, penalty):
 
 # Decode-regime GEMMs (csrc/skinny_gemm.hip) vs the library GEMM, from the MI355X
 # sweeps in profiles/r1_skinny_gemm.md and profiles/r1_ws_sweep.md:
-#  * M <= 16: the fragment-load kernel (weights straight to VGPRs, split-K);
-#  * 16 < M <= 256: the LDS-DMA weight-streaming kernel: 1.2-2.3x hipBLASLt on every
-#    Llama projection (QKV / O / down; gate_up+SwiGLU fused up to M = 160);
-#  * hipBLASLt keeps the LM head (N = 128256 fills the chip by itself) and anything larger.
-SKINNY_MAX_M = int(os.environ.get("LK_SKINNY_MAX_M", "16"))
+#  * M <= 256: the LDS-DMA weight-streaming kernel: 1.2-2.3x hipBLASLt on every
+#    Llama projection (QKV / O / down; gate_up+SwiGLU fused up to M = 160), and its
+#    split-K reduction fused into the consumer (RMSNorm+residual, RoPE+KV write);
+#  * the LM head (N >= 65536) at M <= 16: the fragment-load kernel (weights straight to
+#    VGPRs, split-K); larger M: the prefill GEMM.
+# The fragment-load kernel also served every projection at M <= 16 until round 2; the
+# fused weight-streaming path beat it end to end at every small batch (bench.py --batch
+# 1/2/4/8 on MI355X: p50 227 -> 201, 235 -> 207, 252 -> 224, 292 -> 259 ms), so
+# LK_SKINNY_MAX_M now defaults to 0.
+SKINNY_MAX_M = int(os.environ.get("LK_SKINNY_MAX_M", "0"))
+LM_HEAD_SKINNY_MAX_M = 16
 WS_MAX_M = int(os.environ.get("LK_WS_MAX_M", "256"))
 WS_SWIGLU_MAX_M = 160
 
@@ -270,7 +276,7 @@ def _decode_gemm_kind(x, w, swiglu: bool) -> Optional[str]:
     if M <= SKINNY_MAX_M:
         return "skinny"
     if N >= 65536 and not swiglu:
-        return None
+        return "skinny" if M <= LM_HEAD_SKINNY_MAX_M else None
     if M <= (WS_SWIGLU_MAX_M if swiglu else WS_MAX_M):
         return "ws"
     return None

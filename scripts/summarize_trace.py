@@ -12,6 +12,27 @@ import sys
 
 BY_GRID = os.environ.get("SUMMARY_BY_GRID") == "1"
 
+# coarse classes for the budget table (first match wins)
+CLASSES = [
+    ("decode GEMM (wsgemm / skinny, weight streaming)", ("wsgemm", "skinny", "ws_linear")),
+    ("prefill GEMM (gemm_kernel, MFMA 256x256/192)", ("gemm_kernel",)),
+    ("hipBLASLt / rocBLAS", ("Cijk", "rocblas")),
+    ("flash prefill + cascade", ("flash_prefill",)),
+    ("paged decode attention", ("paged_decode", "decode_reduce", "split_reduce")),
+    ("norms (rms/layer)", ("rmsnorm", "layernorm")),
+    ("rope + KV write", ("rope", "kv_write")),
+    ("sampling / select", ("sample", "select", "argmax", "gumbel")),
+    ("kNN", ("knn", "score_topk", "topk")),
+    ("activations / elementwise", ("act", "silu", "gelu", "elementwise", "vectorized", "copy")),
+]
+
+
+def _cls(name):
+    for label, keys in CLASSES:
+        if any(k in name for k in keys):
+            return label
+    return "other"
+
 
 def main(path, window_s, top=25):
     rows = list(csv.DictReader(open(path)))
@@ -54,6 +75,12 @@ def main(path, window_s, top=25):
         k = "<5us" if g < 5e3 else "5-20us" if g < 2e4 else "20-100us" if g < 1e5 else "0.1-1ms" if g < 1e6 else ">1ms"
         b[k] += 1
         bt[k] += g
+    byc = collections.defaultdict(float)
+    for k, (t, n) in agg.items():
+        byc[_cls(k)] += t
+    print("\n| class | total ms | share |\n|---|---|---|")
+    for k, t in sorted(byc.items(), key=lambda x: -x[1]):
+        print(f"| {k} | {t / 1e6:.1f} | {100 * t / tot:.1f} % |")
     print("\n| idle gap | count | total ms |\n|---|---|---|")
     for k in ["<5us", "5-20us", "20-100us", "0.1-1ms", ">1ms"]:
         print(f"| {k} | {b[k]} | {bt[k] / 1e6:.1f} |")

@@ -352,18 +352,23 @@ def test_skinny_swiglu_matches_unfused(hip, M, IK):
         _close(hip.skinny_linear(x, w, True, 2), a_ref, 0.03, 0.01, "swiglu split 2")
 
 
-def test_linear_dispatch_uses_skinny(hip):
+def test_linear_dispatch_decode_kernels(hip):
+    """Decode-sized projections take the weight-streaming kernel (whose split-K reduce the
+    consumer fuses) from M = 1; the LM head at M <= 16 the fragment-load kernel."""
     x = torch.randn(8, 4096, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(6144, 4096, device=DEV, dtype=torch.bfloat16) * 0.05
-    assert ops._decode_gemm_kind(x, w, False) == "skinny"
+    assert ops._decode_gemm_kind(x, w, False) == "ws"
     _close(ops.linear(x, w), x.float() @ w.float().t(), 0.02, 0.01)
+    head = torch.randn(128256, 4096, device=DEV, dtype=torch.bfloat16) * 0.05
+    assert ops._decode_gemm_kind(x, head, False) == "skinny"
+    _close(ops.linear(x, head), x.float() @ head.float().t(), 0.02, 0.01)
     assert ops._decode_gemm_kind(torch.randn(512, 4096, device=DEV, dtype=torch.bfloat16), w, False) is None
     x128 = torch.randn(128, 4096, device=DEV, dtype=torch.bfloat16)
     assert ops._decode_gemm_kind(x128, w, False) == "ws"
     _close(ops.linear(x128, w), x128.float() @ w.float().t(), 0.02, 0.01)
 
 
-@pytest.mark.parametrize("M", [33, 64, 65, 100, 128, 129, 200, 256])
+@pytest.mark.parametrize("M", [1, 2, 8, 16, 33, 64, 65, 100, 128, 129, 200, 256])
 @pytest.mark.parametrize("NK", [(6144, 4096), (4096, 4096), (4096, 14336), (1280, 8192), (128256, 4096)])
 def test_ws_linear(hip, M, NK):
     """LDS-DMA staged weight-streaming GEMM (every BN / split plan) vs an fp32 matmul."""
@@ -379,7 +384,7 @@ def test_ws_linear(hip, M, NK):
                 _close(hip.ws_linear(x, w, False, bn, S), y_ref, 0.02, 0.01, f"ws bn{bn} S{S}")
 
 
-@pytest.mark.parametrize("M", [64, 128, 256])
+@pytest.mark.parametrize("M", [1, 8, 64, 128, 256])
 @pytest.mark.parametrize("IK", [(14336, 4096), (3584, 8192)])
 def test_ws_swiglu(hip, M, IK):
     I, K = IK
@@ -472,7 +477,7 @@ def test_serving_gemms_never_reach_the_library(hip):
     assert not ops.LIBRARY_FALLBACKS, ops.LIBRARY_FALLBACKS
 
 
-@pytest.mark.parametrize("M", [33, 64, 100, 128, 200, 256])
+@pytest.mark.parametrize("M", [1, 4, 16, 33, 64, 100, 128, 200, 256])
 @pytest.mark.parametrize("NK", [(4096, 4096), (4096, 14336), (8192, 8192), (8192, 28672)])
 def test_ws_linear_rmsnorm_matches_unfused(hip, M, NK):
     """Decode fusion: split-K weight-streaming GEMM -> (reduce + residual add + RMSNorm in one
@@ -497,7 +502,7 @@ def test_ws_linear_rmsnorm_matches_unfused(hip, M, NK):
     _close(y, y_ref, 0.05, 0.02, f"rmsnorm M{M} N{N}")
 
 
-@pytest.mark.parametrize("M", [40, 128, 200])
+@pytest.mark.parametrize("M", [1, 3, 40, 128, 200])
 @pytest.mark.parametrize("neox", [True, False])
 @pytest.mark.parametrize("inplace", [False, True])
 def test_ws_linear_rope_kv_matches_unfused(hip, M, neox, inplace):
@@ -516,7 +521,8 @@ def test_ws_linear_rope_kv_matches_unfused(hip, M, neox, inplace):
     kc = torch.zeros(NB, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
     vc = torch.zeros_like(kc)
     slots = torch.randperm(NB * BS, device=DEV)[:M].int()
-    slots[1] = -1
+    if M > 1:
+        slots[1] = -1
     kc2, vc2 = kc.clone(), vc.clone()
     qkv = hip.ws_linear_rope_kv(x, w, pos, cs, Hq, Hkv, D, kc, vc, slots, neox, inplace, bn, S)
     qkv2 = hip.ws_linear(x, w, False, bn, S)
