@@ -90,26 +90,29 @@ class EmbeddingEngine:
         return out
 
     def embed_cpu(self, texts: list[str]) -> torch.Tensor:
-        """Host f32 [n, D] embeddings computed on this engine's own high-priority HIP stream,
-        copied back on it and synchronised there: a serving process's query embeddings do not
-        queue behind the LLM engine's pipelined steps."""
+        """Host f32 [n, D] embeddings computed on one of this engine's high-priority HIP
+        streams and copied back on it: a serving process's query embeddings do not queue
+        behind the LLM engine's pipelined steps.  The lock covers only the launches; the wait
+        for the copy happens outside it, so concurrent callers (the server's micro-batcher
+        runs up to two batches at once) overlap their device waits."""
         if self.device.type != "cuda":
             return self.embed(texts).float()
         t0 = time.perf_counter()
         with self.lock:
-            if getattr(self, "_stream", None) is None:
+            if getattr(self, "_streams", None) is None:
                 # high priority: a query embedding (a few ms of small kernels) is dispatched
                 # ahead of the queued kernels of the LLM engine's step instead of behind them
-                self._stream = torch.cuda.Stream(self.device, priority=-1)
-            with torch.cuda.stream(self._stream):
+                self._streams = [torch.cuda.Stream(self.device, priority=-1) for _ in range(2)]
+                self._next = 0
+            st = self._streams[self._next]
+            self._next = (self._next + 1) % len(self._streams)
+            with torch.cuda.stream(st):
                 r = self._embed_texts(list(texts)) if texts else torch.zeros((0, self.dim), device=self.device)
-                n = r.numel()
-                if getattr(self, "_pinned", None) is None or self._pinned.numel() < n:  # grown, then reused
-                    self._pinned = torch.empty(max(n, 1 << 16), dtype=torch.float32, pin_memory=True)
-                host = self._pinned[:n].view(r.shape)
+                host = torch.empty(r.shape, dtype=torch.float32, pin_memory=True)
                 host.copy_(r, non_blocking=True)
-            self._stream.synchronize()
-            host = host.clone()
+                ev = torch.cuda.Event()
+                ev.record(st)
+        ev.synchronize()
         M.EMBED_LAT.observe(time.perf_counter() - t0)
         return host
 

@@ -243,7 +243,7 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
         h = await asyncio.to_thread(mgr.embedder, model)
         b = batchers.get(h.name)
         if b is None:
-            b = batchers[h.name] = MicroBatcher(h.engine.embed_cpu)
+            b = batchers[h.name] = MicroBatcher(h.engine.embed_cpu, max_inflight=2)
         vec = await b.submit(texts) if texts else h.engine.embed_cpu(texts)
         return h, vec.tolist()
 
