@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--kv-gb", type=float, default=48.0)
     ap.add_argument("--max-batched-tokens", type=int, default=None,
                     help="token budget per engine step (default: 4096 continuous, 65536 batch)")
-    ap.add_argument("--admit-chunk", type=int, default=8,
+    ap.add_argument("--admit-chunk", type=int, default=16,
                     help="continuous mode: requests retrieved + admitted together (batched embed/kNN)")
     ap.add_argument("--unconstrained", dest="constrained", action="store_false",
                     help="decode without the tool-call grammar.  Default: the grammar (engine/constrained.py) makes "
@@ -81,6 +81,9 @@ def parse():
                          "(reduce-scatter / all-gather around the norms); default off")
     ap.add_argument("--token-align", type=int, default=256,
                     help="trim mixed steps' prefill chunks to a multiple of this many rows (0: off)")
+    ap.add_argument("--token-align-wave", type=int, default=0,
+                    help="steps longer than this many rows are trimmed to a multiple of it (4096: whole "
+                         "waves of 256x256 tiles on the N=4096 projections); 0: off")
     ap.add_argument("--admission", choices=["deferred", "inline", "threaded"], default="deferred",
                     help="continuous mode, how retrieval for newly freed slots runs on the engine thread: "
                          "deferred (default) launches query encoder + kNN on a side stream and admits the "
@@ -214,16 +217,17 @@ def main():
         llm.sp_min_tokens = args.sp_min_tokens
     sync()
     log(rank, f"{args.model} random-init (tp={args.tp}) in {time.perf_counter() - t0:.1f}s")
-    # continuous: ~4k-token steps keep most steps mixed (decode rows ride on the prefill
-    # GEMMs) without starving decode (profiles/r1_sched_sweep.md)
-    mbt = args.max_batched_tokens or (4096 if args.mode == "continuous" else 65536)
+    # continuous: 8k-token steps (whole waves of 256x256 tiles on every projection: 6144-row
+    # steps measured 4 % slower) -- on MI355X 8192-token steps with admission chunks of 16
+    # beat 4096 / 8 by 2 % in q/s and p50 on the same box (profiles/r2_sched_sweep.md)
+    mbt = args.max_batched_tokens or (8192 if args.mode == "continuous" else 65536)
     runner_kw = dict(block_size=16, max_model_len=8192, max_num_seqs=max(args.batch, 64), kv_cache_gb=args.kv_gb,
                      use_graphs=on_gpu and not args.no_graphs)
     if not on_gpu:
         runner_kw.pop("kv_cache_gb")
         runner_kw["num_blocks"] = max(256, args.batch * 80)
     engine_kw = dict(max_num_batched_tokens=mbt, enable_prefix_caching=not args.no_prefix_cache, eos_ids=set(),
-                     token_align=args.token_align)
+                     token_align=args.token_align, token_align_wave=args.token_align_wave)
     if args.sampling == "ollama":
         params = SamplingParams(max_tokens=args.max_new_tokens, ignore_eos=True)  # Ollama defaults
         args.constrained = False

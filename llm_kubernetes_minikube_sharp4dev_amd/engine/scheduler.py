@@ -33,12 +33,17 @@ class ScheduledBatch:
 
 class Scheduler:
     def __init__(self, allocator, block_size: int, max_num_seqs: int = 256,
-                 max_num_batched_tokens: int = 65536, max_model_len: int = 8192, token_align: int = 256):
+                 max_num_batched_tokens: int = 65536, max_model_len: int = 8192, token_align: int = 256,
+                 token_align_wave: int = 0):
         self.alloc = allocator
         # mixed steps: trim prefill chunks so the step's row count is a multiple of the
-        # library GEMM's 256-row macro tile (a 3852-row step runs 16 row tiles, the 16th
+        # prefill GEMM's 256-row macro tile (a 3852-row step runs 16 row tiles, the 16th
         # nearly empty); the trimmed tokens lead the next step
         self.token_align = token_align
+        # ... and, past token_align_wave rows, to a multiple of it: with 256 x 256 tiles a
+        # 4096-row step fills the chip's 256 CUs exactly once on the N = 4096 projections
+        # (o / down), a 5120-row step runs 1.25 waves of them
+        self.token_align_wave = token_align_wave
         self.bs = block_size
         self.max_num_seqs = max_num_seqs
         self.max_tokens = max_num_batched_tokens
@@ -142,6 +147,8 @@ class Scheduler:
         if not a:
             return
         total = batch.num_tokens
+        if self.token_align_wave and total > self.token_align_wave:
+            a = self.token_align_wave
         ex = total % a
         if total <= a or not ex:
             return
