@@ -87,7 +87,7 @@ class EngineConfig:
     gpu_memory_fraction: float = 0.85                  # of the 288 GB HBM3E
     kv_cache_gb: Optional[float] = None                # explicit KV budget (overrides the fraction)
     max_num_seqs: int = 256
-    max_num_batched_tokens: int = 65536
+    max_num_batched_tokens: int = 8192                 # per step: whole waves of 256x256 GEMM tiles (profiles/r2_sched_sweep.md)
     max_model_len: int = 8192
     enable_prefix_caching: bool = True
     use_hip_graphs: bool = True
