@@ -72,10 +72,15 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(
     LK_DASSERT(blk[i] >= 0);
   __syncthreads();
 
-  auto row_ptr = [&](const bf16_t* cache, int rel) {
-    rel = min(rel, nkeys - 1);
-    const int abs_k = k_begin + rel;
-    return cache + (((long)blk[rel / BS] * Hkv + kvh) * BS + (abs_k % BS)) * D;
+  // A wave's 16 K rows (16t + r16) and the 4 V rows of one load (i * RPL + lane / CPR) lie in
+  // one cache block (BS >= 16, splits and chunks block-aligned: checked on the host), so the
+  // block lookup is wave-uniform -- a scalar read of the LDS slice -- and the lane part a
+  // constant.  Rows past the split re-read its last key (block clamped here, slot by the
+  // clamped row): never a stale slot, whose bytes could be NaN under a zero P.
+  const int last_blk = (nkeys - 1) / BS;
+  auto blk_base = [&](const bf16_t* cache, int rel0) {
+    const int bi = __builtin_amdgcn_readfirstlane(min(rel0 / BS, last_blk));
+    return cache + ((long)blk[bi] * Hkv + kvh) * BS * D;
   };
 
   // Q^T fragments (B of QK): lane holds Q[q = r16][32kk + 8*h4 + j]
@@ -88,17 +93,21 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(
 
   const int nch = (nkeys + 31) >> 5;
   short8 kr[2][KK], vr[NVL];
+  // k_begin is block-aligned (split % BS == 0, k_start a multiple of BS): row rel of the
+  // split sits at slot rel % BS of its block
   auto load_chunk = [&](int c, short8 (&kd)[2][KK], short8 (&vd)[NVL]) {
     const int base = 32 * c;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const bf16_t* kp = row_ptr(kc, base + 16 * t + r16) + 8 * h4;
+      const bf16_t* kp = blk_base(kc, base + 16 * t) + (min(base + 16 * t + r16, nkeys - 1) % BS) * D + 8 * h4;
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) kd[t][kk] = *reinterpret_cast<const short8*>(kp + 32 * kk);
     }
 #pragma unroll
-    for (int i = 0; i < NVL; ++i)
-      vd[i] = *reinterpret_cast<const short8*>(row_ptr(vc, base + i * RPL + lane / CPR) + (lane % CPR) * 8);
+    for (int i = 0; i < NVL; ++i) {
+      const int rel = min(base + i * RPL + lane / CPR, nkeys - 1);
+      vd[i] = *reinterpret_cast<const short8*>(blk_base(vc, base + i * RPL) + (rel % BS) * D + (lane % CPR) * 8);
+    }
   };
 
   floatx4 o[ND];
@@ -264,7 +273,9 @@ __global__ __launch_bounds__(D) void decode_reduce_kernel(const float* __restric
 // (few partials) at large batch; static per (B, Hkv) so hipGraph launches are fixed.
 int lk_decode_split_size(int B, int Hkv) {
   const int bh = B * Hkv;
-  if (bh >= 512) return 1024;
+  // >= 2 workgroups per CU without splitting: the longest split (fewest launched-but-empty
+  // split workgroups in the static graph grid, no partials below 2k keys)
+  if (bh >= 512) return kMaxSplit;
   if (bh >= 128) return 512;
   if (bh >= 32) return 256;
   return 128;

@@ -106,7 +106,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
   // Paged K/V: the 64 / (D / 8) rows one wave stages lie in ONE cache block (BS >= 512 / D,
   // checked on the host), so the block-table lookup is wave-uniform: a scalar load and a
   // scalar base per chunk, the lane part (row within block, 16-byte chunk) a constant.
-  // Rows past the context read the last block (masked later).
+  // Rows past the context re-read the last valid key (block clamped here, slot by the
+  // clamped key): never a stale slot, whose bytes could be NaN under a zero P.
   const int kvh_u = blockIdx.y * WH / G;  // == head / G for every wave of the workgroup
   auto paged_base = [&](int kt, int row) -> long {
     const int last = (ctx - 1) >> p.bs_shift;
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
       const bf16_t *kp, *vp;
       if constexpr (PAGED) {
         const long base = paged_base(kt, row);
-        const int loff = (row & (p.BS - 1)) * D + ch * 8;
+        const int loff = (key & (p.BS - 1)) * D + ch * 8;  // clamped key: a valid slot
         kp = p.k + base + loff;
         vp = p.v + base + loff;
       } else {
