@@ -68,9 +68,11 @@ def parse():
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (ranks per replica)")
     ap.add_argument("--kv-gb", type=float, default=48.0)
     ap.add_argument("--max-batched-tokens", type=int, default=None,
-                    help="token budget per engine step (default: 4096 continuous, 65536 batch)")
-    ap.add_argument("--admit-chunk", type=int, default=16,
-                    help="continuous mode: requests retrieved + admitted together (batched embed/kNN)")
+                    help="token budget per engine step (default: continuous 64 x --batch capped at 8192, "
+                         "batch mode 65536)")
+    ap.add_argument("--admit-chunk", type=int, default=None,
+                    help="continuous mode: requests retrieved + admitted together (batched embed/kNN); "
+                         "default --batch / 8")
     ap.add_argument("--unconstrained", dest="constrained", action="store_false",
                     help="decode without the tool-call grammar.  Default: the grammar (engine/constrained.py) makes "
                          "the random-init model emit valid tool calls, so every request also runs the k8s dispatch "
@@ -103,6 +105,10 @@ def parse():
     ap.add_argument("--via-http", action="store_true",
                     help="the .NET-facing path: Ollama-compatible server + Minimal_RAG app as separate processes, "
                          "/agent_rag driven over HTTP at concurrency 1, 8, 128 (benchmarks/http_bench.py)")
+    ap.add_argument("--tokenizer", default=None,
+                    help="tokenizer.json to use instead of the built-in one (e.g. benchmarks/data/"
+                         "bpe_runbooks_r1.json, the round-1 tokenizer trained on the synthetic corpus itself, "
+                         "for like-for-like comparisons with round-1 numbers)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -114,6 +120,8 @@ def log(rank, *a):
 
 def main():
     args = parse()
+    if args.admit_chunk is None:  # 1/8 of the in-flight requests per retrieval batch (16 at 128)
+        args.admit_chunk = max(1, args.batch // 8)
     if args.via_http:  # before any GPU use: the servers are child processes
         import subprocess
 
@@ -182,7 +190,12 @@ def main():
     n_replicas = world // args.tp
 
     cfg = Config()
-    tok = builtin_tokenizer()
+    if args.tokenizer:
+        from llm_kubernetes_minikube_sharp4dev_amd.models.tokenizer import load_tokenizer
+
+        tok = load_tokenizer(args.tokenizer)
+    else:
+        tok = builtin_tokenizer()
 
     # ---- embedder + index build (embedding work sharded over ALL ranks, all-gather over RCCL;
     # every replica driver then holds the whole corpus in HBM: 1M x 768 bf16 = 1.5 GB)
@@ -220,7 +233,9 @@ def main():
     # continuous: 8k-token steps (whole waves of 256x256 tiles on every projection: 6144-row
     # steps measured 4 % slower) -- on MI355X 8192-token steps with admission chunks of 16
     # beat 4096 / 8 by 2 % in q/s and p50 on the same box (profiles/r2_sched_sweep.md)
-    mbt = args.max_batched_tokens or (8192 if args.mode == "continuous" else 65536)
+    # (scaled with the in-flight count: 64 tokens per request in flight, e.g. 4096 at 64 for
+    # the 70B config, where 8192-token steps measured 9 % slower)
+    mbt = args.max_batched_tokens or (min(8192, 64 * max(args.batch, 32)) if args.mode == "continuous" else 65536)
     runner_kw = dict(block_size=16, max_model_len=8192, max_num_seqs=max(args.batch, 64), kv_cache_gb=args.kv_gb,
                      use_graphs=on_gpu and not args.no_graphs)
     if not on_gpu:
@@ -423,6 +438,8 @@ def main():
                 # RAG prompt bodies planned in the timed window: characters, tokens (chat template
                 # included) and their ratio under the built-in tokenizer (models/tokenizer.py)
                 **prompt_len,
+                "tokenizer": (os.path.basename(args.tokenizer) if args.tokenizer
+                              else f"built-in byte-level BPE, llama-3 split, {tok.vocab_size} vocab"),
                 "parallelism": par,
                 "load": (f"continuous batching, closed loop, {args.batch} requests in flight per replica, "
                          f"step = {args.batch} completions per replica" if args.mode == "continuous"

@@ -294,6 +294,8 @@ EPI = {None: 0, "swiglu": 1, "bias": 2, "gelu": 3, "relu": 4}
 # measurement knob only: LK_GEMM_LIBRARY=1 sends the prefill-regime GEMMs to hipBLASLt (+ the
 # separate activation kernels) for in-situ A/B against the hand-written kernel
 GEMM_LIBRARY = os.environ.get("LK_GEMM_LIBRARY", "0") == "1"
+# K-loop schedule of untuned shapes (0: 4 phases per K-tile, 1: 2 phases); in-situ A/B knob
+GEMM_SCHED = int(os.environ.get("LK_GEMM_SCHED", "0"))
 _GEMM_TABLE: dict = {}
 LIBRARY_FALLBACKS: dict = {}
 
@@ -321,7 +323,7 @@ def _gemm_default(M: int, N: int, K: int, epi: int):
             best = (cost, bn)
     if best is None:
         return None
-    return (0, best[1])
+    return (GEMM_SCHED, best[1])
 
 
 def _gemm_ok(x, w) -> bool:
