@@ -48,15 +48,16 @@ def paged_setup(B, ctx, Hkv, D, BS=16):
     return kc, vc, bt
 
 
-def case_decode(B=64, ctx=1000, Hq=32, Hkv=8, D=128):
-    kc, vc, bt = paged_setup(B, ctx, Hkv, D)
+def case_decode(B=64, ctx=1000, Hq=32, Hkv=8, D=128, BS=16):
+    kc, vc, bt = paged_setup(B, ctx, Hkv, D, BS)
     q = torch.randn(B, Hq, D, device=DEV, dtype=torch.bfloat16)
     cl = torch.full((B,), ctx, dtype=torch.int32, device=DEV)
-    bt_full = torch.zeros(B, 8192 // 16, dtype=torch.int32, device=DEV)
+    bt_full = torch.zeros(B, 8192 // BS, dtype=torch.int32, device=DEV)
     bt_full[:, : bt.shape[1]] = bt
     t = timeit(lambda: ops.paged_decode(q, kc, vc, bt_full, cl, 1 / math.sqrt(D)))
     byts = B * ctx * Hkv * D * 2 * 2
-    return {"case": f"paged_decode B{B} ctx{ctx} Hq{Hq} Hkv{Hkv} D{D}", "us": t * 1e6, "GB/s": byts / t / 1e9}
+    bs = "" if BS == 16 else f" BS{BS}"
+    return {"case": f"paged_decode B{B} ctx{ctx} Hq{Hq} Hkv{Hkv} D{D}{bs}", "us": t * 1e6, "GB/s": byts / t / 1e9}
 
 
 def case_prefill(B=32, L=1024, Hq=32, Hkv=8, D=128):
@@ -256,6 +257,8 @@ LLAMA8B_SHAPES = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]
 
 CASES = {
     "decode": lambda: [case_decode(), case_decode(B=128, ctx=1000), case_decode(B=8, ctx=3000)],
+    "decode_bs": lambda: [case_decode(B=128, ctx=1000, BS=bs) for bs in (16, 32, 64)] +
+                         [case_decode(B=64, ctx=1000, BS=bs) for bs in (16, 32, 64)],
     "prefill": lambda: [case_prefill(), case_prefill(B=8, L=4096), case_prefill_chunk()],
     "prefill_chunk": lambda: [case_prefill_chunk()],
     "encoder": lambda: [case_encoder_attn()],

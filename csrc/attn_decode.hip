@@ -20,6 +20,9 @@
 namespace {
 
 constexpr int kMaxSplit = 2048;  // max keys per workgroup (LDS block-table slice)
+#ifndef LK_DECODE_WG_PER_CU
+#define LK_DECODE_WG_PER_CU 3
+#endif
 typedef short4_t __attribute__((address_space(3))) * lds_s4_ptr;
 
 // v3 (streaming): workgroup = (split, kv_head, seq), 4 waves; each wave walks 32-key
@@ -34,7 +37,7 @@ typedef short4_t __attribute__((address_space(3))) * lds_s4_ptr;
 // The 4 waves' (m, l, O) are merged through LDS at the end; splits > 1 emit
 // partials for lk_decode_reduce (flash-decoding).
 template <int D, int G>
-__global__ __launch_bounds__(256, 2) void paged_decode_kernel(
+__global__ __launch_bounds__(256, LK_DECODE_WG_PER_CU) void paged_decode_kernel(
     const bf16_t* __restrict__ q, long qs, const bf16_t* __restrict__ kc,
     const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ctx_lens, bf16_t* __restrict__ out, long os,
@@ -126,13 +129,6 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(
       const int row = i * RPL + lane / CPR, ch = lane % CPR;
       *reinterpret_cast<short8*>(vw + row * D + ((ch ^ ((row & 7) << 1)) & (CPR - 1)) * 8) = vr[i];
     }
-    short8 kcur[2][KK];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) kcur[t][kk] = kr[t][kk];
-    if (c + 4 < nch) load_chunk(c + 4, kr, vr);  // next chunk in flight under the math
-
     // S^T tiles: lane (q = r16) holds keys 16t + 4*h4 + i
     floatx4 sc[2];
 #pragma unroll
@@ -140,8 +136,11 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(
       sc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk)
-        sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kcur[t][kk], qf[kk], sc[t], 0, 0, 0);
+        sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr[t][kk], qf[kk], sc[t], 0, 0, 0);
     }
+    // K consumed, V already in LDS: the next chunk's loads fly under softmax + PV (no
+    // second register set: 32 VGPRs fewer, three workgroups per CU)
+    if (c + 4 < nch) load_chunk(c + 4, kr, vr);
     float mx = -INFINITY;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
