@@ -32,8 +32,8 @@ VARIANTS = [int(v) for v in os.environ.get("LK_GEMM_VARIANTS", "0,1").split(",")
 BGE = [(2304, 768, "bias"), (768, 768, "bias"), (3072, 768, "gelu"), (768, 3072, "bias")]
 
 
-def cases(quick: bool):
-    ms = [4096] if quick else [2048, 3072, 3328, 3584, 3840, 4096, 8192]
+def cases(quick: bool, ms_override=None):
+    ms = ms_override or ([4096] if quick else [2048, 3072, 3328, 3584, 3840, 4096, 8192])
     for M in ms:
         for N, K, e in LLAMA:
             yield M, N, K, e
@@ -86,11 +86,12 @@ def main():
                     help="rotate over weight copies totalling > 2x the 256 MB MALL, as in serving (each layer's "
                          "weights arrive from HBM; the activations are fresh)")
     ap.add_argument("--llama-only", action="store_true")
+    ap.add_argument("--ms", default=None, help="comma-separated M values (Llama shapes)")
     a = ap.parse_args()
     L = ops.lib()
     torch.manual_seed(0)
     rows = []
-    for M, N, K, epi in cases(a.quick):
+    for M, N, K, epi in cases(a.quick, [int(v) for v in a.ms.split(",")] if a.ms else None):
         if a.llama_only and K == 768 or a.llama_only and N == 768:
             continue
         x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)

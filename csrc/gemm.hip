@@ -42,6 +42,8 @@
 //     8-byte packed, and SwiGLU pairs the gate / up fragments of the same columns in a lane;
 //   * tiles are visited in an XCD-aware order (bijective remap, 4 row tiles x all column
 //     tiles per group), so an XCD's ~32 concurrent tiles share their X / W K-slices in L2.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -50,7 +52,7 @@ namespace {
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 
-constexpr int kBM = 256, kBK = 64, kGroupM = 4;
+constexpr int kBM = 256, kBK = 64;
 constexpr int kSlotA = 128 * 128;  // an A slot: 128 rows x 128 B
 
 enum { EPI_NONE = 0, EPI_SWIGLU = 1, EPI_BIAS = 2, EPI_BIAS_GELU = 3, EPI_BIAS_RELU = 4 };
@@ -84,7 +86,7 @@ struct Geo {
 template <int NF, int EPI, int PH, int PRIO>
 __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W,
                                            const bf16_t* __restrict__ bias, int M, int K, int I,
-                                           bf16_t* __restrict__ out, long ldo, int TM, int TN) {
+                                           bf16_t* __restrict__ out, long ldo, int TM, int TN, int group_m) {
   using G = Geo<NF>;
   constexpr int BN = G::BN, NF0 = G::NF0, NF1 = G::NF1;
   static_assert(EPI != EPI_SWIGLU || NF == 4, "SwiGLU pairs fragments n and n+2");
@@ -93,9 +95,9 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
   // ---- tile of this block: XCD-contiguous logical ids, grouped 4 row tiles at a time
   const int nwg = TM * TN;
   const int L = xcd_remap(blockIdx.x, nwg);
-  const int per_group = kGroupM * TN;
-  const int first = (L / per_group) * kGroupM;
-  const int gm = min(TM - first, kGroupM);
+  const int per_group = group_m * TN;
+  const int first = (L / per_group) * group_m;
+  const int gm = min(TM - first, group_m);
   const int tm = first + (L % per_group) % gm;
   const int tn = (L % per_group) / gm;
 
@@ -378,8 +380,18 @@ template <int NF, int EPI, int PH, int PRIO>
 __global__ __launch_bounds__(512, 1) void gemm_kernel(const bf16_t* __restrict__ X, long ldx,
                                                       const bf16_t* __restrict__ W,
                                                       const bf16_t* __restrict__ bias, int M, int K, int I,
-                                                      bf16_t* __restrict__ out, long ldo, int TM, int TN) {
-  gemm8_body<NF, EPI, PH, PRIO>(X, ldx, W, bias, M, K, I, out, ldo, TM, TN);
+                                                      bf16_t* __restrict__ out, long ldo, int TM, int TN, int group_m) {
+  gemm8_body<NF, EPI, PH, PRIO>(X, ldx, W, bias, M, K, I, out, ldo, TM, TN, group_m);
+}
+
+// row tiles per XCD group of the tile order (LK_GEMM_GROUP_M, default 4)
+int group_rows() {
+  static const int g = [] {
+    const char* e = getenv("LK_GEMM_GROUP_M");
+    const int v = e ? atoi(e) : 4;
+    return v >= 1 ? v : 4;
+  }();
+  return g;
 }
 
 template <int NF, int EPI, int PH, int PRIO = 0>
@@ -392,7 +404,7 @@ void launch_ph(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, i
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  gemm_kernel<NF, EPI, PH, PRIO><<<TM * TN, 512, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN);
+  gemm_kernel<NF, EPI, PH, PRIO><<<TM * TN, 512, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, group_rows());
 }
 // schedule: 0 = 4 phases per K-tile (per-cluster priority), 1 = 2 phases (static priority)
 template <int NF, int EPI>
