@@ -86,7 +86,8 @@ struct Geo {
 template <int NF, int EPI, int PH, int PRIO>
 __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W,
                                            const bf16_t* __restrict__ bias, int M, int K, int I,
-                                           bf16_t* __restrict__ out, long ldo, int TM, int TN, int group_m) {
+                                           bf16_t* __restrict__ out, long ldo, int TM, int TN, int group_m,
+                                           int tile) {
   using G = Geo<NF>;
   constexpr int BN = G::BN, NF0 = G::NF0, NF1 = G::NF1;
   static_assert(EPI != EPI_SWIGLU || NF == 4, "SwiGLU pairs fragments n and n+2");
@@ -94,7 +95,7 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
 
   // ---- tile of this block: XCD-contiguous logical ids, grouped 4 row tiles at a time
   const int nwg = TM * TN;
-  const int L = xcd_remap(blockIdx.x, nwg);
+  const int L = xcd_remap(tile, nwg);
   const int per_group = group_m * TN;
   const int first = (L / per_group) * group_m;
   const int gm = min(TM - first, group_m);
@@ -381,7 +382,27 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const bf16_t* __restrict__
                                                       const bf16_t* __restrict__ W,
                                                       const bf16_t* __restrict__ bias, int M, int K, int I,
                                                       bf16_t* __restrict__ out, long ldo, int TM, int TN, int group_m) {
-  gemm8_body<NF, EPI, PH, PRIO>(X, ldx, W, bias, M, K, I, out, ldo, TM, TN, group_m);
+  // gridDim.x == TM * TN: one tile per workgroup; fewer: persistent workgroups walking the
+  // tiles b, b + grid, ... (same XCD: the grid is a multiple of 8), the epilogue stores of one
+  // tile drained before the next tile's LDS-DMA prologue (vmcnt counts stores too)
+  const int nwg = TM * TN;
+  for (int t = blockIdx.x; t < nwg; t += gridDim.x) {
+    gemm8_body<NF, EPI, PH, PRIO>(X, ldx, W, bias, M, K, I, out, ldo, TM, TN, group_m, t);
+    wait_vm<0>();
+  }
+}
+
+// persistent grid (LK_GEMM_PERSIST=1: one workgroup per CU walking the tiles) or one
+// workgroup per tile (default)
+int gemm_grid(int tiles) {
+  static const bool persist = [] {
+    const char* e = getenv("LK_GEMM_PERSIST");
+    return e && atoi(e) != 0;
+  }();
+  if (!persist) return tiles;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  return tiles < cus ? tiles : cus;
 }
 
 // row tiles per XCD group of the tile order (LK_GEMM_GROUP_M, default 4)
@@ -404,7 +425,8 @@ void launch_ph(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, i
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  gemm_kernel<NF, EPI, PH, PRIO><<<TM * TN, 512, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, group_rows());
+  gemm_kernel<NF, EPI, PH, PRIO><<<gemm_grid(TM * TN), 512, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN,
+                                                                   group_rows());
 }
 // schedule: 0 = 4 phases per K-tile (per-cluster priority), 1 = 2 phases (static priority)
 template <int NF, int EPI>
