@@ -256,6 +256,8 @@ def repeat_penalty_(logits, window, penalty):
 # LK_SKINNY_MAX_M now defaults to 0.
 SKINNY_MAX_M = int(os.environ.get("LK_SKINNY_MAX_M", "0"))
 LM_HEAD_SKINNY_MAX_M = 16
+# LM head (N >= 65536) at 16 < M <= 256: weight-streaming kernel (1) or the prefill GEMM (0)
+WS_LM_HEAD = os.environ.get("LK_WS_LM_HEAD", "0") == "1"
 WS_MAX_M = int(os.environ.get("LK_WS_MAX_M", "256"))
 WS_SWIGLU_MAX_M = 160
 
@@ -276,7 +278,9 @@ def _decode_gemm_kind(x, w, swiglu: bool) -> Optional[str]:
     if M <= SKINNY_MAX_M:
         return "skinny"
     if N >= 65536 and not swiglu:
-        return "skinny" if M <= LM_HEAD_SKINNY_MAX_M else None
+        if M <= LM_HEAD_SKINNY_MAX_M:
+            return "skinny"
+        return "ws" if WS_LM_HEAD and M <= WS_MAX_M else None
     if M <= (WS_SWIGLU_MAX_M if swiglu else WS_MAX_M):
         return "ws"
     return None
