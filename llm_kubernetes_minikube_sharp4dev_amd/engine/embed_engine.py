@@ -9,6 +9,7 @@ one HTTP round-trip per chunk (``RagIndex.cs:47``).
 from __future__ import annotations
 
 import itertools
+import os
 import threading
 import time
 from typing import Optional
@@ -17,6 +18,9 @@ import numpy as np
 import torch
 
 from ..utils import metrics as M
+
+# high-priority HIP streams for concurrent serving embeddings (one per in-flight micro-batch)
+EMBED_STREAMS = int(os.environ.get("LK_EMBED_STREAMS", "2"))
 
 
 class EmbeddingEngine:
@@ -102,7 +106,7 @@ class EmbeddingEngine:
             if getattr(self, "_streams", None) is None:
                 # high priority: a query embedding (a few ms of small kernels) is dispatched
                 # ahead of the queued kernels of the LLM engine's step instead of behind them
-                self._streams = [torch.cuda.Stream(self.device, priority=-1) for _ in range(2)]
+                self._streams = [torch.cuda.Stream(self.device, priority=-1) for _ in range(EMBED_STREAMS)]
                 self._next = 0
             st = self._streams[self._next]
             self._next = (self._next + 1) % len(self._streams)

@@ -11,6 +11,7 @@ queueing behind it."""
 from __future__ import annotations
 
 import asyncio
+import concurrent.futures
 from typing import Callable, Optional
 
 
@@ -22,6 +23,9 @@ class MicroBatcher:
         self.max_wait_s = max_wait_s
         self.max_inflight = max(1, max_inflight)
         self._sem: Optional[asyncio.Semaphore] = None
+        # the batches run on their own threads, never queued behind other work in the
+        # event loop's default executor
+        self._pool = concurrent.futures.ThreadPoolExecutor(self.max_inflight, thread_name_prefix="lk-batch")
         self._q: Optional[asyncio.Queue] = None
         self._task: Optional[asyncio.Task] = None
         self.batches = 0
@@ -60,7 +64,7 @@ class MicroBatcher:
     async def _batch(self, group):
         texts = [t for g in group for t in g[0]]
         try:
-            out = await asyncio.to_thread(self.fn, texts)
+            out = await asyncio.get_running_loop().run_in_executor(self._pool, self.fn, texts)
         except Exception as e:  # every waiter sees the failure
             for _, f in group:
                 if not f.done():

@@ -25,12 +25,14 @@ from fastapi import Request  # module level: FastAPI resolves string annotations
 
 import asyncio
 import json
+import os
 import time
 import uuid
 from datetime import datetime, timezone
 from typing import Any, Optional
 
 from ..engine.sampling import SamplingParams
+from ..utils import tracing
 from ..models.tokenizer import IncrementalDetokenizer
 from ..utils import metrics as M
 from ..utils.logging import get_logger
@@ -73,6 +75,17 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
 
     def err(status: int, msg: str):
         return JSONResponse({"error": msg}, status_code=status)
+
+    # loaded models are looked up on the event loop (a dict read); only a first request that
+    # has to LOAD a model hops to a worker thread.  (A thread hop per request queued 128
+    # concurrent lookups in the default executor in front of the embedding batches.)
+    async def _gen_handle(model: str):
+        h = mgr.generators.get(model)
+        return h if h is not None else await asyncio.to_thread(mgr.generator, model)
+
+    async def _emb_handle(model: str):
+        h = mgr.embedders.get(model)
+        return h if h is not None else await asyncio.to_thread(mgr.embedder, model)
 
     async def body_of(request: Request) -> dict:
         raw = await request.body()
@@ -171,7 +184,7 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
         if not model:
             return err(400, "model is required")
         try:
-            h = await asyncio.to_thread(mgr.generator, model)
+            h = await _gen_handle(model)
         except KeyError as e:
             return err(404, str(e).strip("'\""))
         prompt = b.get("prompt") or ""
@@ -210,7 +223,7 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
         if not model:
             return err(400, "model is required")
         try:
-            h = await asyncio.to_thread(mgr.generator, model)
+            h = await _gen_handle(model)
         except KeyError as e:
             return err(404, str(e).strip("'\""))
         msgs = b.get("messages") or []
@@ -240,11 +253,24 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
 
     async def _embed(model: str, texts: list[str]):
         """Concurrent requests for one model share packed encoder passes (MicroBatcher)."""
-        h = await asyncio.to_thread(mgr.embedder, model)
+        t0 = time.perf_counter()
+        h = await _emb_handle(model)
         b = batchers.get(h.name)
         if b is None:
-            b = batchers[h.name] = MicroBatcher(h.engine.embed_cpu, max_inflight=2)
+            from ..engine.embed_engine import EMBED_STREAMS
+
+            eng = h.engine
+
+            def run(texts, eng=eng):  # the batch's own time, apart from its queueing
+                t = time.perf_counter()
+                out = eng.embed_cpu(texts)
+                tracing.record("server", "embed_batch", time.perf_counter() - t, n=len(texts))
+                return out
+
+            b = batchers[h.name] = MicroBatcher(run, max_inflight=EMBED_STREAMS,
+                                                max_wait_s=float(os.environ.get("LK_EMBED_WAIT_MS", "2")) / 1e3)
         vec = await b.submit(texts) if texts else h.engine.embed_cpu(texts)
+        tracing.record("server", "embed_request", time.perf_counter() - t0)
         return h, vec.tolist()
 
     @app.post("/api/embeddings")
@@ -379,7 +405,7 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
         b = await body_of(request)
         model = b.get("model")
         try:
-            h = await asyncio.to_thread(mgr.generator, model)
+            h = await _gen_handle(model)
         except KeyError as e:
             return JSONResponse({"error": {"message": str(e), "type": "invalid_request_error"}}, status_code=404)
         system, prompt = _chat_to_prompt(b.get("messages") or [])
@@ -402,7 +428,7 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
         b = await body_of(request)
         model = b.get("model")
         try:
-            h = await asyncio.to_thread(mgr.generator, model)
+            h = await _gen_handle(model)
         except KeyError as e:
             return JSONResponse({"error": {"message": str(e)}}, status_code=404)
         ids = h.tokenizer.encode(b.get("prompt") or "", add_bos=True)
