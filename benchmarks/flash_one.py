@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """One flash-prefill shape, N launches (for rocprofv3 PMC passes): causal B8 L4096 or the
-in-situ chunk shape.  LK_PREFILL_WAVES / LK_PREFILL_PIPE select the kernel variant."""
+in-situ chunk shape.  LK_PREFILL_WAVES / LK_PREFILL_PIPE / LK_PREFILL_DEFER select the kernel variant."""
 import argparse
 import math
 import os

@@ -16,9 +16,14 @@
 //  * LDS images are XOR-swizzled per head dim so that the row reads (K) and the
 //    transposed reads (V) are bank-conflict free.
 //  * K/V for tile t+1 are loaded into registers while tile t is computed and
-//    written to LDS after the barrier (issue-early / write-late staging).
+//    written to LDS after the barrier (issue-early / write-late staging).  With PIPE the
+//    loop is software-pipelined by one tile (PV(t-1) next to the exponentials of tile t).
+//  * paged K/V come in through buffer loads whose descriptor is the cache block's
+//    (wave-uniform) base: the per-lane offset is a loop constant, the block-table lookup
+//    and the 64-bit base are scalar, so staging a tile costs no address VALU.
 //  * online softmax in the exp2 domain with the scale folded into one multiply.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
@@ -63,12 +68,13 @@ struct PrefillParams {
   // in the log2 domain of the split-K decode partials
   float* part_o;
   float* part_ml;
+  float defer;  // PIPE: move the running max only when it grows by more than this (log2 units)
 };
 
 // NW waves per workgroup (4 or 8): WH of them share a row group (one head each), and
 // NW / WH row groups of 32 queries sit on top of each other, all fed by the same staged
 // K/V tile -- with NW = 8 each K/V byte brought into LDS serves 2x the MFMA work.
-template <int D, bool CAUSAL, bool PAGED, int WH, int NW>
+template <int D, bool CAUSAL, bool PAGED, int WH, int NW, bool PIPE>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillParams p) {
   constexpr int NT = 64 * NW;      // threads
   constexpr int KK = D / 16;       // QK k-steps
@@ -81,8 +87,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
   static_assert(CPT >= 1 && NCH % NT == 0, "tile too small for the workgroup");
 
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * KT * D];
-  bf16_t* Ks = lds;
-  bf16_t* Vs = lds + KT * D;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -109,7 +113,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
   // Rows past the context re-read the last valid key (block clamped here, slot by the
   // clamped key): never a stale slot, whose bytes could be NaN under a zero P.
   const int kvh_u = blockIdx.y * WH / G;  // == head / G for every wave of the workgroup
-  auto paged_base = [&](int kt, int row) -> long {
+  auto paged_base = [&](int kt, int row) __attribute__((always_inline)) -> long {
     const int last = (ctx - 1) >> p.bs_shift;
     const int bi = __builtin_amdgcn_readfirstlane(min((kt + row) >> p.bs_shift, last));
     const long blk = p.block_tables[(long)b * p.bt_stride + bi];
@@ -133,35 +137,58 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
     for (int i = 0; i < 16; ++i) o[n][i] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
 
-  // ---- staging helpers: chunk c of the tile = (row c / CPR, col chunk c % CPR)
+  // ---- staging helpers: chunk c of the tile = (row c / CPR, col chunk c % CPR); CPR divides
+  // NT, so a lane's column chunk is the same for every i and its row advances by NT / CPR
   short8 kreg[CPT], vreg[CPT];
-  auto gload = [&](int kt) {
+  const int lch = tid % CPR, lrow = tid / CPR;
+  // paged, full tile: slot of row r = (kt & (BS-1)) + (r & (BS-1)) (no carry: kt is a multiple
+  // of KT, r < KT) -> a per-lane constant byte offset plus a scalar one
+  unsigned poff[CPT];
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) poff[i] = (unsigned)((((lrow + (NT / CPR) * i) & (p.BS - 1)) * D + lch * 8) * 2);
+  const int wrow0 = __builtin_amdgcn_readfirstlane(w) * (64 / CPR);  // first tile row a wave stages
+  auto paged_load = [&](const bf16_t* cache, long base, unsigned off, unsigned soff) __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(cache + base), (short)0, p.BS * D * 2, 0x00020000);
+    return __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rs, off, soff, 0));
+  };
+  // rows of one tile of the K or V cache -> registers
+  auto gload_one = [&](const bf16_t* cache, long dstride, int kt, short8* reg) __attribute__((always_inline)) {
+    if constexpr (PAGED) {
+      if (kt + KT <= ctx) {  // every row a valid key (uniform branch)
+        const unsigned soff = (unsigned)((kt & (p.BS - 1)) * D * 2);
+#pragma unroll
+        for (int i = 0; i < CPT; ++i)
+          reg[i] = paged_load(cache, paged_base(kt, wrow0 + (NT / CPR) * i), poff[i], soff);
+        return;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int c = tid + NT * i;
-      const int row = c / CPR, ch = c % CPR;
+      const int row = lrow + (NT / CPR) * i;
       const int key = min(kt + row, ctx - 1);  // clamp: masked later
-      const bf16_t *kp, *vp;
       if constexpr (PAGED) {
-        const long base = paged_base(kt, row);
-        const int loff = (key & (p.BS - 1)) * D + ch * 8;  // clamped key: a valid slot
-        kp = p.k + base + loff;
-        vp = p.v + base + loff;
+        const unsigned loff = (unsigned)(((key & (p.BS - 1)) * D + lch * 8) * 2);  // clamped key: a valid slot
+        reg[i] = paged_load(cache, paged_base(kt, row), loff, 0);
       } else {
-        kp = p.k + (long)(qbeg + key) * p.ks + (long)kvh * D + ch * 8;
-        vp = p.v + (long)(qbeg + key) * p.vs + (long)kvh * D + ch * 8;
+        reg[i] = *reinterpret_cast<const short8*>(cache + (long)(qbeg + key) * dstride + (long)kvh * D + lch * 8);
       }
-      kreg[i] = *reinterpret_cast<const short8*>(kp);
-      vreg[i] = *reinterpret_cast<const short8*>(vp);
     }
   };
-  auto swrite = [&]() {
+  auto gload_k = [&](int kt) __attribute__((always_inline)) { gload_one(p.k, p.ks, kt, kreg); };
+  auto gload_v = [&](int kt) __attribute__((always_inline)) { gload_one(p.v, p.vs, kt, vreg); };
+  auto swrite_k = [&](bf16_t* Ks) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int c = tid + NT * i;
-      const int row = c / CPR, ch = c % CPR;
-      *reinterpret_cast<short8*>(Ks + row * D + k_swz<D>(row, ch) * 8) = kreg[i];
-      *reinterpret_cast<short8*>(Vs + row * D + v_swz<D>(row, ch) * 8) = vreg[i];
+      const int row = lrow + (NT / CPR) * i;
+      *reinterpret_cast<short8*>(Ks + row * D + k_swz<D>(row, lch) * 8) = kreg[i];
+    }
+  };
+  auto swrite_v = [&](bf16_t* Vs) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int row = lrow + (NT / CPR) * i;
+      *reinterpret_cast<short8*>(Vs + row * D + v_swz<D>(row, lch) * 8) = vreg[i];
     }
   };
 
@@ -181,17 +208,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
     voff[n] = r0 * D + v_swz<D>(r0, c0 >> 3) * 8 + (c0 & 7);
   }
 
-  const int ntiles = (kend + KT - 1) / KT;
-  if (ntiles > 0) gload(0);
-  for (int t = 0; t < ntiles; ++t) {
-    const int kt = t * KT;
-    __syncthreads();  // everyone finished reading the previous tile
-    swrite();
-    __syncthreads();
-    if (t + 1 < ntiles) gload(kt + KT);
-
-    // ---- S^T = K . Q^T  for two 32-key halves
-    floatx16 s[2];
+  // ---- S^T = K . Q^T  for two 32-key halves
+  auto qk = [&](const bf16_t* Ks, floatx16* s) __attribute__((always_inline)) {
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
 #pragma unroll
@@ -202,11 +220,17 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
         s[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[kk], s[m], 0, 0, 0);
       }
     }
-
-    // ---- mask + online softmax (this lane = query row qrow; 32 of the 64 keys).
-    // One uniform branch for the (rare) boundary tiles; the row max is taken on the
-    // raw scores and scaled once, the scale is folded into the exp2 argument (FMA).
-    const bool need_mask = (kt + KT > ctx) || (CAUSAL && kt + KT - 1 > past + q0 + rg * 32);
+  };
+  // ---- mask + running max (this lane = query row qrow; 32 of the 64 keys).  One uniform
+  // branch for the (rare) boundary tiles; the row max is taken on the raw scores and scaled
+  // once.  Returns the rescale factor of the accumulated O / l; sets *base for exp_pack.
+  // PIPE: the max is only moved when it grows by more than p.defer (LK_PREFILL_DEFER, log2
+  // units: P <= 2^defer is as exact in bf16 and the f32 sums have the range), so after the
+  // first tiles alpha == 1 and O is not rescaled at all.
+  auto stats = [&](int kt, floatx16* s, float* base, auto may_mask) __attribute__((always_inline)) -> float {
+    bool need_mask = false;
+    if constexpr (decltype(may_mask)::value)
+      need_mask = (kt + KT > ctx) || (CAUSAL && kt + KT - 1 > past + q0 + rg * 32);
     float mx = -INFINITY;
     if (need_mask) {
 #pragma unroll
@@ -225,10 +249,17 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
         for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[m][i]);
     }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * p.scale_log2;
-    const float m_new = fmaxf(m_run, mx);
-    const float base = m_new == -INFINITY ? 0.f : m_new;
+    float m_new = fmaxf(m_run, mx);
+    if constexpr (PIPE) m_new = m_new > m_run + p.defer ? m_new : m_run;
+    *base = m_new == -INFINITY ? 0.f : m_new;
     // bare v_exp_f32 (softmax tolerates flushed denormals)
-    const float alpha = __builtin_amdgcn_exp2f(m_run - base);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - *base);
+    m_run = m_new;
+    return alpha;
+  };
+  // ---- P = exp2(s * scale - base), row sums into l, P^T fragments (B operand): k-step
+  // (m, s2) = regs 8*s2 .. 8*s2+7 of s[m]
+  auto exp_pack = [&](floatx16* s, float base, float alpha, short8 (*pf)[2]) __attribute__((always_inline)) {
     float rs = 0.f;
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -240,18 +271,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
       }
     rs += __shfl_xor(rs, 32, 64);
     l_run = l_run * alpha + rs;
-    m_run = m_new;
-    // rescale O only when some row's running max moved (wave-uniform branch; once the
-    // early tiles have found each row's max this is skipped)
-    if (!__all(alpha == 1.f)) {
-#pragma unroll
-      for (int n = 0; n < ND; ++n)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[n][i] *= alpha;
-    }
-
-    // ---- P^T fragments (B operand): k-step (m, s2) = regs 8*s2 .. 8*s2+7 of s[m]
-    short8 pf[2][2];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -261,9 +280,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
         for (int j = 0; j < 4; ++j) pk[j] = pack_bf2(s[m][8 * s2 + 2 * j], s[m][8 * s2 + 2 * j + 1]);
         pf[m][s2] = __builtin_bit_cast(short8, pk);
       }
-
-    // ---- O^T += V^T . P^T ; V^T fragments by transposed LDS reads.
-    // element j of lane-half h in k-step (m,s2) is key 32m + 16s2 + 8(j>>2) + 4h + (j&3)
+  };
+  // rescale O only when some row's running max moved (wave-uniform branch)
+  auto rescale = [&](float alpha) __attribute__((always_inline)) {
+    if (!__all(alpha == 1.f)) {
+#pragma unroll
+      for (int n = 0; n < ND; ++n)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[n][i] *= alpha;
+    }
+  };
+  // ---- O^T += V^T . P^T ; V^T fragments by transposed LDS reads.
+  // element j of lane-half h in k-step (m,s2) is key 32m + 16s2 + 8(j>>2) + 4h + (j&3)
+  auto pv = [&](const bf16_t* Vs, short8 (*pf)[2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int n = 0; n < ND; ++n) {
 #pragma unroll
@@ -278,6 +307,82 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
           o[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pf[m][s2], o[n], 0, 0, 0);
         }
     }
+  };
+
+  bf16_t* Ks = lds;
+  bf16_t* Vs = lds + KT * D;
+  const int ntiles = (kend + KT - 1) / KT;
+  floatx16 s[2];
+  short8 pf[2][2];
+  if constexpr (!PIPE) {
+    if (ntiles > 0) {
+      gload_k(0);
+      gload_v(0);
+    }
+    for (int t = 0; t < ntiles; ++t) {
+      const int kt = t * KT;
+      __syncthreads();  // everyone finished reading the previous tile
+      swrite_k(Ks);
+      swrite_v(Vs);
+      __syncthreads();
+      if (t + 1 < ntiles) {
+        gload_k(kt + KT);
+        gload_v(kt + KT);
+      }
+      qk(Ks, s);
+      float base;
+      const float alpha = stats(kt, s, &base, std::true_type{});
+      exp_pack(s, base, alpha, pf);
+      rescale(alpha);
+      pv(Vs, pf);
+    }
+  } else if (ntiles > 0) {
+    // Software-pipelined by one tile: iteration t runs QK(t), then PV(t-1) in the same basic
+    // block as the exponentials of tile t (independent work the scheduler interleaves: MFMA
+    // next to VALU within the wave), then O <- (O + P(t-1) V(t-1)) * alpha(t).  The LDS holds
+    // K(t) and V(t-1); after each tile K(t+1) and V(t) are written and K(t+2) / V(t+1) issued.
+    auto stage = [&](int t) __attribute__((always_inline)) {
+      __syncthreads();  // K(t) and V(t-1) read by everyone
+      if (t + 1 < ntiles) swrite_k(Ks);
+      swrite_v(Vs);
+      __syncthreads();
+      if (t + 2 < ntiles) gload_k((t + 2) * KT);
+      if (t + 1 < ntiles) gload_v((t + 1) * KT);
+    };
+    gload_k(0);
+    gload_v(0);
+    swrite_k(Ks);
+    if (ntiles > 1) gload_k(KT);
+    __syncthreads();
+    short8 pfp[2][2];
+    {
+      qk(Ks, s);
+      float base;
+      const float alpha = stats(0, s, &base, std::true_type{});
+      exp_pack(s, base, alpha, pfp);
+      stage(0);
+    }
+    auto step = [&](int t, auto may_mask) __attribute__((always_inline)) {
+      qk(Ks, s);
+      float base;
+      const float alpha = stats(t * KT, s, &base, may_mask);
+      pv(Vs, pfp);
+      exp_pack(s, base, alpha, pf);
+      rescale(alpha);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) pfp[m][s2] = pf[m][s2];
+      stage(t);
+    };
+    // leading tiles that no row of the workgroup masks: a branch-free body, so the row max
+    // is scheduled next to PV(t-1) too.  (Unrolling by two to swap pf / pfp instead of
+    // copying them takes the kernel to 256 VGPRs and spills.)
+    const int nfree = min(ntiles, min(ctx / KT, CAUSAL ? (past + q0 + 1) / KT : ntiles));
+    int t = 1;
+    for (; t < nfree; ++t) step(t, std::false_type{});
+    for (; t < ntiles; ++t) step(t, std::true_type{});
+    pv(Vs, pfp);
   }
 
   // ---- epilogue: O^T lane layout: d = 32n + (i&3) + 8(i>>2) + 4h, query row = qrow
@@ -325,6 +430,23 @@ static int prefill_waves(int G, int D) {
   return (G >= 4 && D >= 64 && env == 8) ? 8 : 4;
 }
 
+// LK_PREFILL_PIPE=1: the software-pipelined tile loop (PV(t-1) beside the exponentials of t)
+static bool prefill_pipe() {
+  static const bool env = [] {
+    const char* e = getenv("LK_PREFILL_PIPE");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return env;
+}
+
+static float prefill_defer() {
+  static const float env = [] {
+    const char* e = getenv("LK_PREFILL_DEFER");
+    return e ? (float)atof(e) : 8.f;
+  }();
+  return env;
+}
+
 int lk_prefill_rows_per_tile(int G) { return G >= 4 ? 32 * (prefill_waves(G, 128) / 4) : 32 * (4 / G); }
 
 int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v, long ks, long vs,
@@ -342,16 +464,20 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
   int bs_shift = 0;
   while ((1 << bs_shift) < BS) ++bs_shift;
   PrefillParams pr{q, qs, k, v, ks, vs, block_tables, bt_stride, cu_q, ctx_lens, tile_seq,
-                   tile_q0, out, os, Hq, Hkv, BS, bs_shift, scale * 1.4426950408889634f, part_o, part_ml};
+                   tile_q0, out, os, Hq, Hkv, BS, bs_shift, scale * 1.4426950408889634f, part_o, part_ml,
+                   part_o ? 0.f : prefill_defer()};
   const int WH = G >= 4 ? 4 : G;
   const int NW = prefill_waves(G, D);
   dim3 grid(ntiles, Hq / WH);
-#define L(DD, C, PG, W, N) flash_prefill_kernel<DD, C, PG, W, N><<<grid, 64 * N, 0, st>>>(pr)
+  const bool pipe = causal && prefill_pipe();
+#define L(DD, C, PG, W, N)                                                        \
+  if (pipe) flash_prefill_kernel<DD, C, PG, W, N, true><<<grid, 64 * N, 0, st>>>(pr); \
+  else flash_prefill_kernel<DD, C, PG, W, N, false><<<grid, 64 * N, 0, st>>>(pr)
 #define BY_W(DD, C, PG)                                 \
-  if (WH == 4 && NW == 8) L(DD, C, PG, 4, (DD >= 64 ? 8 : 4));   \
-  else if (WH == 4) L(DD, C, PG, 4, 4);                 \
-  else if (WH == 2) L(DD, C, PG, 2, 4);                 \
-  else L(DD, C, PG, 1, 4);
+  if (WH == 4 && NW == 8) { L(DD, C, PG, 4, (DD >= 64 ? 8 : 4)); } \
+  else if (WH == 4) { L(DD, C, PG, 4, 4); }                   \
+  else if (WH == 2) { L(DD, C, PG, 2, 4); }                   \
+  else { L(DD, C, PG, 1, 4); }
 #define BY_MODE(DD)                                    \
   if (causal && paged) { BY_W(DD, true, true) }        \
   else if (causal && !paged) { BY_W(DD, true, false) } \

@@ -97,11 +97,27 @@ def test_pipelined_steps_equal_synchronous(graphs):
         assert drive(True, mk) == ref
 
 
+def _assert_same_or_near_tie(hf, prompts, got, ref):
+    """Greedy sequences from two bf16 paths that sum attention in a different order: equal,
+    or first apart at a step where the fp32 model itself rates the two tokens within the
+    engine's logit error (0.05 * max|logit|, test_llama_gpu_logits_match_hf_fp32) -- a tie
+    the rounding may break either way, not a wrong attention result."""
+    for p, g, r in zip(prompts, got, ref):
+        if g == r:
+            continue
+        k = next(i for i, (a, b) in enumerate(zip(g, r)) if a != b)
+        with torch.no_grad():
+            want = hf(torch.tensor([p + r[:k]])).logits[0, -1]
+        gap = abs(want[g[k]] - want[r[k]]).item()
+        assert gap < 0.05 * want.abs().max().item() + 0.05, (k, g[k], r[k], gap)
+
+
 def test_cascade_decode_engine_matches_plain(monkeypatch):
     """Requests sharing a long prompt prefix (prefix-cache hits on the same blocks) decode
     with the cascade path (shared blocks attended once per step) -- eager and graphed --
-    to the same tokens as engines with cascade off."""
-    _, m = _gpu_llama()
+    to the same tokens as engines with cascade off (up to a near-tie, see
+    _assert_same_or_near_tie)."""
+    hf, m = _gpu_llama()
     base = list(range(40, 40 + 70))
     prompts = [base + [300 + i, 7, 9 + i] for i in range(6)]
 
@@ -118,8 +134,8 @@ def test_cascade_decode_engine_matches_plain(monkeypatch):
         return [s.output_ids for s in seqs]
 
     ref = run(False, False)
-    assert run(True, False) == ref
-    assert run(True, True) == ref
+    _assert_same_or_near_tie(hf, prompts, run(True, False), ref)
+    _assert_same_or_near_tie(hf, prompts, run(True, True), ref)
 
 
 def test_bert_gpu_matches_hf_fp32():

@@ -178,9 +178,12 @@ def test_cascade_decode(hip, G, D, S):
 
 @pytest.mark.parametrize("G", [1, 2, 4, 8])
 @pytest.mark.parametrize("D", [64, 128])
-def test_flash_prefill_paged(G, D):
+@pytest.mark.parametrize("BS", [8, 16, 128])
+def test_flash_prefill_paged(G, D, BS):
+    """Paged K/V through the block table for cache blocks smaller than, equal to a wave's
+    staged rows and larger than a key tile (BS 128: a scalar in-block offset on odd tiles)."""
     torch.manual_seed(7)
-    Hkv, BS = 2, 16
+    Hkv = 2
     Hq = Hkv * G
     q_lens = [1, 33, 100, 257, 64]
     past = [0, 5, 0, 40, 700]
