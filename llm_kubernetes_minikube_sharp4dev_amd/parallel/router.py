@@ -50,21 +50,34 @@ class ReplicaPool:
 
 
 def create_router_app(urls: list[str], probe_interval_s: float = 5.0, timeout_s: float = 600.0):
-    import httpx
+    """The router ASGI app.  Upstream calls go through one aiohttp session per event loop
+    (an unbounded keep-alive pool): httpx's pool scans grow with the connections in flight
+    and took a whole core at 128 concurrent streams in the RAG app (profiles/r2_http_bench.md)."""
+    import aiohttp
     from fastapi import FastAPI
     from fastapi.responses import JSONResponse, Response, StreamingResponse
 
     pool = ReplicaPool(urls)
     app = FastAPI(title="MI355X DP router")
     app.state.pool = pool
-    client = httpx.AsyncClient(timeout=timeout_s)
+    sessions: dict = {}
+
+    def session() -> "aiohttp.ClientSession":
+        loop = asyncio.get_running_loop()
+        s = sessions.get(loop)
+        if s is None or s.closed:
+            s = sessions[loop] = aiohttp.ClientSession(
+                timeout=aiohttp.ClientTimeout(total=timeout_s),
+                connector=aiohttp.TCPConnector(limit=0, keepalive_timeout=60))
+        return s
 
     async def probe_loop():
         while True:
             await asyncio.sleep(probe_interval_s)
             for r in pool.replicas:
                 try:
-                    ok = (await client.get(r.url + "/api/version", timeout=2.0)).status_code == 200
+                    async with session().get(r.url + "/api/version", timeout=aiohttp.ClientTimeout(total=2.0)) as resp:
+                        ok = resp.status == 200
                 except Exception:
                     ok = False
                 if ok and not r.healthy:
@@ -75,6 +88,13 @@ def create_router_app(urls: list[str], probe_interval_s: float = 5.0, timeout_s:
     @app.on_event("startup")
     async def _start():
         app.state.probe = asyncio.create_task(probe_loop())
+
+    @app.on_event("shutdown")
+    async def _stop():
+        app.state.probe.cancel()
+        for s in list(sessions.values()):
+            await s.close()
+        sessions.clear()
 
     @app.get("/router/status")
     async def status():
@@ -92,9 +112,8 @@ def create_router_app(urls: list[str], probe_interval_s: float = 5.0, timeout_s:
             tried.add(r.url)
             r.inflight += 1
             try:
-                req = client.build_request(request.method, f"{r.url}/{path}", content=body, headers=headers,
-                                           params=dict(request.query_params))
-                resp = await client.send(req, stream=True)
+                resp = await session().request(request.method, f"{r.url}/{path}", data=body or None, headers=headers,
+                                               params=list(request.query_params.multi_items()))
             except Exception:
                 r.inflight -= 1
                 pool.mark_failed(r)
@@ -102,17 +121,17 @@ def create_router_app(urls: list[str], probe_interval_s: float = 5.0, timeout_s:
 
             async def relay(resp=resp, rep=r):
                 try:
-                    async for chunk in resp.aiter_raw():
+                    async for chunk in resp.content.iter_any():
                         yield chunk
                 finally:
-                    await resp.aclose()
+                    resp.release()
                     rep.inflight -= 1
                     rep.served += 1
 
             media = resp.headers.get("content-type")
             if media and "ndjson" in media:
-                return StreamingResponse(relay(), status_code=resp.status_code, media_type=media)
+                return StreamingResponse(relay(), status_code=resp.status, media_type=media)
             data = b"".join([c async for c in relay()])
-            return Response(data, status_code=resp.status_code, media_type=media)
+            return Response(data, status_code=resp.status, media_type=media)
 
     return app

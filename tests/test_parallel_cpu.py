@@ -493,3 +493,70 @@ def test_context_parallel_attention_matches_single_process(world):
         for r in range(world):
             got = torch.load(f"{out}.{r}", weights_only=True)
             torch.testing.assert_close(got, ref, atol=2e-5, rtol=2e-5)
+
+
+def _serve_in_thread(app):
+    """uvicorn on a free 127.0.0.1 port in a daemon thread; returns (url, server)."""
+    import socket
+    import threading
+    import time
+
+    import uvicorn
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    srv = uvicorn.Server(uvicorn.Config(app, host="127.0.0.1", port=port, log_level="warning"))
+    threading.Thread(target=srv.run, daemon=True).start()
+    t0 = time.time()
+    while not srv.started:
+        assert time.time() - t0 < 20, "replica did not start"
+        time.sleep(0.02)
+    return f"http://127.0.0.1:{port}", srv
+
+
+def test_router_proxies_streams_and_fails_over():
+    """The router in front of one live replica and one dead URL: NDJSON streams pass through
+    chunk by chunk, JSON routes are answered, the dead replica leaves the rotation after its
+    first failed request and in-flight counts return to zero."""
+    import json
+    import socket
+
+    from fastapi import FastAPI
+    from fastapi.responses import StreamingResponse
+    from fastapi.testclient import TestClient
+
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.router import create_router_app
+
+    rep = FastAPI()
+
+    @rep.get("/api/version")
+    async def version():
+        return {"version": "0.0-test"}
+
+    @rep.post("/api/generate")
+    async def generate(body: dict):
+        async def gen():
+            for i in range(3):
+                yield json.dumps({"response": f"{body['prompt']}{i}", "done": False}) + "\n"
+            yield json.dumps({"response": "", "done": True}) + "\n"
+        return StreamingResponse(gen(), media_type="application/x-ndjson")
+
+    live, srv = _serve_in_thread(rep)
+    with socket.socket() as so:  # a port nobody listens on
+        so.bind(("127.0.0.1", 0))
+        dead = f"http://127.0.0.1:{so.getsockname()[1]}"
+    try:
+        app = create_router_app([dead, live], probe_interval_s=3600)
+        with TestClient(app) as c:
+            for k in range(4):
+                r = c.post("/api/generate", json={"model": "m", "prompt": f"p{k}"})
+                assert r.status_code == 200 and "ndjson" in r.headers["content-type"]
+                lines = [json.loads(x) for x in r.text.splitlines()]
+                assert [x["response"] for x in lines] == [f"p{k}0", f"p{k}1", f"p{k}2", ""] and lines[-1]["done"]
+            assert c.get("/api/version").json() == {"version": "0.0-test"}
+            st = {x["url"]: x for x in c.get("/router/status").json()["replicas"]}
+            assert not st[dead]["healthy"] and st[dead]["failures"] == 1
+            assert st[live]["served"] == 5 and st[live]["inflight"] == 0 and st[dead]["inflight"] == 0
+    finally:
+        srv.should_exit = True
