@@ -230,6 +230,11 @@ def main(argv=None):
     import faulthandler
 
     faulthandler.enable(all_threads=True)
+    # GIL hand-off interval of the serving processes (Python's default is 5 ms: an event loop
+    # waking up while the engine thread runs Python waits up to that long for the GIL, per hop)
+    sw = os.environ.get("LK_GIL_SWITCH_US")
+    if sw:
+        sys.setswitchinterval(float(sw) / 1e6)
     ap = argparse.ArgumentParser(prog="llm_kubernetes_minikube_sharp4dev_amd")
     sub = ap.add_subparsers(dest="cmd", required=True)
 
