@@ -29,14 +29,17 @@ EPI = {"none": 0, "swiglu": 1, "bias": 2, "gelu": 3, "relu": 4}
 # the LM head is not here (M <= 256: weight-streaming regime), bge-base encoder layers
 LLAMA = [(6144, 4096, "none"), (4096, 4096, "none"), (28672, 4096, "swiglu"), (4096, 14336, "none")]
 VARIANTS = [int(v) for v in os.environ.get("LK_GEMM_VARIANTS", "0,1").split(",")]
+SPLITS = [int(v) for v in os.environ.get("LK_GEMM_SPLITS", "1").split(",")]
 BGE = [(2304, 768, "bias"), (768, 768, "bias"), (3072, 768, "gelu"), (768, 3072, "bias")]
 
 
-def cases(quick: bool, ms_override=None):
+def cases(quick: bool, ms_override=None, shapes=None):
     ms = ms_override or ([4096] if quick else [2048, 3072, 3328, 3584, 3840, 4096, 8192])
     for M in ms:
-        for N, K, e in LLAMA:
+        for N, K, e in (shapes or LLAMA):
             yield M, N, K, e
+    if shapes:
+        return
     for M in ([32768] if quick else [16384, 32768, 65536]):
         for N, K, e in BGE:
             yield M, N, K, e
@@ -87,11 +90,13 @@ def main():
                          "weights arrive from HBM; the activations are fresh)")
     ap.add_argument("--llama-only", action="store_true")
     ap.add_argument("--ms", default=None, help="comma-separated M values (Llama shapes)")
+    ap.add_argument("--shapes", default=None, help="N:K:epi,... instead of the Llama-3-8B projections (no bge rows)")
     a = ap.parse_args()
     L = ops.lib()
     torch.manual_seed(0)
     rows = []
-    for M, N, K, epi in cases(a.quick, [int(v) for v in a.ms.split(",")] if a.ms else None):
+    shapes = [(int(t.split(":")[0]), int(t.split(":")[1]), t.split(":")[2]) for t in a.shapes.split(",")] if a.shapes else None
+    for M, N, K, epi in cases(a.quick, [int(v) for v in a.ms.split(",")] if a.ms else None, shapes):
         if a.llama_only and K == 768 or a.llama_only and N == 768:
             continue
         x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
@@ -110,9 +115,10 @@ def main():
         refv = ref_fp32(x[rs], w, b, epi)
         best = None
         t_lib = []
-        cfgs = [(v, bn) for v in VARIANTS for bn in bns]
+        cfgs = [(v, bn, sp) for v in VARIANTS for bn in bns for sp in SPLITS
+                if L.gemm_supported(M, N, K, EPI[epi], bn, sp)]
         t_ours = {c: [] for c in cfgs}
-        fns = {c: (lambda c=c: L.gemm(x, wnext(), b, EPI[epi], c[1], None, c[0])) for c in cfgs}
+        fns = {c: (lambda c=c: L.gemm(x, wnext(), b, EPI[epi], c[1], None, c[0], c[2])) for c in cfgs}
         for bn in cfgs:
             y = fns[bn]()
             err = (y[rs].float() - refv).abs().max().item()
@@ -138,7 +144,8 @@ def main():
         row = {"M": M, "N": N, "K": K, "epi": epi, "ours_us": round(best[1], 1), "bn": best[0],
                "ours_TF": round(flops / best[1] / 1e6, 0), "lib_us": round(tl, 1),
                "lib_TF": round(flops / tl / 1e6, 0), "speedup": round(tl / best[1], 3),
-               "per_cfg_us": {f"v{c[0]}/{c[1]}": round(statistics.median(v), 1) for c, v in t_ours.items()}}
+               "per_cfg_us": {f"v{c[0]}/{c[1]}" + (f"/k{c[2]}" if c[2] > 1 else ""): round(statistics.median(v), 1)
+                              for c, v in t_ours.items()}}
         rows.append(row)
         print(json.dumps(row), flush=True)
         del x, w, b, wcopies
@@ -147,7 +154,7 @@ def main():
             f.write("| M | N | K | epilogue | ours us | variant/tile N | ours TF/s | hipBLASLt us | hipBLASLt TF/s | speedup |\n")
             f.write("|---|---|---|---|---|---|---|---|---|---|\n")
             for r in rows:
-                f.write(f"| {r['M']} | {r['N']} | {r['K']} | {r['epi']} | {r['ours_us']} | v{r['bn'][0]}/{r['bn'][1]} | {r['ours_TF']:.0f} | "
+                f.write(f"| {r['M']} | {r['N']} | {r['K']} | {r['epi']} | {r['ours_us']} | v{r['bn'][0]}/{r['bn'][1]}/k{r['bn'][2]} | {r['ours_TF']:.0f} | "
                         f"{r['lib_us']} | {r['lib_TF']:.0f} | {r['speedup']:.3f} |\n")
             sp = [r["speedup"] for r in rows]
             f.write(f"\nspeedup: min {min(sp):.3f}, median {statistics.median(sp):.3f}; "

@@ -235,13 +235,13 @@ at::Tensor ws_linear_rope_kv(const at::Tensor& x, const at::Tensor& w, const at:
 // Prefill / encoder-regime linear (csrc/gemm.hip): epi(x [M, K] . w[N, K]^T (+ bias)).
 // epi 0 none, 1 SwiGLU (w = [Wg; Wu], out [M, N/2]), 2 bias, 3 bias+GELU(erf), 4 bias+ReLU.
 at::Tensor gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t epi,
-                int64_t bn, const c10::optional<at::Tensor>& out_, int64_t variant) {
+                int64_t bn, const c10::optional<at::Tensor>& out_, int64_t variant, int64_t splits) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_LASTDIM(x); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "x [M,K], w [N,K]");
   check_rows16(x, "x"); check_rows16(w, "w");
   const int M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(lk_gemm_supported(M, N, K, (int)epi, (int)bn), "gemm: unsupported shape M", M, " N", N, " K", K,
-              " epi", epi, " bn", bn);
+  TORCH_CHECK(lk_gemm_supported(M, N, K, (int)epi, (int)bn, (int)splits), "gemm: unsupported shape M", M, " N", N,
+              " K", K, " epi", epi, " bn", bn, " splits", splits);
   if (epi >= 2) {
     TORCH_CHECK(bias.has_value(), "gemm: this epilogue needs a bias");
     CHECK_CUDA(*bias); CHECK_BF16(*bias); CHECK_CONTIG(*bias);
@@ -252,14 +252,17 @@ at::Tensor gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at
   CHECK_BF16(out); CHECK_LASTDIM(out);
   TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == n_out, "out shape");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 8 == 0 && out.stride(0) % 4 == 0, "out alignment");
+  // split-K partials: fp32 [splits, M, N] from the caching allocator (stream-ordered reuse)
+  at::Tensor ws;
+  if (splits > 1) ws = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
   int rc = lk_gemm(bp(x), x.stride(0), bp(w), epi >= 2 ? bp(*bias) : nullptr, M, N, K, (int)epi, (int)bn, (int)variant, bp(out),
-                   out.stride(0), cur_stream());
+                   out.stride(0), cur_stream(), (int)splits, splits > 1 ? ws.data_ptr<float>() : nullptr);
   CHECK_RC(rc, "gemm");
   return out;
 }
 
-bool gemm_supported(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bn) {
-  return lk_gemm_supported((int)M, (int)N, (int)K, (int)epi, (int)bn) != 0;
+bool gemm_supported(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bn, int64_t splits) {
+  return lk_gemm_supported((int)M, (int)N, (int)K, (int)epi, (int)bn, (int)splits) != 0;
 }
 
 std::vector<int64_t> ws_plan(int64_t M, int64_t N, int64_t K, bool swiglu) {
@@ -657,8 +660,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("splits") = 0, py::arg("out") = py::none());
   m.def("ws_plan", &ws_plan);
   m.def("gemm", &gemm, "", py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("epi") = 0,
-        py::arg("bn") = 256, py::arg("out") = py::none(), py::arg("variant") = 1);
-  m.def("gemm_supported", &gemm_supported);
+        py::arg("bn") = 256, py::arg("out") = py::none(), py::arg("variant") = 1,
+        py::arg("splits") = 1);
+  m.def("gemm_supported", &gemm_supported, "", py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bn"),
+        py::arg("splits") = 1);
   m.def("silu_mul", &silu_mul, "", py::arg("x"), py::arg("out") = py::none());
   m.def("activation_", &activation_);
   m.def("rope_kv_", &rope_kv_);

@@ -55,7 +55,7 @@ typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 constexpr int kBM = 256, kBK = 64;
 constexpr int kSlotA = 128 * 128;  // an A slot: 128 rows x 128 B
 
-enum { EPI_NONE = 0, EPI_SWIGLU = 1, EPI_BIAS = 2, EPI_BIAS_GELU = 3, EPI_BIAS_RELU = 4 };
+enum { EPI_NONE = 0, EPI_SWIGLU = 1, EPI_BIAS = 2, EPI_BIAS_GELU = 3, EPI_BIAS_RELU = 4, EPI_PARTIAL = 5 };
 
 LK_DEVICE int swz(int row) { return (row >> 1) & 7; }
 template <int N>
@@ -130,6 +130,9 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)W, (short)0, (int)min((long)(EPI == EPI_SWIGLU ? 2 * I : TN * BN) * K * 2, 0x7FFFFFF0L), 0x00020000);
   const int lr = lane >> 3, lc = lane & 7;
+  // split-K (gridDim.y = splits): this workgroup's K-tiles [kt0, kt0 + nk)
+  const int nkt = K / kBK, kz = blockIdx.y, ks = gridDim.y;
+  const int kt0 = kz * nkt / ks, nk = (kz + 1) * nkt / ks - kt0;
   unsigned aoff[2][2], b0off[2], b1off[G::G_B1];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -148,8 +151,8 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
     const int s = 8 * G::G_B1 * w + 8 * i + lr;
     b1off[i] = (unsigned)(wrow(b1_row(s)) * K * 2) + ((lc ^ swz(s)) << 4);
   }
-  auto dma = [](__amdgpu_buffer_rsrc_t rs, unsigned off, int kt, unsigned char* dst) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, (unsigned)kt * kBK * 2, 0, 0);
+  auto dma = [&](__amdgpu_buffer_rsrc_t rs, unsigned off, int kt, unsigned char* dst) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, (unsigned)(kt0 + kt) * kBK * 2, 0, 0);
   };
   auto issue_a = [&](int h, int kt) {
     unsigned char* d = smem + (kt & 1) * G::BUF + (h ? G::OFF_A1 : G::OFF_A0) + 16 * w * 128;
@@ -222,7 +225,6 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
     if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
   };
 
-  const int nk = K / kBK;
   if constexpr (PH == 2) {
     // 2 phases per K-tile: X = m-half 0 x both n-halves (32 MFMAs), Y = m-half 1.  SA0/SB0/SB1
     // of K-tile t+1 are staged in X(t) (their buffer's previous tile was last read in X(t-1)),
@@ -320,7 +322,17 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
   if (wr == 0) seg_barrier();  // equal barrier counts for both halves
 
   // ---- epilogue: lane holds row (.. + r), columns (.. + 4g + v), v = 0..3
-  if constexpr (EPI == EPI_SWIGLU) {
+  if constexpr (EPI == EPI_PARTIAL) {  // fp32 partial sums of split kz: out is float [splits, M, ldo]
+    float* part = reinterpret_cast<float*>(out) + (long)kz * M * ldo;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int row = tm * kBM + wr * 128 + m * 16 + r;
+      if (row >= M) continue;
+#pragma unroll
+      for (int n = 0; n < NF; ++n)
+        *reinterpret_cast<floatx4*>(part + (long)row * ldo + tn * BN + wc * 16 * NF + n * 16 + 4 * g) = acc[m][n];
+    }
+  } else if constexpr (EPI == EPI_SWIGLU) {
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int row = tm * kBM + wr * 128 + m * 16 + r;
@@ -377,6 +389,34 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
   }
 }
 
+// split-K reduction: out[r, c..c+3] = epi(sum_z part[z, r, c..c+3] (+ bias)), rounded like the
+// fused epilogues; one thread per 4 columns
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N,
+                                                            const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
+                                                            long ldo) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nq = N / 4;
+  if (i >= (long)M * nq) return;
+  const int row = (int)(i / nq), col = (int)(i % nq) * 4;
+  const long MN = (long)M * N;
+  floatx4 a = *reinterpret_cast<const floatx4*>(part + (long)row * N + col);
+  for (int z = 1; z < S; ++z) a += *reinterpret_cast<const floatx4*>(part + z * MN + (long)row * N + col);
+  float y[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    float e = a[v];
+    if constexpr (EPI != EPI_NONE) e = rbf(e + bf2f(bias[col + v]));
+    if constexpr (EPI == EPI_BIAS_GELU) e = lk_gelu_erf(e);
+    if constexpr (EPI == EPI_BIAS_RELU) e = fmaxf(e, 0.f);
+    y[v] = e;
+  }
+  uint2 pk;
+  pk.x = pack_bf2(y[0], y[1]);
+  pk.y = pack_bf2(y[2], y[3]);
+  *reinterpret_cast<uint2*>(out + (long)row * ldo + col) = pk;
+}
+
 template <int NF, int EPI, int PH, int PRIO>
 __global__ __launch_bounds__(512, 1) void gemm_kernel(const bf16_t* __restrict__ X, long ldx,
                                                       const bf16_t* __restrict__ W,
@@ -417,7 +457,7 @@ int group_rows() {
 
 template <int NF, int EPI, int PH, int PRIO = 0>
 void launch_ph(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
-               long ldo, int TM, int TN, hipStream_t st) {
+               long ldo, int TM, int TN, int ks, hipStream_t st) {
   constexpr int lds = 2 * Geo<NF>::BUF;
   static bool attr = false;
   if (!attr) {
@@ -425,21 +465,36 @@ void launch_ph(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, i
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  gemm_kernel<NF, EPI, PH, PRIO><<<gemm_grid(TM * TN), 512, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN,
-                                                                   group_rows());
+  gemm_kernel<NF, EPI, PH, PRIO><<<dim3(gemm_grid(TM * TN), ks), 512, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo,
+                                                                              TM, TN, group_rows());
 }
 // schedule: 0 = 4 phases per K-tile (per-cluster priority), 1 = 2 phases (static priority)
 template <int NF, int EPI>
 void launch(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
-            long ldo, int TM, int TN, int sched, hipStream_t st) {
-  if (sched == 1) launch_ph<NF, EPI, 2, 1>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, st);
-  else launch_ph<NF, EPI, 4, 0>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, st);
+            long ldo, int TM, int TN, int sched, hipStream_t st, int ks = 1) {
+  if (sched == 1) launch_ph<NF, EPI, 2, 1>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
+  else launch_ph<NF, EPI, 4, 0>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
 }
 
 template <int NF>
 int dispatch(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi,
-             int sched, bf16_t* out, long ldo, hipStream_t st) {
+             int sched, int ks, float* ws, bf16_t* out, long ldo, hipStream_t st) {
   const int TM = (M + kBM - 1) / kBM;
+  if (ks > 1) {  // fp32 partials of ks K-ranges into ws [ks, M, N], then the reduce applies the epilogue
+    constexpr int BN = 64 * NF;
+    if (epi == EPI_SWIGLU || N % BN || ws == nullptr || (epi != EPI_NONE && bias == nullptr)) return -1;
+    launch<NF, EPI_PARTIAL>(x, ldx, w, nullptr, M, K, 0, reinterpret_cast<bf16_t*>(ws), N, TM, N / BN, sched, st, ks);
+    const long n = (long)M * (N / 4);
+    const int blocks = (int)((n + 255) / 256);
+    switch (epi) {
+      case EPI_NONE: splitk_reduce_kernel<EPI_NONE><<<blocks, 256, 0, st>>>(ws, ks, M, N, bias, out, ldo); break;
+      case EPI_BIAS: splitk_reduce_kernel<EPI_BIAS><<<blocks, 256, 0, st>>>(ws, ks, M, N, bias, out, ldo); break;
+      case EPI_BIAS_GELU: splitk_reduce_kernel<EPI_BIAS_GELU><<<blocks, 256, 0, st>>>(ws, ks, M, N, bias, out, ldo); break;
+      case EPI_BIAS_RELU: splitk_reduce_kernel<EPI_BIAS_RELU><<<blocks, 256, 0, st>>>(ws, ks, M, N, bias, out, ldo); break;
+      default: return -1;
+    }
+    return 0;
+  }
   if (epi == EPI_SWIGLU) {
     if constexpr (NF != 4) {
       return -1;
@@ -464,8 +519,9 @@ int dispatch(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int
 
 }  // namespace
 
-int lk_gemm_supported(int M, int N, int K, int epi, int bn) {
+int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks) {
   if (M < 1 || K < kBK || K % kBK || (bn != 192 && bn != 256)) return 0;
+  if (ks < 1 || ks > 8 || K / kBK < 2 * ks || (ks > 1 && (epi == EPI_SWIGLU || N % 4))) return 0;
   if (epi == EPI_SWIGLU) return bn == 256 && N % 2 == 0 && (N / 2) % 128 == 0;
   return epi >= EPI_NONE && epi <= EPI_BIAS_RELU && N % bn == 0;
 }
@@ -475,8 +531,8 @@ int lk_gemm_supported(int M, int N, int K, int epi, int bn) {
 // N % bn == 0 (SwiGLU: bn = 256 and I = N/2 % 128 == 0), 16-B aligned X / W rows and
 // 8-B aligned output rows; any M >= 1.
 int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
-            int variant, bf16_t* out, long ldo, hipStream_t st) {
-  if (!lk_gemm_supported(M, N, K, epi, bn) || ldx % 8 || ldo % 4) return -1;
+            int variant, bf16_t* out, long ldo, hipStream_t st, int ks, float* ws) {
+  if (!lk_gemm_supported(M, N, K, epi, bn, ks) || ldx % 8 || ldo % 4) return -1;
   // operands are addressed through 32-bit buffer offsets: W must fit, X is cut into row chunks
   if ((long)N * K * 2 >= 0x7FFFFFF0L) return -1;
   const long max_rows = (0x7FFFFFF0L / (ldx * 2)) / kBM * kBM;
@@ -484,14 +540,14 @@ int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int 
     if (max_rows < kBM) return -1;
     for (long m0 = 0; m0 < M; m0 += max_rows) {
       const int mc = (int)min((long)M - m0, max_rows);
-      const int rc = lk_gemm(x + m0 * ldx, ldx, w, bias, mc, N, K, epi, bn, variant, out + m0 * ldo, ldo, st);
+      const int rc = lk_gemm(x + m0 * ldx, ldx, w, bias, mc, N, K, epi, bn, variant, out + m0 * ldo, ldo, st, 1, nullptr);
       if (rc) return rc;
     }
     return 0;
   }
   if (variant < 0 || variant > 1) return -1;
-  const int rc = bn == 256 ? dispatch<4>(x, ldx, w, bias, M, N, K, epi, variant, out, ldo, st)
-                           : dispatch<3>(x, ldx, w, bias, M, N, K, epi, variant, out, ldo, st);
+  const int rc = bn == 256 ? dispatch<4>(x, ldx, w, bias, M, N, K, epi, variant, ks, ws, out, ldo, st)
+                           : dispatch<3>(x, ldx, w, bias, M, N, K, epi, variant, ks, ws, out, ldo, st);
   LK_CHECK_LAUNCH();
   return rc;
 }

@@ -51,9 +51,11 @@ int lk_xgmi_allreduce(bf16_t* const* data, unsigned* const* sig, int rank, int w
 
 // gemm.hip (prefill / encoder-regime linear, 256 x {256,192} MFMA tiles, fused epilogues)
 // epi: 0 none, 1 SwiGLU (W = [Wg; Wu]), 2 bias, 3 bias + GELU(erf), 4 bias + ReLU; bn: 256 | 192
-int lk_gemm_supported(int M, int N, int K, int epi, int bn);
+// ks > 1: split-K over ks K-ranges, fp32 partials in ws [ks, M, N], then a reduce applies the
+// epilogue (not SwiGLU) -- for shapes with fewer tiles than CUs
+int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks = 1);
 int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
-            int variant, bf16_t* out, long ldo, hipStream_t st);
+            int variant, bf16_t* out, long ldo, hipStream_t st, int ks = 1, float* ws = nullptr);
 
 // rope_kv.hip
 int lk_rope_kv(bf16_t* qkv, long qs, const int* positions, const float* cos_sin, long T, int Hq,

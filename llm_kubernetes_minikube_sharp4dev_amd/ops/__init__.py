@@ -327,7 +327,23 @@ def _gemm_default(M: int, N: int, K: int, epi: int):
             best = (cost, bn)
     if best is None:
         return None
-    return (GEMM_SCHED, best[1])
+    return (GEMM_SCHED, best[1], _gemm_splits(M, N, K, epi, best[1]))
+
+
+# split-K for shapes with at most half as many tiles as CUs (M <= 2048 O / down projections,
+# the 70B TP=8 QKV shard at N 1280): fp32 partials of up to 4 K-ranges, each of >= 8 K-tiles,
+# summed by a reduce kernel that applies the epilogue (profiles/r2_gemm_splitk.md); LK_GEMM_SPLITK=0
+# turns it off
+GEMM_SPLITK = os.environ.get("LK_GEMM_SPLITK", "1") != "0"
+
+
+def _gemm_splits(M: int, N: int, K: int, epi: int, bn: int) -> int:
+    if not GEMM_SPLITK or epi == 1:
+        return 1
+    tiles = ((M + 255) // 256) * (N // bn)
+    if tiles > 128:
+        return 1
+    return max(1, min(4, 256 // tiles, K // 64 // 8))
 
 
 def _gemm_ok(x, w) -> bool:
@@ -344,9 +360,9 @@ def gemm(x, w, b=None, epi: int = 0, out=None):
     cfg = _GEMM_TABLE.get(key)
     if cfg is None:
         cfg = _gemm_default(M, N, K, epi)
-        if cfg is None or not lib().gemm_supported(M, N, K, epi, cfg[1]):
+        if cfg is None or not lib().gemm_supported(M, N, K, epi, cfg[1], cfg[2]):
             return None
-    return lib().gemm(x, w, b, epi, cfg[1], out, cfg[0])
+    return lib().gemm(x, w, b, epi, cfg[1], out, cfg[0], cfg[2] if len(cfg) > 2 else 1)
 
 
 def _library(x, w, b, act, key):

@@ -420,6 +420,42 @@ def test_gemm(hip, M, NK):
     assert ran >= 2
 
 
+@pytest.mark.parametrize("MNK", [(2048, 4096, 4096), (300, 1280, 8192), (1000, 768, 3072), (4096, 1280, 8192)])
+@pytest.mark.parametrize("splits", [2, 3, 4])
+@pytest.mark.parametrize("epi", [0, 2, 3, 4])
+def test_gemm_splitk(hip, MNK, splits, epi):
+    """Split-K (fp32 partials of `splits` K-ranges + a reduce kernel applying the epilogue) vs
+    fp32 linear -> bf16 -> activation, with uneven K-ranges (K-tiles % splits != 0) and M tails."""
+    M, N, K = MNK
+    torch.manual_seed(M + N + splits + epi)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16) if epi else None
+    y = x.float() @ w.float().t()
+    if epi:
+        y = (y + b.float()).to(torch.bfloat16).float()
+    if epi == 3:
+        y = torch.nn.functional.gelu(y)
+    elif epi == 4:
+        y = torch.relu(y)
+    for sched in (0, 1):
+        for bn in (256, 192):
+            if hip.gemm_supported(M, N, K, epi, bn, splits):
+                _close(hip.gemm(x, w, b, epi, bn, None, sched, splits), y, 0.03, 0.01,
+                       f"gemm split{splits} epi{epi} s{sched}/{bn} M{M} N{N} K{K}")
+
+
+def test_gemm_splitk_dispatch(hip):
+    """ops.gemm picks split-K for the low-tile-count shapes and stays on one pass elsewhere."""
+    assert ops._gemm_default(2048, 4096, 4096, 0)[2] == 2
+    assert ops._gemm_default(4096, 1280, 8192, 0)[2] == 3
+    assert ops._gemm_default(8192, 4096, 4096, 0)[2] == 1
+    assert ops._gemm_default(2048, 28672, 4096, 1)[2] == 1
+    x = torch.randn(2048, 4096, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(4096, 4096, device=DEV, dtype=torch.bfloat16) * 0.05
+    _close(ops.gemm(x, w), x.float() @ w.float().t(), 0.02, 0.01, "ops.gemm split-K")
+
+
 def test_gemm_asymmetric_layout(hip):
     """A = I with an asymmetric B catches a transposed C write (CDNA4 playbook §3)."""
     M = N = K = 256

@@ -179,3 +179,19 @@ def test_fused_decode_ops_cpu_fallback():
     q2 = ops.linear(x, wq)
     ops.rope_kv_(q2, pos, cs, Hq, Hkv, D, kc2, vc2, slots)
     assert torch.equal(q1, q2) and torch.equal(kc, kc2) and torch.equal(vc, vc2)
+
+
+def test_gemm_split_k_policy():
+    """Prefill-GEMM dispatch (pure host logic): split-K only where the 256-row tile grid covers
+    at most half of the 256 CUs, never for SwiGLU, at most 4 splits of >= 8 K-tiles each
+    (profiles/r2_gemm_splitk.md)."""
+    from llm_kubernetes_minikube_sharp4dev_amd import ops
+
+    assert ops._gemm_default(1024, 4096, 4096, 0) == (ops.GEMM_SCHED, 256, 4)
+    assert ops._gemm_default(2048, 4096, 14336, 0)[2] == 2
+    assert ops._gemm_default(1024, 6144, 4096, 0)[1:] == (192, 2)
+    assert ops._gemm_default(4096, 1280, 8192, 0)[2] == 3
+    assert ops._gemm_default(8192, 4096, 4096, 0)[2] == 1
+    assert ops._gemm_default(2560, 4096, 4096, 2)[2] == 1
+    assert ops._gemm_default(512, 28672, 4096, 1)[2] == 1  # SwiGLU: single pass
+    assert ops._gemm_default(256, 768, 768, 2)[2] == 1  # 12 K-tiles: < 8 per split at S 2
