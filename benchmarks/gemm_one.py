@@ -28,13 +28,14 @@ def main():
     ap.add_argument("--bn", type=int, default=256)
     ap.add_argument("--impl", default="ours")
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--variant", type=int, default=0, help="K-loop schedule (0: 4-phase, 1: 2-phase)")
     a = ap.parse_args()
     x = torch.randn(a.M, a.K, device="cuda", dtype=torch.bfloat16)
     w = torch.randn(a.N, a.K, device="cuda", dtype=torch.bfloat16)
     b = torch.randn(a.N, device="cuda", dtype=torch.bfloat16) if a.epi not in ("none", "swiglu") else None
     if a.impl == "ours":
         L = ops.lib()
-        fn = lambda: L.gemm(x, w, b, EPI[a.epi], a.bn)  # noqa: E731
+        fn = lambda: L.gemm(x, w, b, EPI[a.epi], a.bn, None, a.variant)  # noqa: E731
     else:
         fn = lambda: F.linear(x, w, b)  # noqa: E731
     for _ in range(a.iters):
