@@ -176,14 +176,18 @@ def case_prefill_gemm(M, N, K, swiglu=False):
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
     epi = 1 if swiglu else 0
-    cfgs = ops._gemm_configs(N, epi)
-    ts = {c: timeit(lambda c=c: L.gemm(x, w, None, epi, c[1], None, c[0])) for c in cfgs}
+    cfgs = [(sc, bn, 1) for sc, bn in ops._gemm_configs(N, epi)]
+    dflt = ops._gemm_default(M, N, K, epi)  # the dispatch policy's pick, split-K included
+    if dflt is not None and dflt not in cfgs:
+        cfgs.append(dflt)
+    ts = {c: timeit(lambda c=c: L.gemm(x, w, None, epi, c[1], None, c[0], c[2])) for c in cfgs}
     c, t = min(ts.items(), key=lambda kv: kv[1])
     if swiglu:
         tb = timeit(lambda: L.silu_mul(torch.nn.functional.linear(x, w)))
     else:
         tb = timeit(lambda: torch.nn.functional.linear(x, w))
-    return {"case": f"gemm M{M} N{N} K{K}{' swiglu' if swiglu else ''} s{c[0]}/{c[1]}", "us": t * 1e6,
+    return {"case": f"gemm M{M} N{N} K{K}{' swiglu' if swiglu else ''} s{c[0]}/{c[1]}" + (f"/k{c[2]}" if c[2] > 1 else ""),
+            "us": t * 1e6,
             "TFLOP/s": 2 * M * N * K / t / 1e12, "hipblaslt_us": tb * 1e6, "speedup": tb / t}
 
 
@@ -278,7 +282,7 @@ CASES = {
     "gemm_mid": lambda: [case_gemm(M, N, K) for M in (1024, 2048, 2560, 3072, 3328, 3584, 3840, 4096, 4352,
                                                       5120, 5376, 6144, 8192)
                          for (N, K) in LLAMA8B_SHAPES],
-    "prefill_gemm": lambda: [case_prefill_gemm(M, N, K, N == 28672) for M in (2048, 3328, 3584, 3840, 4096, 8192)
+    "prefill_gemm": lambda: [case_prefill_gemm(M, N, K, N == 28672) for M in (1024, 2048, 3328, 3584, 3840, 4096, 8192)
                     for (N, K) in LLAMA8B_SHAPES],
     "gemm_sweep": lambda: [case_gemm(M, N, K, lay) for M in (128, 256, 1024, 4096, 8192, 16384)
                            for (N, K) in LLAMA8B_SHAPES for lay in ("NT", "NN")],
