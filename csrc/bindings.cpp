@@ -245,13 +245,13 @@ at::Tensor gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at
   if (epi >= 2) {
     TORCH_CHECK(bias.has_value(), "gemm: this epilogue needs a bias");
     CHECK_CUDA(*bias); CHECK_BF16(*bias); CHECK_CONTIG(*bias);
-    TORCH_CHECK(bias->numel() == N && reinterpret_cast<uintptr_t>(bias->data_ptr()) % 8 == 0, "gemm: bias [N], 8-B aligned");
+    TORCH_CHECK(bias->numel() == N && reinterpret_cast<uintptr_t>(bias->data_ptr()) % 16 == 0, "gemm: bias [N], 16-B aligned");
   }
   const int n_out = epi == 1 ? N / 2 : N;
   at::Tensor out = out_ ? *out_ : at::empty({M, n_out}, x.options());
   CHECK_BF16(out); CHECK_LASTDIM(out);
   TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == n_out, "out shape");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 8 == 0 && out.stride(0) % 4 == 0, "out alignment");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0 && out.stride(0) % 8 == 0, "out alignment (16 B)");
   // split-K partials: fp32 [splits, M, N] from the caching allocator (stream-ordered reuse)
   at::Tensor ws;
   if (splits > 1) ws = at::empty({splits, M, N}, x.options().dtype(at::kFloat));

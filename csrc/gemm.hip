@@ -38,8 +38,10 @@
 //     XOR applied on the SOURCE offset, which keeps every ds_read_b128 lane group of the
 //     fragment reads on 16 distinct bank slots (SQ_LDS_BANK_CONFLICT = 0);
 //   * operands are swapped in the MFMA (A <- W rows, B <- X rows): a lane ends with one
-//     output row and 4 consecutive columns, so epilogues are per-lane and the stores are
-//     8-byte packed, and SwiGLU pairs the gate / up fragments of the same columns in a lane;
+//     output row and 4 consecutive columns per fragment, and the B-slot row order pairs
+//     fragments so that it holds 8 consecutive columns: epilogues are per-lane, the stores
+//     16-byte packed (the store tail is issue-bound), and SwiGLU pairs the gate / up fragments
+//     of the same columns in a lane;
 //   * tiles are visited in an XCD-aware order (bijective remap, 4 row tiles x all column
 //     tiles per group), so an XCD's ~32 concurrent tiles share their X / W K-slices in L2.
 #include <cstdlib>
@@ -118,8 +120,18 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
   };
   // slot row -> tile row
   auto a_row = [](int h, int s) { return (s & 63) + ((s >> 6) << 7) + 64 * h; };
-  auto b0_row = [](int s) { return (s >> 5) * (16 * NF) + (s & 31); };
-  auto b1_row = [](int s) { return (s / (16 * NF1)) * (16 * NF) + 32 + s % (16 * NF1); };
+  // B slot row -> tile column.  A fragment pair (n, n+1) of an n-half covers 32 columns, and
+  // fragment-local column c of fragment n is tile column 8 (c >> 2) + 4 n + (c & 3), so lane
+  // group g ends with 8 CONSECUTIVE output columns 8g .. 8g+7 (4 from each fragment): the
+  // epilogue stores 16 B per lane (dwordx4) instead of 8 B.  Its store tail is issue-bound
+  // (~7 B/cycle/CU with dwordx2: a ~9 us burst per wave of tiles, profiles/r2_gemm_tile_overhead.md),
+  // so half the store instructions halve it.  NF = 3: the unpaired third fragment keeps c.
+  auto pair_col = [](int rem) { return 8 * ((rem & 15) >> 2) + 4 * (rem >> 4) + (rem & 3); };  // rem < 32
+  auto b0_row = [&](int s) { return (s >> 5) * (16 * NF) + pair_col(s & 31); };
+  auto b1_row = [&](int s) {
+    if constexpr (NF1 == 2) return (s >> 5) * (16 * NF) + 32 + pair_col(s & 31);
+    else return (s / (16 * NF1)) * (16 * NF) + 32 + s % (16 * NF1);
+  };
 
   // ---- LDS-DMA sources and per-wave destinations: a wave instruction moves 8 slot rows x
   // 128 B; lane l -> row l >> 3, 16-B chunk l & 7 (source chunk swizzled).  Sources are
@@ -321,69 +333,96 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
   }
   if (wr == 0) seg_barrier();  // equal barrier counts for both halves
 
-  // ---- epilogue: lane holds row (.. + r), columns (.. + 4g + v), v = 0..3
+  // ---- epilogue: lane holds row (.. + r); fragment pair (2p, 2p+1) gives it the 8 consecutive
+  // columns 32p + 8g .. +7 of its wave's 16NF (the pair_col layout); NF = 3's third fragment
+  // the 4 columns 32 + 4g .. +3
+  auto put8 = [](bf16_t* dst, const float (&y)[8]) {
+    uint4_t pk;
+    pk.x = pack_bf2(y[0], y[1]);
+    pk.y = pack_bf2(y[2], y[3]);
+    pk.z = pack_bf2(y[4], y[5]);
+    pk.w = pack_bf2(y[6], y[7]);
+    *reinterpret_cast<uint4_t*>(dst) = pk;
+  };
   if constexpr (EPI == EPI_PARTIAL) {  // fp32 partial sums of split kz: out is float [splits, M, ldo]
     float* part = reinterpret_cast<float*>(out) + (long)kz * M * ldo;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int row = tm * kBM + wr * 128 + m * 16 + r;
       if (row >= M) continue;
+      float* prow = part + (long)row * ldo + tn * BN + wc * 16 * NF;
 #pragma unroll
-      for (int n = 0; n < NF; ++n)
-        *reinterpret_cast<floatx4*>(part + (long)row * ldo + tn * BN + wc * 16 * NF + n * 16 + 4 * g) = acc[m][n];
+      for (int n = 0; n < NF; ++n) {
+        const int col = (NF == 3 && n == 2) ? 32 + 4 * g : 32 * (n >> 1) + 8 * g + 4 * (n & 1);
+        *reinterpret_cast<floatx4*>(prow + col) = acc[m][n];
+      }
     }
   } else if constexpr (EPI == EPI_SWIGLU) {
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int row = tm * kBM + wr * 128 + m * 16 + r;
       if (row >= M) continue;
-      bf16_t* orow = out + (long)row * ldo;
+      float y[8];
 #pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const int col = tn * 128 + wc * 32 + n * 16 + 4 * g;
-        float y[4];
+      for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) y[v] = rbf(lk_silu(rbf(acc[m][n][v]))) * rbf(acc[m][n + 2][v]);
-        uint2 pk;
-        pk.x = pack_bf2(y[0], y[1]);
-        pk.y = pack_bf2(y[2], y[3]);
-        *reinterpret_cast<uint2*>(orow + col) = pk;
-      }
+        for (int v = 0; v < 4; ++v) y[4 * h + v] = rbf(lk_silu(rbf(acc[m][h][v]))) * rbf(acc[m][h + 2][v]);
+      put8(out + (long)row * ldo + tn * 128 + wc * 32 + 8 * g, y);
     }
   } else {
+    constexpr int NP = NF / 2;  // fragment pairs
     float bv[NF][4];
 #pragma unroll
-    for (int n = 0; n < NF; ++n) {
-      const int col = tn * BN + wc * 16 * NF + n * 16 + 4 * g;
-      if constexpr (EPI != EPI_NONE) {
-        const uint2 b = *reinterpret_cast<const uint2*>(bias + col);
-        bv[n][0] = bf2f((bf16_t)(b.x & 0xFFFF));
-        bv[n][1] = bf2f((bf16_t)(b.x >> 16));
-        bv[n][2] = bf2f((bf16_t)(b.y & 0xFFFF));
-        bv[n][3] = bf2f((bf16_t)(b.y >> 16));
+    for (int n = 0; n < NF; ++n)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) bv[n][v] = 0.f;
+    if constexpr (EPI != EPI_NONE) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const uint4_t b = *reinterpret_cast<const uint4_t*>(bias + tn * BN + wc * 16 * NF + 32 * p + 8 * g);
+        const unsigned bw[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          bv[2 * p + (q >> 1)][2 * (q & 1)] = bf2f((bf16_t)(bw[q] & 0xFFFF));
+          bv[2 * p + (q >> 1)][2 * (q & 1) + 1] = bf2f((bf16_t)(bw[q] >> 16));
+        }
+      }
+      if constexpr (NF == 3) {
+        const uint2 b = *reinterpret_cast<const uint2*>(bias + tn * BN + wc * 48 + 32 + 4 * g);
+        bv[2][0] = bf2f((bf16_t)(b.x & 0xFFFF));
+        bv[2][1] = bf2f((bf16_t)(b.x >> 16));
+        bv[2][2] = bf2f((bf16_t)(b.y & 0xFFFF));
+        bv[2][3] = bf2f((bf16_t)(b.y >> 16));
       }
     }
+    auto act = [&](float e, float b) {
+      if constexpr (EPI != EPI_NONE) e = rbf(e + b);
+      if constexpr (EPI == EPI_BIAS_GELU) e = lk_gelu_erf(e);
+      if constexpr (EPI == EPI_BIAS_RELU) e = fmaxf(e, 0.f);
+      return e;
+    };
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int row = tm * kBM + wr * 128 + m * 16 + r;
       if (row >= M) continue;
-      bf16_t* orow = out + (long)row * ldo;
+      bf16_t* orow = out + (long)row * ldo + tn * BN + wc * 16 * NF;
 #pragma unroll
-      for (int n = 0; n < NF; ++n) {
-        const int col = tn * BN + wc * 16 * NF + n * 16 + 4 * g;
+      for (int p = 0; p < NP; ++p) {
+        float y[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) y[4 * h + v] = act(acc[m][2 * p + h][v], bv[2 * p + h][v]);
+        put8(orow + 32 * p + 8 * g, y);
+      }
+      if constexpr (NF == 3) {
         float y[4];
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          float e = acc[m][n][v];
-          if constexpr (EPI != EPI_NONE) e = rbf(e + bv[n][v]);
-          if constexpr (EPI == EPI_BIAS_GELU) e = lk_gelu_erf(e);
-          if constexpr (EPI == EPI_BIAS_RELU) e = fmaxf(e, 0.f);
-          y[v] = e;
-        }
+        for (int v = 0; v < 4; ++v) y[v] = act(acc[m][2][v], bv[2][v]);
         uint2 pk;
         pk.x = pack_bf2(y[0], y[1]);
         pk.y = pack_bf2(y[2], y[3]);
-        *reinterpret_cast<uint2*>(orow + col) = pk;
+        *reinterpret_cast<uint2*>(orow + 32 + 4 * g) = pk;
       }
     }
   }
@@ -532,7 +571,10 @@ int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks) {
 // 8-B aligned output rows; any M >= 1.
 int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
             int variant, bf16_t* out, long ldo, hipStream_t st, int ks, float* ws) {
-  if (!lk_gemm_supported(M, N, K, epi, bn, ks) || ldx % 8 || ldo % 4) return -1;
+  // 16-B epilogue stores / bias loads: output rows and the bias 16-B aligned
+  if (!lk_gemm_supported(M, N, K, epi, bn, ks) || ldx % 8 || ldo % 8 || reinterpret_cast<uintptr_t>(out) % 16 ||
+      (bias != nullptr && reinterpret_cast<uintptr_t>(bias) % 16))
+    return -1;
   // operands are addressed through 32-bit buffer offsets: W must fit, X is cut into row chunks
   if ((long)N * K * 2 >= 0x7FFFFFF0L) return -1;
   const long max_rows = (0x7FFFFFF0L / (ldx * 2)) / kBM * kBM;
