@@ -399,18 +399,37 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
       p.part_ml[pr * 2] = m_run;
       p.part_ml[pr * 2 + 1] = l_run;
     }
-  } else if (qvalid) {
+  } else if (!p.part_o) {
+    // lanes l and l+32 hold the two halves (4h) of each 8-column group of the same query row:
+    // one v_permlane32_swap per dword gives lanes 0-31 group 2k whole and lanes 32-63 group
+    // 2k+1 whole, so the row is written with 16-B stores (half the store instructions of the
+    // issue-bound tail: CDNA playbook T21).  The swap runs on every lane (the pair shares qvalid).
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
     bf16_t* op = p.out + (long)(qbeg + qrow) * p.os + (long)head * D;
 #pragma unroll
     for (int n = 0; n < ND; ++n)
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = 32 * n + 8 * g4 + 4 * h;
-        uint2 pk;
-        pk.x = pack_bf2(o[n][4 * g4 + 0] * inv, o[n][4 * g4 + 1] * inv);
-        pk.y = pack_bf2(o[n][4 * g4 + 2] * inv, o[n][4 * g4 + 3] * inv);
-        *reinterpret_cast<uint2*>(op + d) = pk;
+      for (int g2 = 0; g2 < 2; ++g2) {
+        unsigned a[2], b[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          a[j] = pack_bf2(o[n][8 * g2 + 2 * j] * inv, o[n][8 * g2 + 2 * j + 1] * inv);
+          b[j] = pack_bf2(o[n][8 * g2 + 4 + 2 * j] * inv, o[n][8 * g2 + 4 + 2 * j + 1] * inv);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const auto r2 = __builtin_amdgcn_permlane32_swap(a[j], b[j], false, false);
+          a[j] = r2[0];
+          b[j] = r2[1];
+        }
+        if (qvalid) {
+          uint4_t pk;
+          pk.x = a[0];
+          pk.y = a[1];
+          pk.z = b[0];
+          pk.w = b[1];
+          *reinterpret_cast<uint4_t*>(op + 32 * n + 16 * g2 + 8 * h) = pk;
+        }
       }
   }
 }
@@ -456,6 +475,8 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
                      float* part_o, float* part_ml, hipStream_t st) {
   if (ntiles == 0) return 0;
   if (Hq % Hkv) return -1;
+  // 16-B output stores (permlane-paired epilogue): 16-B aligned output rows
+  if (part_o == nullptr && (os % 8 || reinterpret_cast<uintptr_t>(out) % 16)) return -5;
   const int G = Hq / Hkv;
   if (!(G == 1 || G == 2 || G % 4 == 0)) return -2;
   if (paged && (BS <= 0)) return -4;

@@ -9,6 +9,7 @@ fp32 torch references in :mod:`.reference`.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
 import threading
 
@@ -31,7 +32,13 @@ def try_lib():
             try:
                 import torch  # noqa: F401  (loads libamdhip64 / libtorch first)
 
-                _mod = importlib.import_module("llm_kubernetes_minikube_sharp4dev_amd._C")
+                alt = os.environ.get("LK_LIB_PATH")
+                if alt:  # A/B knob: another build of this extension (e.g. the previous commit's)
+                    spec = importlib.util.spec_from_file_location("llm_kubernetes_minikube_sharp4dev_amd._C", alt)
+                    _mod = importlib.util.module_from_spec(spec)
+                    spec.loader.exec_module(_mod)
+                else:
+                    _mod = importlib.import_module("llm_kubernetes_minikube_sharp4dev_amd._C")
                 if os.environ.get("LK_WS_ROT"):  # weight-streaming GEMM K-step rotation override
                     _mod.ws_set_rot(int(os.environ["LK_WS_ROT"]))
             except Exception as e:  # pragma: no cover - depends on build state
