@@ -343,11 +343,15 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
         const int row = 16 * n + r;
         b[n] = *reinterpret_cast<const short8*>(base + XB + row * 128 + ((c ^ wsz(row)) << 4));
       }
+      // W fragment as the MFMA's A operand: the lane ends with ONE output row and 4
+      // consecutive columns, so the epilogue writes 16 B (f32 partials) / 8 B (bf16) per lane
+      // -- a quarter of the store instructions of a column-per-lane image (the store tail
+      // of a short weight-streaming kernel is issue-bound)
 #pragma unroll
       for (int m = 0; m < MTW; ++m)
 #pragma unroll
         for (int n = 0; n < NT; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], b[n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[n], a[m], acc[m][n], 0, 0, 0);
     }
   };
 
@@ -364,31 +368,60 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
     compute(st);
   }
 
-  // ---- epilogue straight from the accumulators: lane holds rows 4g+i, column r of each tile
+  // ---- epilogue straight from the accumulators: lane holds row 16m + r of its wave's rows,
+  // tile columns 16n + 4g .. +3
   const bool split = part != nullptr;
+  const bool part_vec = split && part_ld % 4 == 0 && reinterpret_cast<uintptr_t>(part) % 16 == 0;
+  const bool out_vec = ldo % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 8 == 0;
 #pragma unroll
   for (int m = 0; m < MTW; ++m) {
+    const int row = w * (4 * MT) + 16 * m + r;
+    if (row >= M) continue;
+    if (SWIGLU && !split) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = w * (4 * MT) + 16 * m + 4 * g + i;
-      if (row >= M) continue;
-      if (SWIGLU && !split) {
+      for (int n = 0; n < NT / 2; ++n) {
+        float y[4];
 #pragma unroll
-        for (int n = 0; n < NT / 2; ++n) {
-          const float y = rbf(silu_f(rbf(acc[m][n][i]))) * rbf(acc[m][n + NT / 2][i]);
-          out[(long)row * ldo + (long)t * (BN / 2) + 16 * n + r] = f2bf(y);
+        for (int i = 0; i < 4; ++i) y[i] = rbf(silu_f(rbf(acc[m][n][i]))) * rbf(acc[m][n + NT / 2][i]);
+        bf16_t* dst = out + (long)row * ldo + (long)t * (BN / 2) + 16 * n + 4 * g;
+        if (out_vec) {
+          uint2 pk;
+          pk.x = pack_bf2(y[0], y[1]);
+          pk.y = pack_bf2(y[2], y[3]);
+          *reinterpret_cast<uint2*>(dst) = pk;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dst[i] = f2bf(y[i]);
         }
-      } else if (split) {
+      }
+    } else if (split) {
 #pragma unroll
-        for (int n = 0; n < NT; ++n) {
-          const long col = wrow(16 * n + r);
-          if (col < n_rows) part[(long)s * M * part_ld + (long)row * part_ld + col] = acc[m][n][i];
+      for (int n = 0; n < NT; ++n) {
+        // 4 consecutive tile rows stay inside one half of a SwiGLU tile: contiguous W rows
+        const long col = wrow(16 * n + 4 * g);
+        float* dst = part + (long)s * M * part_ld + (long)row * part_ld + col;
+        if (part_vec && col + 3 < n_rows) {
+          *reinterpret_cast<floatx4*>(dst) = acc[m][n];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (col + i < n_rows) dst[i] = acc[m][n][i];
         }
-      } else {
+      }
+    } else {
 #pragma unroll
-        for (int n = 0; n < NT; ++n) {
-          const long col = (long)t * BN + 16 * n + r;
-          if (col < n_rows) out[(long)row * ldo + col] = f2bf(acc[m][n][i]);
+      for (int n = 0; n < NT; ++n) {
+        const long col = (long)t * BN + 16 * n + 4 * g;
+        bf16_t* dst = out + (long)row * ldo + col;
+        if (out_vec && col + 3 < n_rows) {
+          uint2 pk;
+          pk.x = pack_bf2(acc[m][n][0], acc[m][n][1]);
+          pk.y = pack_bf2(acc[m][n][2], acc[m][n][3]);
+          *reinterpret_cast<uint2*>(dst) = pk;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (col + i < n_rows) dst[i] = f2bf(acc[m][n][i]);
         }
       }
     }
