@@ -295,6 +295,9 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
   }
   seg_barrier();
   if (wr == 1) seg_barrier();  // waves 4-7 run one segment behind
+  if constexpr (PRIO == 1) {  // static priority for the lagging (younger) half instead of per-cluster flips
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
   for (int t = 0; t < nk; ++t) {
     const unsigned char* buf = smem + (t & 1) * G::BUF;
     // phase 1: quadrant (0, 0)
@@ -512,6 +515,7 @@ template <int NF, int EPI>
 void launch(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
             long ldo, int TM, int TN, int sched, hipStream_t st, int ks = 1) {
   if (sched == 1) launch_ph<NF, EPI, 2, 1>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
+  else if (sched == 2) launch_ph<NF, EPI, 4, 1>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
   else launch_ph<NF, EPI, 4, 0>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
 }
 
@@ -587,7 +591,7 @@ int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int 
     }
     return 0;
   }
-  if (variant < 0 || variant > 1) return -1;
+  if (variant < 0 || variant > 2) return -1;
   const int rc = bn == 256 ? dispatch<4>(x, ldx, w, bias, M, N, K, epi, variant, ks, ws, out, ldo, st)
                            : dispatch<3>(x, ldx, w, bias, M, N, K, epi, variant, ks, ws, out, ldo, st);
   LK_CHECK_LAUNCH();

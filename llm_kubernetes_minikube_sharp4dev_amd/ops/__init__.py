@@ -298,8 +298,18 @@ EPI = {None: 0, "swiglu": 1, "bias": 2, "gelu": 3, "relu": 4}
 # measurement knob only: LK_GEMM_LIBRARY=1 sends the prefill-regime GEMMs to hipBLASLt (+ the
 # separate activation kernels) for in-situ A/B against the hand-written kernel
 GEMM_LIBRARY = os.environ.get("LK_GEMM_LIBRARY", "0") == "1"
-# K-loop schedule of untuned shapes (0: 4 phases per K-tile, 1: 2 phases); in-situ A/B knob
-GEMM_SCHED = int(os.environ.get("LK_GEMM_SCHED", "0"))
+# K-loop schedule of untuned shapes (0: 4 phases per K-tile with per-cluster priority flips,
+# 1: 2 phases, 2: 4 phases with a static priority for the lagging half of the waves).  Default:
+# 2 for the decoder's K >= 4096 projections (1-5 % faster cold on every Llama-3-8B shape at
+# M 4096 / 8192), 0 for the encoder's K 768 / 3072 (neutral there, and 2 lost 8 % on the
+# bge QKV at M 65536): profiles/r2_gemm_prio.md.  LK_GEMM_SCHED forces one for every shape.
+GEMM_SCHED = int(os.environ["LK_GEMM_SCHED"]) if os.environ.get("LK_GEMM_SCHED") else None
+
+
+def _gemm_sched(K: int) -> int:
+    if GEMM_SCHED is not None:
+        return GEMM_SCHED
+    return 2 if K >= 4096 else 0
 _GEMM_TABLE: dict = {}
 LIBRARY_FALLBACKS: dict = {}
 
@@ -311,7 +321,7 @@ def _gemm_key(M: int, N: int, K: int, epi: int):
 def _gemm_configs(N: int, epi: int):
     """(schedule, column tile) candidates the kernel supports for this N / epilogue."""
     bns = [256] if epi == 1 else [bn for bn in (256, 192) if N % bn == 0]
-    return [(sched, bn) for bn in bns for sched in (0, 1)]
+    return [(sched, bn) for bn in bns for sched in (0, 1, 2)]
 
 
 def _gemm_default(M: int, N: int, K: int, epi: int):
@@ -327,7 +337,7 @@ def _gemm_default(M: int, N: int, K: int, epi: int):
             best = (cost, bn)
     if best is None:
         return None
-    return (GEMM_SCHED, best[1], _gemm_splits(M, N, K, epi, best[1]))
+    return (_gemm_sched(K), best[1], _gemm_splits(M, N, K, epi, best[1]))
 
 
 # split-K for shapes with at most half as many tiles as CUs (M <= 2048 O / down projections,

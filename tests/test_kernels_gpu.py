@@ -399,7 +399,7 @@ def test_ws_swiglu(hip, M, IK):
     _close(hip.ws_linear(x, w, True, 64, 2), a_ref, 0.03, 0.01, "ws swiglu bn64 S2")
 
 
-GEMM_CFGS = [(0, 256), (1, 256), (0, 192), (1, 192)]
+GEMM_CFGS = [(0, 256), (1, 256), (2, 256), (0, 192), (1, 192), (2, 192)]
 
 
 @pytest.mark.parametrize("M", [1, 257, 1000, 3584])

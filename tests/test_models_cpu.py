@@ -187,7 +187,9 @@ def test_gemm_split_k_policy():
     (profiles/r2_gemm_splitk.md)."""
     from llm_kubernetes_minikube_sharp4dev_amd import ops
 
-    assert ops._gemm_default(1024, 4096, 4096, 0) == (ops.GEMM_SCHED, 256, 4)
+    assert ops._gemm_default(1024, 4096, 4096, 0) == (ops._gemm_sched(4096), 256, 4)
+    if ops.GEMM_SCHED is None:  # default schedule policy: static-priority 4-phase for the decoder's K
+        assert ops._gemm_sched(4096) == 2 and ops._gemm_sched(14336) == 2 and ops._gemm_sched(768) == 0
     assert ops._gemm_default(2048, 4096, 14336, 0)[2] == 2
     assert ops._gemm_default(1024, 6144, 4096, 0)[1:] == (192, 2)
     assert ops._gemm_default(4096, 1280, 8192, 0)[2] == 3
