@@ -197,3 +197,23 @@ def test_gemm_split_k_policy():
     assert ops._gemm_default(2560, 4096, 4096, 2)[2] == 1
     assert ops._gemm_default(512, 28672, 4096, 1)[2] == 1  # SwiGLU: single pass
     assert ops._gemm_default(256, 768, 768, 2)[2] == 1  # 12 K-tiles: < 8 per split at S 2
+
+
+def test_lib_path_ab_knob_loads_the_named_build():
+    """LK_LIB_PATH (same-box A/B of two builds of the kernel library) loads the extension from
+    the given file instead of the in-tree one."""
+    import glob
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    so = glob.glob(os.path.join(root, "llm_kubernetes_minikube_sharp4dev_amd", "_C.*.so"))
+    if not so:
+        pytest.skip("kernel library not built")
+    code = ("from llm_kubernetes_minikube_sharp4dev_amd.ops import _ext; m = _ext.try_lib(); "
+            "print(m.__file__ if m is not None else 'ERR ' + repr(_ext._err))")
+    env = {**os.environ, "LK_LIB_PATH": so[0]}
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True,
+                         timeout=300).stdout.strip().splitlines()[-1]
+    assert out == so[0], out
