@@ -92,10 +92,10 @@ class Sampler:
         a = np.asarray(allowed, dtype=np.int64)
         if len(a) and (a.min() < 0 or a.max() >= V):
             a = a[(a >= 0) & (a < V)]
-        if len(a) > 64:
-            if len(self._arr_cache) > 4096:
-                self._arr_cache.clear()
-            self._arr_cache[id(allowed)] = (allowed, a)
+        # every list, short ones too: the grammar states recur (literal / EOS lists)
+        if len(self._arr_cache) > 8192:
+            self._arr_cache.clear()
+        self._arr_cache[id(allowed)] = (allowed, a)
         return a
 
     @staticmethod

@@ -84,3 +84,29 @@ def test_tool_call_grammar_enums_and_fast_forward():
         if "replicas" in obj:
             assert isinstance(obj["replicas"], int) and (obj["replicas"] == 0 or not str(obj["replicas"]).startswith("0"))
         assert len(ids) <= 40
+
+
+def test_tool_call_grammar_incremental_text_matches_full_decode():
+    """The grammar extends a running history's decoded text token by token (printable-ASCII
+    pieces, EOS dropped) instead of re-decoding it every step; the text and the allowed sets
+    must equal the full-decode ones along random constrained generations."""
+    import random
+
+    from llm_kubernetes_minikube_sharp4dev_amd.config import Config
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.constrained import tool_call_processor
+    from llm_kubernetes_minikube_sharp4dev_amd.models.tokenizer import builtin_tokenizer
+
+    tok = builtin_tokenizer()
+    cfg = Config()
+    enums = {"namespace": list(cfg.agent.allowed_namespaces) + ["default"], "name": ["echoserver", "api"]}
+    inc = tool_call_processor(tok, max_str=16, enums=enums)
+    ref = tool_call_processor(tok, max_str=16, enums=enums)
+    rng = random.Random(1)
+    for _ in range(25):
+        ids: list = []
+        for _ in range(40):
+            allowed = inc(ids)
+            assert inc._text(ids) == (tok.decode(ids) if ids else "")
+            ref._texts = {}  # no text cache: the full-decode path
+            assert list(allowed) == list(ref(list(ids)))
+            ids.append(rng.choice(list(allowed)))
