@@ -53,6 +53,14 @@ def test_bench_two_rank_dp():
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 4
 
 
+def test_bench_four_rank_dp():
+    """The driver's N=4 launch shape (torchrun, one rank per device, rank-0 JSON over all ranks):
+    four replicas share the index build and report the whole-job aggregate."""
+    d = _run([], nproc=4)
+    assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "dp4" and d["config"]["global_batch"] == 8
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+
+
 def test_bench_two_rank_tp():
     d = _run(["--tp", "2"], nproc=2)
     assert d["config"]["parallelism"] == "tp2" and d["config"]["global_batch"] == 2 and d["value"] > 0
