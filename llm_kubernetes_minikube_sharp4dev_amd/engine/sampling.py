@@ -98,10 +98,12 @@ class Sampler:
         self._arr_cache[id(allowed)] = (allowed, a)
         return a
 
-    @staticmethod
-    def _plan(rows: dict, B: int, dev) -> torch.Tensor:
+    def _plan(self, rows: dict, B: int, dev) -> torch.Tensor:
         """Device int32 [B flags | B+1 offsets | allowed ids] of the constrained rows
-        (flag 0 = unconstrained row) for the HIP select_allowed kernel."""
+        (flag 0 = unconstrained row) for the HIP select_allowed kernel.  Staged through a small
+        ring of pinned buffers: a pageable host->device copy makes the host wait until the
+        device queue reaches it (behind the step's forward), which would stall the pipelined
+        engine's next launch."""
         order = sorted(rows)
         flags = np.zeros(B, dtype=np.int32)
         counts = np.zeros(B + 1, dtype=np.int64)
@@ -111,7 +113,24 @@ class Sampler:
         offs = np.cumsum(counts)
         ids = np.concatenate([rows[i] for i in order])
         plan = np.concatenate([flags, offs.astype(np.int32), ids.astype(np.int32)])
-        return torch.from_numpy(plan).to(dev, non_blocking=True)
+        if dev.type != "cuda":
+            return torch.from_numpy(plan)
+        ring = getattr(self, "_plan_ring", None)
+        if ring is None:
+            ring = self._plan_ring = [[None, None] for _ in range(4)]  # [pinned int32 buffer, event]
+            self._plan_k = 0
+        self._plan_k = (self._plan_k + 1) % len(ring)
+        slot = ring[self._plan_k]
+        if slot[1] is not None:
+            slot[1].synchronize()  # the copy that last read this buffer has run
+        if slot[0] is None or slot[0].numel() < plan.size:
+            slot[0] = torch.empty(max(2 * plan.size, 1 << 14), dtype=torch.int32, pin_memory=True)
+        slot[0][: plan.size].numpy()[:] = plan
+        out = torch.empty(plan.size, dtype=torch.int32, device=dev)
+        out.copy_(slot[0][: plan.size], non_blocking=True)
+        slot[1] = torch.cuda.Event()
+        slot[1].record()
+        return out
 
     # ---------------------------------------------------------------- device sampler state
     RING = 256        # history window per sequence (repeat_last_n is clamped to it)

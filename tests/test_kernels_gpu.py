@@ -603,7 +603,7 @@ def test_select_allowed_matches_masked_select(hip, sample):
     rows = {0: torch.randint(0, V, (3000,), generator=g).numpy(), 2: np.array([77, 500, 9, 128000]),
             3: np.array([5]), 5: torch.randint(0, V, (40,), generator=g).numpy(), 6: np.array([V - 1, 0])}
     rows = {i: a.astype(np.int64) for i, a in rows.items()}
-    plan = Sampler._plan(rows, B, torch.device(DEV))
+    plan = Sampler(V)._plan(rows, B, torch.device(DEV))
     masked = logits.clone()
     for i, a in rows.items():
         m = torch.full((V,), float("-inf"), device=DEV)
