@@ -366,6 +366,11 @@ def gemm(x, w, b=None, epi: int = 0, out=None):
     """epi(x w^T (+ b)) on the hand-written kernel; None if the shape is unsupported."""
     M, K = x.shape
     N = w.shape[0]
+    # the epilogue stores / bias loads are 16-byte vectors
+    if b is not None and (b.data_ptr() % 16 or not b.is_contiguous()):
+        return None
+    if out is not None and (out.data_ptr() % 16 or out.stride(0) % 8 or out.stride(1) != 1):
+        return None
     key = _gemm_key(M, N, K, epi)
     cfg = _GEMM_TABLE.get(key)
     if cfg is None:
