@@ -178,6 +178,12 @@ def flash_prefill(q, k, v, cu_q, Hq: int, Hkv: int, D: int, scale: float, causal
             tiles = (torch.from_numpy(ts).to(q.device, non_blocking=True),
                      torch.from_numpy(tq).to(q.device, non_blocking=True))
         pp_o, pp_ml = part if part is not None else (None, None)
+        if out is not None and part is None and (out.data_ptr() % 16 or out.stride(0) % 8):
+            # the kernel's output rows leave as 16-byte stores: stage a misaligned view
+            y = lib().flash_prefill(q, k, v, block_tables, cu_q, ctx_lens, tiles[0], tiles[1], Hq,
+                                    Hkv, D, scale, causal, None, None, None)
+            out[:, : Hq * D].copy_(y)
+            return out
         return lib().flash_prefill(q, k, v, block_tables, cu_q, ctx_lens, tiles[0], tiles[1], Hq,
                                    Hkv, D, scale, causal, out, pp_o, pp_ml)
     y = ref.flash_prefill(q, k, v, block_tables, cu_q, ctx_lens, Hq, Hkv, D, scale, causal)
