@@ -347,7 +347,8 @@ def _gemm_default(M: int, N: int, K: int, epi: int):
 
 
 # split-K for shapes with at most half as many tiles as CUs (M <= 2048 O / down projections,
-# the 70B TP=8 QKV shard at N 1280): fp32 partials of up to 4 K-ranges, each of >= 8 K-tiles,
+# the 70B TP=8 QKV shard at N 1280), and 3 K-ranges for long-K shapes of 129-160 tiles:
+# fp32 partials of up to 4 K-ranges, each of >= 8 K-tiles,
 # summed by a reduce kernel that applies the epilogue (profiles/r2_gemm_splitk.md); LK_GEMM_SPLITK=0
 # turns it off
 GEMM_SPLITK = os.environ.get("LK_GEMM_SPLITK", "1") != "0"
@@ -358,7 +359,9 @@ def _gemm_splits(M: int, N: int, K: int, epi: int, bn: int) -> int:
         return 1
     tiles = ((M + 255) // 256) * (N // bn)
     if tiles > 128:
-        return 1
+        # long K just past half a wave: three K-ranges give ~1.7-1.9 waves of tiles
+        # (M 2304 / 2560 down projection: 295 -> 278, 277 -> 255 us; from 176 tiles on, worse)
+        return 3 if tiles <= 160 and K >= 8192 else 1
     return max(1, min(4, 256 // tiles, K // 64 // 8))
 
 

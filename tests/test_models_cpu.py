@@ -195,6 +195,8 @@ def test_gemm_split_k_policy():
     assert ops._gemm_default(4096, 1280, 8192, 0)[2] == 3
     assert ops._gemm_default(8192, 4096, 4096, 0)[2] == 1
     assert ops._gemm_default(2560, 4096, 4096, 2)[2] == 1
+    assert ops._gemm_default(2560, 4096, 14336, 0)[2] == 3  # 160 tiles, long K
+    assert ops._gemm_default(2816, 4096, 14336, 0)[2] == 1  # 176 tiles
     assert ops._gemm_default(512, 28672, 4096, 1)[2] == 1  # SwiGLU: single pass
     assert ops._gemm_default(256, 768, 768, 2)[2] == 1  # 12 K-tiles: < 8 per split at S 2
 
