@@ -66,6 +66,10 @@ def parse():
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--embedder", default="bge-base")
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (ranks per replica)")
+    ap.add_argument("--tp-sim", type=int, default=1,
+                    help="one GPU runs rank 0's shard of a TP group of this size with local stand-in "
+                         "collectives (parallel.tp.SimulatedTPGroup): per-rank compute of e.g. 70B TP=8; "
+                         "the JSON reports the all-reduce bytes the real group would move")
     ap.add_argument("--kv-gb", type=float, default=48.0)
     ap.add_argument("--max-batched-tokens", type=int, default=None,
                     help="token budget per engine step (default: continuous 64 x --batch capped at 8192, "
@@ -134,6 +138,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world % args.tp:
         raise SystemExit(f"--tp {args.tp} must divide the world size {world}")
+    if args.tp_sim > 1 and (args.tp > 1 or world > 1):
+        raise SystemExit("--tp-sim runs one rank's shard in a single process (no --tp, WORLD_SIZE 1)")
     if args.device == "cuda" and os.environ.get("LK_FORCE_REFERENCE", "0") not in ("", "0", "false", "False"):
         # the flag routes GPU tensors to the torch reference ops: never measure that as the framework
         raise SystemExit("bench.py: LK_FORCE_REFERENCE is set -- refusing to time the torch reference path "
@@ -160,7 +166,7 @@ def main():
     from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder, build_encoder
     from llm_kubernetes_minikube_sharp4dev_amd.models.tokenizer import builtin_tokenizer
     from llm_kubernetes_minikube_sharp4dev_amd.ops import _ext
-    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp import SINGLE, new_tp_groups
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp import SINGLE, SimulatedTPGroup, new_tp_groups
     from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp_engine import (make_tp_engine, run_tp_worker,
                                                                           shutdown_tp, tp_barrier, tp_capture_all)
     from llm_kubernetes_minikube_sharp4dev_amd.rag.embedder import LocalEmbedder
@@ -186,6 +192,8 @@ def main():
 
     wdtype = torch.bfloat16 if on_gpu else torch.float32
     tpg = new_tp_groups(args.tp) if args.tp > 1 else SINGLE
+    if args.tp_sim > 1:
+        tpg = SimulatedTPGroup(rank=0, size=args.tp_sim)
     leader = tpg.rank == 0
     n_replicas = world // args.tp
 
@@ -229,7 +237,8 @@ def main():
     if args.sp_min_tokens is not None and hasattr(llm, "sp_min_tokens"):
         llm.sp_min_tokens = args.sp_min_tokens
     sync()
-    log(rank, f"{args.model} random-init (tp={args.tp}) in {time.perf_counter() - t0:.1f}s")
+    log(rank, f"{args.model} random-init (tp={args.tp}{f', tp-sim {args.tp_sim}' if args.tp_sim > 1 else ''}) "
+              f"in {time.perf_counter() - t0:.1f}s")
     # continuous: 8k-token steps (whole waves of 256x256 tiles on every projection: 6144-row
     # steps measured 4 % slower) -- on MI355X 8192-token steps with admission chunks of 16
     # beat 4096 / 8 by 2 % in q/s and p50 on the same box (profiles/r2_sched_sweep.md)
@@ -415,6 +424,20 @@ def main():
                       for k in ("steps_queued", "steps_in_system", "steps_run")
                       if any(r.timings and r.timings.get(k) is not None for r in results)}
         par = f"dp{n_replicas}" if args.tp == 1 else f"tp{args.tp}" + (f"xdp{n_replicas}" if n_replicas > 1 else "")
+        sim = {}
+        if args.tp_sim > 1:
+            par = f"tp{args.tp_sim}-sim (rank-0 shard on one GPU, collectives elided)"
+            # what the real group moves per rank: every step's rows through 2 all-reduces per layer
+            # (o / down row-parallel outputs) + the vocab-parallel embedding all-reduce, bf16
+            lc = llm.cfg
+            rows = sum(t[0] + t[1] for t in trace)
+            ar_calls = (2 * lc.num_layers + 1) * len(trace)
+            sim = {"tp_sim": args.tp_sim,
+                   "allreduce_calls_per_step": 2 * lc.num_layers + 1,
+                   "allreduce_bytes_per_step": round(rows * (2 * lc.num_layers + 1) * lc.hidden * 2 / max(1, len(trace))),
+                   "allreduce_calls": ar_calls,
+                   "rows_per_step": round(rows / max(1, len(trace)), 1),
+                   "decode_only_steps": len(dec_only), "mixed_steps": len(mixed)}
         out = {
             "metric": METRICS[args.workload].format(model=MODEL_NAMES.get(args.model, args.model)),
             "value": round(qps, 3),
@@ -430,6 +453,9 @@ def main():
             "data": f"synthetic ({args.docs} runbook docs -> {n} chunks; random-init weights)",
             "p50_latency_ms": round(p50, 1) if p50 is not None else None,
             "p90_latency_ms": round(p90, 1) if p90 is not None else None,
+            # completions whose tool call executed (HTTP 200) per second: with random weights the
+            # rest end in the reference's own 400 / 500 branches after the same generation work
+            "success_qps": round(statuses.get("200", 0) * (total_req / max(1, len(results))) / t_max, 3),
             "config": {
                 "model": f"{args.model} ({'bf16' if on_gpu else 'fp32, CPU'}, TP={args.tp}) + {args.embedder} embedder",
                 "workload": args.workload,
@@ -461,6 +487,7 @@ def main():
                 "index_build_s": round(t_index, 2),
                 "setup_s": round(tim_setup, 1),
                 "http_status_counts_rank0": statuses,
+                **sim,
             },
         }
         line = json.dumps(out)

@@ -466,7 +466,8 @@ static float prefill_defer() {
   return env;
 }
 
-int lk_prefill_rows_per_tile(int G) { return G >= 4 ? 32 * (prefill_waves(G, 128) / 4) : 32 * (4 / G); }
+// the query rows one workgroup covers: must use the launch's prefill_waves(G, D)
+int lk_prefill_rows_per_tile(int G, int D) { return G >= 4 ? 32 * (prefill_waves(G, D) / 4) : 32 * (4 / G); }
 
 int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v, long ks, long vs,
                      const int* block_tables, int bt_stride, const int* cu_q, const int* ctx_lens,

@@ -373,7 +373,7 @@ at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at
   return out;
 }
 
-int64_t prefill_rows_per_tile(int64_t G) { return lk_prefill_rows_per_tile((int)G); }
+int64_t prefill_rows_per_tile(int64_t G, int64_t D) { return lk_prefill_rows_per_tile((int)G, (int)D); }
 
 at::Tensor flash_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                          const c10::optional<at::Tensor>& block_tables, const at::Tensor& cu_q,
@@ -641,7 +641,11 @@ struct XgmiAr {
 
 }  // namespace
 
+// build provenance: "LKSTAMP:<hash of sources + flags>", generated by csrc/build.py at link time
+extern "C" const char lk_source_stamp[];
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("source_stamp", [] { return std::string(lk_source_stamp + 8); });
   py::class_<XgmiAr>(m, "XgmiAr")
       .def(py::init<int, int, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("bytes"))
       .def("handles", &XgmiAr::handles)

@@ -4,7 +4,10 @@ Compiles every ``csrc/*.hip`` with ``hipcc --offload-arch=gfx950`` straight from
 source (no hipify step: the kernels are written for CDNA4 directly), compiles the
 torch bindings, and links one Python extension module next to the package
 ``__init__``.  Object files are cached under ``build/`` and only rebuilt when the
-source or a header changed, so iterating on one kernel recompiles one file.
+source, a header or the flags changed (content hashes, not mtimes), so iterating on one
+kernel recompiles one file.  The linked library embeds ``LKSTAMP:<hash>`` of every source,
+header and flag (``tree_hash``); ``ops._ext`` refuses to load a library whose stamp does not
+match the sources next to it (utils/provenance.py).
 
     python csrc/build.py            # incremental
     python csrc/build.py --clean    # from scratch
@@ -45,11 +48,44 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
-def _newer(src: Path, obj: Path, headers: list[Path]) -> bool:
-    if not obj.exists():
-        return True
-    t = obj.stat().st_mtime
-    return src.stat().st_mtime > t or any(h.stat().st_mtime > t for h in headers)
+def _provenance():
+    sys.path.insert(0, str(ROOT))
+    try:
+        from llm_kubernetes_minikube_sharp4dev_amd.utils import provenance
+    finally:
+        sys.path.pop(0)
+    return provenance
+
+
+def _codegen_flags(debug: bool = False) -> tuple[list[str], list[str]]:
+    """Flags that shape the generated code (no include paths of the local install)."""
+    common = ["-O3", "-fPIC", "-std=c++17"]
+    if debug:
+        common += ["-DLK_DEBUG", "-g"]
+    kern = common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-ffp-contract=fast"]
+    bind = common + [f"--offload-arch={ARCH}", "-DTORCH_API_INCLUDE_EXTENSION_H", f"-DTORCH_EXTENSION_NAME={EXT_NAME}",
+                     "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1"]
+    return kern, bind
+
+
+def sources() -> list[Path]:
+    return sorted(CSRC.glob("*.hip")) + [CSRC / "bindings.cpp"] + sorted(CSRC.glob("*.h"))
+
+
+def tree_hash(debug: bool = False) -> str:
+    """Content hash of every source / header of ``_C`` plus its code-generation flags: the
+    stamp the linked library must carry."""
+    kern, bind = _codegen_flags(debug)
+    return _provenance().content_hash(sources(), " ".join(kern) + "|" + " ".join(bind), root=ROOT)
+
+
+def so_path() -> Path:
+    return PKG / f"{EXT_NAME}{sysconfig.get_config_var('EXT_SUFFIX') or '.so'}"
+
+
+def _job_key(src: Path, headers: list[Path], cmd: list[str]) -> str:
+    # flags without the local include paths (same image here and on the GPU box)
+    return _provenance().content_hash([src, *headers], " ".join(c for c in cmd if not c.startswith("-I")))
 
 
 def build(clean: bool = False, jobs: int | None = None, verbose: bool = False, debug: bool = False) -> Path:
@@ -86,7 +122,12 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False, d
     bobj = BUILD / "bindings.o"
     jobs_list.append((bsrc, bobj, [hipcc, *bind_flags, "-x", "hip", "-c", str(bsrc), "-o", str(bobj)]))
 
-    todo = [j for j in jobs_list if _newer(j[0], j[1], headers)]
+    def stale(job):
+        src, obj, cmd = job
+        key = obj.with_suffix(".o.key")
+        return not obj.exists() or not key.exists() or key.read_text() != _job_key(src, headers, cmd)
+
+    todo = [j for j in jobs_list if stale(j)]
     n = jobs or min(8, max(1, (os.cpu_count() or 4)))
 
     def run(job):
@@ -96,6 +137,7 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False, d
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"compile failed: {src.name}\n{r.stdout}\n{r.stderr}")
+        obj.with_suffix(".o.key").write_text(_job_key(src, headers, cmd))
         return src.name
 
     if todo:
@@ -103,10 +145,19 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False, d
             for name in ex.map(run, todo):
                 print(f"[build] compiled {name}", flush=True)
 
-    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    out = PKG / f"{EXT_NAME}{suffix}"
-    objs = [j[1] for j in jobs_list]
-    if not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
+    out = so_path()
+    stamp = tree_hash(debug)
+    stamp_src = BUILD / "stamp.cpp"
+    stamp_src.write_text('// generated by csrc/build.py: provenance of the linked library\n'
+                         f'extern "C" __attribute__((used, visibility("default"))) const char lk_source_stamp[] = '
+                         f'"LKSTAMP:{stamp}";\n')
+    stamp_obj = BUILD / "stamp.o"
+    r = subprocess.run([hipcc, "-O2", "-fPIC", "-c", str(stamp_src), "-o", str(stamp_obj)], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"stamp compile failed\n{r.stderr}")
+    objs = [j[1] for j in jobs_list] + [stamp_obj]
+    prov = _provenance()
+    if not out.exists() or todo or prov.read_stamp(out) != stamp:
         link = [
             hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(out),
             f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
@@ -117,7 +168,7 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False, d
         r = subprocess.run(link, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
-        print(f"[build] linked {out.relative_to(ROOT)}", flush=True)
+        print(f"[build] linked {out.relative_to(ROOT)} (stamp {stamp})", flush=True)
     return out
 
 

@@ -197,26 +197,35 @@ LK_DEVICE unsigned fkey(float f) {  // order-preserving float -> uint
   const unsigned u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
+constexpr unsigned kNegInfKey = 0x007FFFFFu;  // fkey(-inf); NaN with the sign bit below it
 LK_DEVICE float keyf(unsigned k) { return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k); }
 
-__global__ __launch_bounds__(256) void sample_penalty_kernel(float* __restrict__ logits, long ls,
+// One workgroup per row.  The window's tokens are de-duplicated through a V-bit "seen" bitmap
+// in LDS (one atomicOr per entry; the thread that sets a token's bit penalises it): O(window)
+// for any repeat_last_n, including -1 (= the whole ring, sized to max_model_len by the engine).
+__global__ __launch_bounds__(256) void sample_penalty_kernel(float* __restrict__ logits, long ls, int V,
                                                              const int* __restrict__ prm,
                                                              const int* __restrict__ hist,
                                                              const int* __restrict__ hist_len, int W) {
+  extern __shared__ unsigned seen[];
   const int row = blockIdx.x;
   const int* p = prm + row * 8;
   const float pen = __int_as_float(p[2]);
   const int last_n = p[4], slot = p[5], reset = p[6];
-  if (pen == 1.f || last_n == 0) return;
+  if (pen == 1.f || last_n == 0) return;  // uniform per workgroup
   const int hl = reset ? 0 : hist_len[slot];
   const int n = min(min(hl, last_n > 0 ? last_n : W), W);
+  if (n == 0) return;
+  const int words = (V + 31) >> 5;
+  for (int i = threadIdx.x; i < words; i += blockDim.x) seen[i] = 0u;
+  __syncthreads();
   const int* h = hist + (long)slot * W;
   float* lp = logits + (long)row * ls;
   for (int j = threadIdx.x; j < n; j += blockDim.x) {
     const int tok = h[(hl - 1 - j) % W];
-    bool dup = false;
-    for (int i = 0; i < j; ++i) dup |= (h[(hl - 1 - i) % W] == tok);
-    if (dup || tok < 0) continue;
+    if (tok < 0 || tok >= V) continue;
+    const unsigned bit = 1u << (tok & 31);
+    if (atomicOr(&seen[tok >> 5], bit) & bit) continue;  // another entry of the window owns it
     const float l = lp[tok];
     lp[tok] = l > 0.f ? l / pen : l * pen;
   }
@@ -288,7 +297,10 @@ __global__ __launch_bounds__(kSampThreads) void sample_topkp_kernel(const float*
   if (tid == 0) ncand_s = 0;
   __syncthreads();
   bitonic(ckey, cidx, kSampThreads);
-  const unsigned t0 = ckey[K - 1];
+  // -inf entries (a grammar mask) are never candidates: with fewer finite entries than K the
+  // bound would otherwise be -inf and every masked entry would flood the candidate list and
+  // the radix fallback's histograms (same-bin atomics).  k_eff below = min(K, finite ones).
+  const unsigned t0 = max(ckey[K - 1], kNegInfKey + 1u);
   __syncthreads();
   // 2. gather every element >= t0
   for (int i = tid; i < V; i += kSampThreads) {
@@ -316,7 +328,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_topkp_kernel(const float*
       __syncthreads();
       for (int i = tid; i < V; i += kSampThreads) {
         const unsigned k = fkey(lp[i]);
-        if ((k & mask) == prefix) atomicAdd(&hst[(k >> shifts[d]) & (nb - 1)], 1u);
+        if (k > kNegInfKey && (k & mask) == prefix) atomicAdd(&hst[(k >> shifts[d]) & (nb - 1)], 1u);
       }
       __syncthreads();
       // thread t owns bins 2t', 2t'+1 counted from the top (t' = 1023 - t)
@@ -378,8 +390,8 @@ __global__ __launch_bounds__(kSampThreads) void sample_topkp_kernel(const float*
   const int k_eff = min(K, nc);
   // 4. temperature softmax over the top K, top-p cut, inverse-CDF draw
   int tok;
-  if (greedy || k_eff == 1) {
-    tok = cidx[0];
+  if (greedy || k_eff <= 1) {
+    tok = k_eff == 0 ? 0 : cidx[0];  // a fully masked row (all -inf) yields id 0
   } else {
     const float v0 = keyf(ckey[0]);
     const float invt = 1.f / temp;
@@ -421,7 +433,17 @@ int lk_sample(float* logits, long ls, int B, int V, const int* prm, int* hist, i
               unsigned long long seed, int* out, hipStream_t st) {
   if (B <= 0) return 0;
   if (V < 1 || W < 1) return -1;
-  sample_penalty_kernel<<<B, 256, 0, st>>>(logits, ls, prm, hist, hist_len, W);
+  const size_t seen_bytes = (size_t)((V + 31) >> 5) * 4;
+  if (seen_bytes > 160 * 1024) return -1;  // the LDS "seen" bitmap: V <= 1.3M
+  if (seen_bytes > 64 * 1024) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(sample_penalty_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+  }
+  sample_penalty_kernel<<<B, 256, seen_bytes, st>>>(logits, ls, V, prm, hist, hist_len, W);
   sample_topkp_kernel<<<B, kSampThreads, 0, st>>>(logits, ls, V, prm, hist, hist_len, W, seed, out);
   return 0;
 }

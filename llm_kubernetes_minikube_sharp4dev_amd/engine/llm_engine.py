@@ -41,7 +41,7 @@ class LLMEngine:
         self.allocator = make_allocator(self.runner.num_blocks, block_size, enable_prefix_caching)
         self.scheduler = Scheduler(self.allocator, block_size, max_num_seqs, max_num_batched_tokens, max_model_len,
                                    token_align, token_align_wave)
-        self.sampler = Sampler(model.cfg.vocab_size, seed)
+        self.sampler = Sampler(model.cfg.vocab_size, seed, history_len=max_model_len)
         self.max_model_len = max_model_len
         if eos_ids is None:
             eos_ids = set(tokenizer.eos_ids) if tokenizer is not None else set(model.cfg.eos_token_ids)

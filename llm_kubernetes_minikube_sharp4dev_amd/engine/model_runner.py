@@ -329,7 +329,7 @@ class ModelRunner:
     def _cascade_meta(self, meta, B: int, shared_len: torch.Tensor):
         """Cascade fields of ``meta`` for B decode rows (static shapes per B: graph-safe)."""
         dev = self.device
-        rpt = ops.prefill_rows_per_tile(self.hq // self.hkv)
+        rpt = ops.prefill_rows_per_tile(self.hq // self.hkv, self.D)
         nt = (B + rpt - 1) // rpt
         meta.shared_len = shared_len
         meta.shared_cu = torch.tensor([0, B], dtype=torch.int32, device=dev)
@@ -364,14 +364,11 @@ class ModelRunner:
         tp = getattr(self.model, "tp", None)
         if not si.prev_bcast or tp is None or not tp.enabled:
             return
-        import torch.distributed as dist
-
         if tp.rank == 0:
             buf = self.prev_ids[: si.prev_bcast].to(torch.int32).contiguous()
         else:
             buf = torch.empty(si.prev_bcast, dtype=torch.int32, device=self.device)
-        dist.broadcast(buf, src=tp.ranks[0] if tp.ranks else 0, group=tp.group)
-        self.prev_ids = buf
+        self.prev_ids = tp.broadcast_(buf)
 
     def forward_logits(self, items, greedy: bool = False):
         """Run one step; returns (rows [(seq,row)], logits [R, V] f32 -- or int32 token

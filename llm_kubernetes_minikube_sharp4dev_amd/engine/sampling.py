@@ -72,9 +72,12 @@ SPARSE_SELECT = os.environ.get("LK_SPARSE_SELECT", "1") != "0"
 
 
 class Sampler:
-    def __init__(self, vocab_size: int, seed: int = 0):
+    def __init__(self, vocab_size: int, seed: int = 0, history_len: int = 256):
         self.vocab_size = vocab_size
         self.seed = seed
+        # the device history ring holds a sequence's whole output (up to max_model_len), so
+        # repeat_last_n > 256 and -1 (Ollama: the whole context) penalise the full history
+        self.RING = max(256, -(-min(int(history_len), 32768) // 256) * 256)
         self.step = 0
         # processors return the same cached list objects for recurring grammar states:
         # memoise their int64 arrays (id -> (list, array); the list reference keeps the id valid)
@@ -133,7 +136,7 @@ class Sampler:
         return out
 
     # ---------------------------------------------------------------- device sampler state
-    RING = 256        # history window per sequence (repeat_last_n is clamped to it)
+    RING = 256        # default history window per sequence (repeat_last_n is clamped to it)
     SLOTS = 1024      # sequences with a live ring (>= 2x max_num_seqs; LRU-evicted beyond)
 
     def _ring(self, dev):

@@ -72,10 +72,10 @@ class AttnMeta:
     def num_tokens(self) -> int:
         return self.num_prefill_tokens + self.num_decode
 
-    def ensure_tiles(self, Hq: int, Hkv: int, device):
+    def ensure_tiles(self, Hq: int, Hkv: int, device, D: int = 128):
         """Build the flash-kernel tile list once per step (GPU only)."""
         if self.tiles is None and self.num_prefill_seqs and device.type == "cuda":
-            ts, tq = ops.prefill_tiles(self.q_lens_cpu, self.ctx_lens_cpu, Hq // Hkv, True)
+            ts, tq = ops.prefill_tiles(self.q_lens_cpu, self.ctx_lens_cpu, Hq // Hkv, True, D)
             self.tiles = (torch.from_numpy(ts).to(device, non_blocking=True),
                           torch.from_numpy(tq).to(device, non_blocking=True))
 
@@ -118,7 +118,7 @@ def paged_attention(qkv: torch.Tensor, k_cache, v_cache, meta: AttnMeta, Hq: int
         qkv.record_stream(side)
         out.record_stream(side)
     if Tp:
-        meta.ensure_tiles(Hq, Hkv, qkv.device)
+        meta.ensure_tiles(Hq, Hkv, qkv.device, D)
         ops.flash_prefill(qkv[:Tp, : Hq * D], k_cache, v_cache, meta.cu_q, Hq, Hkv, D, scale, True,
                           block_tables=meta.block_tables_p, ctx_lens=meta.ctx_lens_p,
                           q_lens_cpu=meta.q_lens_cpu, ctx_lens_cpu=meta.ctx_lens_cpu,

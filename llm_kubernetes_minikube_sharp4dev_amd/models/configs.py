@@ -115,3 +115,8 @@ def param_count(cfg: DecoderConfig) -> int:
     mlp = (3 if cfg.activation == "silu" else 2) * H * I
     emb = V * H * (1 if cfg.tie_word_embeddings else 2)
     return L * (qkv + o + mlp + 2 * H) + emb + H
+
+
+def pad_vocab(n: int, tile: int = 256) -> int:
+    """Rows of an LM head padded to the MFMA GEMM kernels' 256-column tile."""
+    return -(-n // tile) * tile

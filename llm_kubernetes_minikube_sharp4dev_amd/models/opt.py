@@ -14,7 +14,7 @@ import torch.nn as nn
 from .. import ops
 from ..parallel.tp import SINGLE, TPGroup
 from .attention import AttnMeta, paged_attention
-from .configs import DecoderConfig
+from .configs import DecoderConfig, pad_vocab
 
 
 class OPTLayerWeights(nn.Module):
@@ -48,7 +48,10 @@ class OPTModel(nn.Module):
         self.cp_group = None
         e = dict(dtype=dtype, device=device)
         self.vocab_lo, self.vocab_hi = 0, cfg.vocab_size
-        self.embed = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden, **e), requires_grad=False)
+        self.vocab_local = cfg.vocab_size
+        # tied embedding / LM head padded to the GEMM's 256-column tile (50272 -> 50432 zero
+        # rows; logits sliced back): the head runs on the MFMA kernels, not the vendor library
+        self.embed = nn.Parameter(torch.empty(pad_vocab(cfg.vocab_size), cfg.hidden, **e), requires_grad=False)
         self.pos_embed = nn.Parameter(torch.empty(cfg.max_position + cfg.pos_offset, cfg.hidden, **e),
                                       requires_grad=False)
         self.layers = nn.ModuleList([OPTLayerWeights(cfg, tp, dtype, device) for _ in range(cfg.num_layers)])
@@ -67,6 +70,7 @@ class OPTModel(nn.Module):
             else:
                 g = torch.Generator(device=gen_dev).manual_seed(seed * 7919 + i * 104729 + self.tp.rank)
                 p.copy_(torch.randn(p.shape, generator=g, device=gen_dev).mul_(std).to(p.dtype))
+        self.embed[self.vocab_local:].zero_()
         return self
 
     def forward(self, ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
@@ -102,12 +106,16 @@ class OPTModel(nn.Module):
             x = x.index_select(0, meta.logits_idx)
         return x
 
-    def logits(self, hidden, gather: bool = True, dtype=torch.float32):
+    def head(self, hidden):
         lg = ops.linear(hidden, self.lm_head)
+        return lg[:, : self.vocab_local] if lg.shape[1] != self.vocab_local else lg
+
+    def logits(self, hidden, gather: bool = True, dtype=torch.float32):
+        lg = self.head(hidden)
         return lg.to(dtype) if dtype is not None else lg
 
     def greedy(self, hidden):
-        return ops.linear(hidden, self.lm_head).float().argmax(dim=-1).int()
+        return self.tp.greedy_ids(self.head(hidden), self.vocab_lo)
 
     @torch.no_grad()
     def load_hf_state_dict(self, sd: dict):
@@ -120,7 +128,8 @@ class OPTModel(nn.Module):
 
         s, e = tp.shard(cfg.num_heads)
         fs, fe = tp.shard(cfg.intermediate)
-        self.embed.copy_(t("model.decoder.embed_tokens.weight"))
+        self.embed[: self.vocab_local].copy_(t("model.decoder.embed_tokens.weight"))
+        self.embed[self.vocab_local:].zero_()
         self.pos_embed.copy_(t("model.decoder.embed_positions.weight")[: self.pos_embed.shape[0]])
         for i, L in enumerate(self.layers):
             p = f"model.decoder.layers.{i}."

@@ -26,22 +26,37 @@ def sanitized_so_path() -> Path:
     return ROOT / "build" / "asan" / so_path().name
 
 
+def _opt(sanitize: bool) -> list:
+    return (["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
+            if sanitize else ["-O3"])
+
+
+def tree_hash(sanitize: bool = False) -> str:
+    """Content hash of csrc/runtime's sources + flags: the stamp the built module carries."""
+    from ..utils.provenance import content_hash
+
+    deps = sorted(SRC.glob("*.cpp")) + sorted(SRC.glob("*.h"))
+    return content_hash(deps, " ".join(_opt(sanitize) + ["-std=c++17"]), root=ROOT)
+
+
 def build(verbose: bool = False, sanitize: bool = False) -> Path:
     """Compile csrc/runtime/*.cpp into the package (``sanitize=True``: an ASan + UBSan build
-    under build/asan/, loaded by setting LK_NATIVE_RUNTIME_SO and preloading libasan)."""
+    under build/asan/, loaded by setting LK_NATIVE_RUNTIME_SO and preloading libasan).
+    Rebuilds whenever the embedded source stamp differs from the tree's (content, not mtime)."""
     import pybind11
+
+    from ..utils.provenance import read_stamp
 
     out = sanitized_so_path() if sanitize else so_path()
     out.parent.mkdir(parents=True, exist_ok=True)
     srcs = sorted(SRC.glob("*.cpp"))
-    deps = srcs + sorted(SRC.glob("*.h"))
-    if out.exists() and all(s.stat().st_mtime <= out.stat().st_mtime for s in deps):
+    stamp = tree_hash(sanitize)
+    if out.exists() and read_stamp(out) == stamp:
         return out
     cxx = os.environ.get("CXX", "g++")
-    opt = (["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
-           if sanitize else ["-O3"])
-    cmd = [cxx, *opt, "-shared", "-fPIC", "-std=c++17", "-Wall", "-pthread", f"-I{pybind11.get_include()}",
-           f"-I{sysconfig.get_paths()['include']}", *map(str, srcs), "-o", str(out)]
+    cmd = [cxx, *_opt(sanitize), "-shared", "-fPIC", "-std=c++17", "-Wall", "-pthread", f"-I{pybind11.get_include()}",
+           f"-I{sysconfig.get_paths()['include']}", f'-DLK_SOURCE_STAMP="LKSTAMP:{stamp}"', *map(str, srcs),
+           "-o", str(out)]
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -60,6 +75,10 @@ def load():
             _mod = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(_mod)
         else:
+            if SRC.exists() and os.environ.get("LK_ALLOW_STALE_EXT", "0") != "1":
+                from ..utils.provenance import check
+
+                check(so_path(), tree_hash(), "native runtime _runtime", "python -m llm_kubernetes_minikube_sharp4dev_amd.native.runtime")
             _mod = importlib.import_module("llm_kubernetes_minikube_sharp4dev_amd.native._runtime")
     return _mod
 
@@ -132,5 +151,6 @@ class NativeBlockAllocator:
 
 if __name__ == "__main__":  # pragma: no cover
     build(verbose=True)
+    _mod = None
     print("native runtime available:", available())
     sys.exit(0)

@@ -128,19 +128,19 @@ def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_
     return y
 
 
-def prefill_rows_per_tile(G: int) -> int:
-    """Query rows per flash-prefill tile: the HIP library's choice (8-wave 64-row
-    workgroups for GQA groups of >= 4 heads unless LK_PREFILL_WAVES=4), else 32 / 4-wave."""
+def prefill_rows_per_tile(G: int, D: int = 128) -> int:
+    """Query rows per flash-prefill tile: the HIP library's choice for (GQA group, head dim)
+    (8-wave 64-row workgroups for G >= 4, D >= 64 under LK_PREFILL_WAVES=8), else 32 / 4-wave."""
     try:
-        return int(lib().prefill_rows_per_tile(G))
+        return int(lib().prefill_rows_per_tile(G, D))
     except Exception:  # no extension (CPU): the tiles only matter to the HIP kernel
         return 32 if G >= 4 else 32 * (4 // G)
 
 
-def prefill_tiles(q_lens: Sequence[int], ctx_lens: Sequence[int], G: int, causal: bool):
+def prefill_tiles(q_lens: Sequence[int], ctx_lens: Sequence[int], G: int, causal: bool, D: int = 128):
     """Query tiles (seq, q0) for the flash kernel, heaviest first (LPT scheduling:
     with causal masking a tile's cost grows with the keys it sees)."""
-    qb = prefill_rows_per_tile(G)
+    qb = prefill_rows_per_tile(G, D)
     seqs, q0s, cost = [], [], []
     for b, (ql, cl) in enumerate(zip(q_lens, ctx_lens)):
         past = cl - ql
@@ -174,7 +174,7 @@ def flash_prefill(q, k, v, cu_q, Hq: int, Hkv: int, D: int, scale: float, causal
                 need = max((int(c) + BS - 1) // BS for c in ctx_lens_cpu) if ctx_lens_cpu else 0
                 if need > block_tables.shape[1]:
                     raise ValueError("block table too narrow for the context lengths")
-            ts, tq = prefill_tiles(q_lens_cpu, ctx_lens_cpu, Hq // Hkv, causal)
+            ts, tq = prefill_tiles(q_lens_cpu, ctx_lens_cpu, Hq // Hkv, causal, D)
             tiles = (torch.from_numpy(ts).to(q.device, non_blocking=True),
                      torch.from_numpy(tq).to(q.device, non_blocking=True))
         pp_o, pp_ml = part if part is not None else (None, None)
@@ -386,7 +386,7 @@ def gemm(x, w, b=None, epi: int = 0, out=None):
         cfg = _gemm_default(M, N, K, epi)
         if cfg is None or not lib().gemm_supported(M, N, K, epi, cfg[1], cfg[2]):
             return None
-    return lib().gemm(x, w, b, epi, cfg[1], out, cfg[0], cfg[2] if len(cfg) > 2 else 1)
+    return lib().gemm(x, w, b, epi, cfg[1], out, cfg[0], cfg[2])
 
 
 def _library(x, w, b, act, key):
@@ -444,7 +444,11 @@ def tune_gemm(weights, max_m: int, min_m: int = 512, iters: int = 6, cold_bytes:
                     ts[c].append(once(f))
             med = {c: statistics.median(v) for c, v in ts.items()}
             key = _gemm_key(mb * 256, N, K, epi)
-            _GEMM_TABLE[key] = min(med, key=med.get)
+            sched, bn = min(med, key=med.get)
+            # keep the default policy's split-K for the winning tile (a 2-tuple
+            # entry silently dropped it on the low-tile-count O / down shapes)
+            ks = _gemm_splits(mb * 256, N, K, epi, bn)
+            _GEMM_TABLE[key] = (sched, bn, ks if L.gemm_supported(mb * 256, N, K, epi, bn, ks) else 1)
             out[key] = {f"s{c[0]}/{c[1]}": round(t, 1) for c, t in med.items()}
         del copies
     return out

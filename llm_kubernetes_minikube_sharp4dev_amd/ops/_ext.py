@@ -33,6 +33,8 @@ def try_lib():
                 import torch  # noqa: F401  (loads libamdhip64 / libtorch first)
 
                 alt = os.environ.get("LK_LIB_PATH")
+                if not alt:
+                    verify_stamp()
                 if alt:  # A/B knob: another build of this extension (e.g. the previous commit's)
                     spec = importlib.util.spec_from_file_location("llm_kubernetes_minikube_sharp4dev_amd._C", alt)
                     _mod = importlib.util.module_from_spec(spec)
@@ -44,6 +46,36 @@ def try_lib():
             except Exception as e:  # pragma: no cover - depends on build state
                 _err = e
     return _mod
+
+
+def _csrc_build():
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[2]
+    if not (root / "csrc" / "build.py").exists():
+        return None
+    sys.path.insert(0, str(root / "csrc"))
+    try:
+        import build as _b  # csrc/build.py
+    finally:
+        sys.path.pop(0)
+    return _b
+
+
+def verify_stamp() -> str | None:
+    """Refuse a ``_C`` whose embedded source stamp differs from the sources in this tree
+    (a stale binary would otherwise run silently).  ``LK_EXT_AUTOBUILD=1`` rebuilds first;
+    ``LK_ALLOW_STALE_EXT=1`` skips the check.  Returns the stamp (None: no csrc/ tree)."""
+    b = _csrc_build()
+    if b is None or os.environ.get("LK_ALLOW_STALE_EXT", "0") == "1":
+        return None
+    from ..utils import provenance
+
+    expected = b.tree_hash()
+    if os.environ.get("LK_EXT_AUTOBUILD", "0") == "1" and provenance.read_stamp(b.so_path()) != expected:
+        b.build()
+    return provenance.check(b.so_path(), expected, "HIP kernel library _C", "python csrc/build.py")
 
 
 def lib():
@@ -67,13 +99,4 @@ def use_hip(t) -> bool:
 
 def build_if_needed(verbose: bool = False):
     """Compile the library in-tree (used by __graft_entry__.build and tests)."""
-    import sys
-    from pathlib import Path
-
-    root = Path(__file__).resolve().parents[2]
-    sys.path.insert(0, str(root / "csrc"))
-    try:
-        import build as _b  # csrc/build.py
-    finally:
-        sys.path.pop(0)
-    return _b.build(verbose=verbose)
+    return _csrc_build().build(verbose=verbose)

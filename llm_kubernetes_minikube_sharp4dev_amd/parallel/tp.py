@@ -90,6 +90,12 @@ class TPGroup:
         k = v.argmax(dim=0)
         return i.gather(0, k[None]).squeeze(0).int()
 
+    def broadcast_(self, t: torch.Tensor) -> torch.Tensor:
+        """In place: the group leader's ``t`` on every rank."""
+        if self.size > 1:
+            dist.broadcast(t, src=self.ranks[0] if self.ranks else 0, group=self.group)
+        return t
+
     def shard(self, n: int) -> tuple[int, int]:
         """[start, end) of this rank's slice of a dimension of size n (n % size == 0)."""
         if n % self.size:
@@ -99,6 +105,44 @@ class TPGroup:
 
 
 SINGLE = TPGroup()
+
+
+@dataclass
+class SimulatedTPGroup(TPGroup):
+    """Rank ``rank`` of a TP group of ``size`` ranks, simulated in ONE process on one device.
+
+    The model instantiates exactly that rank's shard (its heads, its slice of the FFN, its
+    vocab shard of the embedding / LM head), and every collective is a local stand-in with
+    the real output shape: all-reduce = identity, reduce-scatter = this rank's rows,
+    all-gathers = this rank's part replicated.  Values are one rank's partial sums, not the
+    model's (random-init weights either way), but every kernel the rank runs runs at its
+    serving shape -- so a single MI355X measures the per-rank compute of a 70B TP=8 step,
+    and rocprof shows which kernels that rank would run (``bench.py --tp-sim 8``).  The
+    collectives themselves are budgeted from their message sizes (bench.py reports the
+    all-reduce bytes of the timed steps)."""
+
+    simulated: bool = True
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        return t
+
+    def reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:
+        n = t.shape[0] // self.size
+        return t[self.rank * n:(self.rank + 1) * n].contiguous()
+
+    def all_gather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        return t.repeat(self.size, *([1] * (t.dim() - 1)))
+
+    def all_gather_cat(self, t: torch.Tensor, dim: int = -1) -> torch.Tensor:
+        return torch.cat([t] * self.size, dim=dim)
+
+    def greedy_ids(self, local_logits: torch.Tensor, vocab_lo: int = 0) -> torch.Tensor:
+        from .. import ops
+
+        return (ops.select_tokens(local_logits).long() + vocab_lo).int()
+
+    def broadcast_(self, t: torch.Tensor) -> torch.Tensor:
+        return t
 
 
 def init_distributed(backend: Optional[str] = None) -> TPGroup:

@@ -151,17 +151,27 @@ class _ShmChannel:
             self.acks[:] = 0
         self.me, self.n_workers, self.next = worker_index, n_workers, 1
         self.created = create
+        # a worker that stops acknowledging (crash, hang) fails the driver's step instead of
+        # spinning it forever: the engine's failure path then ends the in-flight requests
+        self.timeout_s = float(os.environ.get("LK_TP_CTRL_TIMEOUT_S", "120"))
 
     def send(self, h: np.ndarray, payload: np.ndarray):
         n = int(self.seq[0]) + 1
         nbytes = h.nbytes + payload.nbytes
         if nbytes > self.SLOT:
             raise ValueError(f"control message of {nbytes} B exceeds the {self.SLOT} B slot")
-        spins = 0
+        spins, t0 = 0, 0.0
         while n > 2 and int(self.acks[: self.n_workers].min()) < n - 2:  # slot still being read
             spins += 1
             if spins > 2000:
                 time.sleep(5e-5)
+                if t0 == 0.0:
+                    t0 = time.monotonic()
+                elif spins % 1000 == 0 and time.monotonic() - t0 > self.timeout_s:
+                    late = [i for i in range(self.n_workers) if int(self.acks[i]) < n - 2]
+                    raise RuntimeError(
+                        f"TP control channel: worker(s) {late} did not take message {n - 2} within "
+                        f"{self.timeout_s:.0f} s (LK_TP_CTRL_TIMEOUT_S); a rank crashed or hung")
         slot = self.slots[n & 1]
         slot[: h.nbytes] = h.view(np.uint8)
         slot[h.nbytes: nbytes] = payload.view(np.uint8)

@@ -560,3 +560,27 @@ def test_router_proxies_streams_and_fails_over():
             assert st[live]["served"] == 5 and st[live]["inflight"] == 0 and st[dead]["inflight"] == 0
     finally:
         srv.should_exit = True
+
+
+def test_shm_control_send_fails_when_a_worker_stops_acknowledging(monkeypatch):
+    """the driver's send() must not spin forever behind a dead TP worker."""
+    import numpy as np
+
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp_engine import _ShmChannel
+
+    monkeypatch.setenv("LK_TP_CTRL_TIMEOUT_S", "0.5")
+    name = f"lk_test_ctrl_{os.getpid()}"
+    drv = _ShmChannel(name, True, n_workers=1)
+    wk = _ShmChannel(name, False, worker_index=0, n_workers=1)
+    try:
+        h = np.zeros(8, dtype=np.int64)
+        p = np.zeros(4, dtype=np.int32)
+        drv.send(h, p)
+        drv.send(h, p)
+        wk.recv()  # the worker takes message 1, then "dies"
+        drv.send(h, p)  # slot of message 1 is free
+        with pytest.raises(RuntimeError, match="did not take message 2"):
+            drv.send(h, p)  # needs message 2 acknowledged: never happens
+    finally:
+        wk.close()
+        drv.close()

@@ -61,3 +61,21 @@ def test_seeded_requests_are_reproducible():
         p = SamplingParams(seed=42)
         outs.append([int(s(base.clone(), [p], [[]], ["r"])[0]) for _ in range(4)])
     assert outs[0] == outs[1]
+
+
+def test_whole_history_window_is_not_clamped_to_256():
+    """repeat_last_n = -1 / > 256: the engine sizes the ring to max_model_len, so a token
+    generated 500 steps back is still penalised (it used to be capped at 256)."""
+    s = Sampler(50, seed=0, history_len=2048)
+    assert s.RING == 2048
+    p = SamplingParams(temperature=0.0, top_k=0, top_p=1.0, repeat_penalty=4.0, repeat_last_n=-1)
+    lg = torch.zeros(1, 50)
+    lg[0, 7] = 3.0
+    lg[0, 9] = 1.0
+    assert int(s(lg.clone(), [p], [[]], ["k"])[0]) == 7
+    flat = torch.zeros(1, 50)
+    flat[0, 11] = 0.5
+    for _ in range(500):  # 500 more tokens, none of them 7
+        assert int(s(flat.clone(), [p], [[]], ["k"])[0]) != 7
+    # token 7 is 500 entries back: 3.0 / 4 = 0.75 < 1.0, so 9 wins
+    assert int(s(lg.clone(), [p], [[]], ["k"])[0]) == 9

@@ -144,3 +144,66 @@ def test_sampler_engine_path_uses_the_kernel(hip):
     s.release("a")
     assert "a" not in s._slot_of
     assert math.isfinite(float(logits.sum()))
+
+
+@pytest.mark.parametrize("last_n", [-1, 600])
+def test_repeat_penalty_window_longer_than_256(hip, last_n):
+    """repeat_last_n = -1 (Ollama: whole context) and > 256 penalise the whole generated
+    history: a 1000-entry ring with every token repeated, greedy rows, kernel == reference."""
+    torch.manual_seed(4)
+    V, B, W = 128256, 8, 1024
+    logits = torch.randn(B, V) * 2
+    hist = torch.randint(0, 700, (B, W), dtype=torch.int32)
+    hl = torch.full((B,), 1000, dtype=torch.int32)
+    logits[:, :700] += 8.0  # the penalised ids dominate: a missed penalty changes the argmax
+    prm = _prm(B, temp=0.0, pen=3.0, last_n=last_n, reset=0)
+    h_ref, l_ref = hist.clone(), hl.clone()
+    exp = ref.sample(logits.clone(), prm, h_ref, l_ref)
+    got = ops.sample(logits.to(DEV), prm.to(DEV), hist.to(DEV), hl.to(DEV))
+    assert torch.equal(got.cpu(), exp.cpu())
+    # an entry 549 tokens back (outside a 256 ring) flips the choice
+    only_old = torch.randint(700, 800, (B, W), dtype=torch.int32)
+    only_old[:, 450] = 5
+    lg = torch.full((B, V), -10.0)
+    lg[:, 5] = 9.0
+    lg[:, 750] = 4.0
+    got2 = ops.sample(lg.to(DEV), _prm(B, temp=0.0, pen=3.0, last_n=last_n, reset=0).to(DEV),
+                      only_old.to(DEV), torch.full((B,), 1000, dtype=torch.int32, device=DEV))
+    assert (got2.cpu() == 750).all()  # token 5 sits 549 entries back in the window: penalised
+
+
+def test_sampler_ring_covers_max_model_len(hip):
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import Sampler, SamplingParams
+
+    s = Sampler(1000, seed=5, history_len=4000)
+    assert s.RING >= 4000
+    p = SamplingParams(temperature=0.0, top_k=0, top_p=1.0, repeat_penalty=5.0, repeat_last_n=-1)
+    lg = torch.zeros(1, 1000, device=DEV)
+    lg[0, :600] = torch.linspace(10.0, 9.0, 600, device=DEV)
+    seen = []
+    for _ in range(600):  # greedy + a strong whole-history penalty walks 600 distinct ids
+        seen.append(int(s(lg.clone(), [p], [[]], ["x"])[0]))
+    assert len(set(seen)) == 600
+
+
+def test_grammar_masked_rows_with_penalty(hip):
+    """rows where a grammar mask leaves fewer finite logits than top_k (a literal
+    state: 1-3 allowed ids) under Ollama's default chain sample only allowed ids (no -inf
+    flood of the candidate list / radix fallback); an all -inf row yields id 0."""
+    torch.manual_seed(6)
+    V, B = 128256, 64
+    logits = torch.full((B, V), float("-inf"), device=DEV)
+    allowed = torch.randint(0, V, (B, 3), device=DEV)
+    for j in range(3):
+        logits[torch.arange(B, device=DEV), allowed[:, j]] = torch.randn(B, device=DEV)
+    logits[B - 1] = float("-inf")
+    hist = torch.randint(0, V, (B, 64), dtype=torch.int32, device=DEV)
+    hl = torch.full((B,), 64, dtype=torch.int32, device=DEV)
+    hist[:, 0] = allowed[:, 0].int()  # one allowed id is in the penalty window
+    out = ops.sample(logits.clone(), _prm(B, temp=0.8, top_k=40, top_p=0.9, pen=1.1, reset=0).to(DEV),
+                     hist, hl, seed=11)
+    ok = (out[:, None].long() == allowed).any(1)
+    assert ok[: B - 1].all()
+    assert int(out[B - 1]) == 0
+    g = ops.sample(logits.clone(), _prm(B, temp=0.0, top_k=40, pen=1.1, reset=0).to(DEV), hist, hl)
+    assert ((g[: B - 1, None].long() == allowed[: B - 1]).any(1)).all() and int(g[B - 1]) == 0
