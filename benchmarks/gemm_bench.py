@@ -28,7 +28,8 @@ EPI = {"none": 0, "swiglu": 1, "bias": 2, "gelu": 3, "relu": 4}
 # Llama-3-8B projections at the mixed-step operating points (M buckets of the engine),
 # the LM head is not here (M <= 256: weight-streaming regime), bge-base encoder layers
 LLAMA = [(6144, 4096, "none"), (4096, 4096, "none"), (28672, 4096, "swiglu"), (4096, 14336, "none")]
-VARIANTS = [int(v) for v in os.environ.get("LK_GEMM_VARIANTS", "0,1").split(",")]
+# K-loop schedules of csrc/gemm.hip (0 / 1 / 2) and "4w" = the one-wave-per-SIMD kernel csrc/gemm4w.hip
+VARIANTS = [v if v == "4w" else int(v) for v in os.environ.get("LK_GEMM_VARIANTS", "0,1").split(",")]
 SPLITS = [int(v) for v in os.environ.get("LK_GEMM_SPLITS", "1").split(",")]
 BGE = [(2304, 768, "bias"), (768, 768, "bias"), (3072, 768, "gelu"), (768, 3072, "bias")]
 
@@ -116,9 +117,15 @@ def main():
         best = None
         t_lib = []
         cfgs = [(v, bn, sp) for v in VARIANTS for bn in bns for sp in SPLITS
-                if L.gemm_supported(M, N, K, EPI[epi], bn, sp)]
+                if (L.gemm4w_supported(M, N, K, EPI[epi], sp) and bn == 256 if v == "4w"
+                    else L.gemm_supported(M, N, K, EPI[epi], bn, sp))]
         t_ours = {c: [] for c in cfgs}
-        fns = {c: (lambda c=c: L.gemm(x, wnext(), b, EPI[epi], c[1], None, c[0], c[2])) for c in cfgs}
+
+        def mk(c):
+            if c[0] == "4w":
+                return lambda: L.gemm4w(x, wnext(), b, EPI[epi], None, c[2])
+            return lambda: L.gemm(x, wnext(), b, EPI[epi], c[1], None, c[0], c[2])
+        fns = {c: mk(c) for c in cfgs}
         for bn in cfgs:
             y = fns[bn]()
             err = (y[rs].float() - refv).abs().max().item()

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--K", type=int, default=14336)
     ap.add_argument("--epi", default="none")
     ap.add_argument("--bn", type=int, default=256)
-    ap.add_argument("--impl", default="ours")
+    ap.add_argument("--impl", default="ours", help="ours (gemm.hip) | 4w (gemm4w.hip) | lib (hipBLASLt)")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--variant", type=int, default=0, help="K-loop schedule (0: 4-phase, 1: 2-phase)")
     a = ap.parse_args()
@@ -36,6 +36,9 @@ def main():
     if a.impl == "ours":
         L = ops.lib()
         fn = lambda: L.gemm(x, w, b, EPI[a.epi], a.bn, None, a.variant)  # noqa: E731
+    elif a.impl == "4w":  # csrc/gemm4w.hip
+        L = ops.lib()
+        fn = lambda: L.gemm4w(x, w, b, EPI[a.epi])  # noqa: E731
     else:
         fn = lambda: F.linear(x, w, b)  # noqa: E731
     for _ in range(a.iters):

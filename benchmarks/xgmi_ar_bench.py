@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Per-call latency of the TP decode tail on one MI355X: two processes share the GPU and map
+each other's IPC buffers (the xGMI code path, minus the link): fused all-reduce + residual +
+RMSNorm (one kernel) vs one-shot all-reduce then the add+norm kernel, for B x 8192 bf16
+messages (B = 1 .. 256, the 70B TP=8 decode batch).  Each call is timed from a captured
+hipGraph of 50 back-to-back calls (launch overhead excluded, as in the decode graphs).
+
+    python benchmarks/xgmi_ar_bench.py [--json out.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import sys
+import tempfile
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+H = 8192
+BS = [1, 4, 16, 64, 128, 256]
+REPS = 50
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from llm_kubernetes_minikube_sharp4dev_amd import ops
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp import TPGroup
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.xgmi_ar import XgmiAllReduce
+
+    tp = TPGroup(rank, world, dist.group.WORLD, ctrl=dist.group.WORLD, ranks=list(range(world)))
+    ar = XgmiAllReduce(tp, 8 << 20)
+    rows = []
+    for B in BS:
+        x = torch.randn(B, H, device="cuda").to(torch.bfloat16)
+        res = torch.randn(B, H, device="cuda").to(torch.bfloat16)
+        w = torch.ones(H, device="cuda", dtype=torch.bfloat16)
+        o = torch.empty_like(x)
+        arms = {
+            "fused": lambda: ar.all_reduce_rmsnorm_(x, res, w, 1e-5, o),
+            "ar_then_norm": lambda: ops.lib().rmsnorm(ar.all_reduce_(x), w, 1e-5, res, o),
+            "allreduce_only": lambda: ar.all_reduce_(x),
+        }
+        rec = {"B": B, "bytes": B * H * 2}
+        for name, fn in arms.items():
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(3):
+                    fn()
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(REPS):
+                    fn()
+            dist.barrier()
+            ts = []
+            for _ in range(5):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                dist.barrier()
+                a.record()
+                g.replay()
+                b.record()
+                b.synchronize()
+                ts.append(a.elapsed_time(b) * 1e3 / REPS)
+            rec[name + "_us"] = round(sorted(ts)[len(ts) // 2], 2)
+        rec["error"] = ar.error()
+        rows.append(rec)
+    if rank == 0:
+        torch.save(rows, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "rows.pt")
+        mp.spawn(_worker, args=(2, _port(), out), nprocs=2, join=True)
+        rows = torch.load(out, weights_only=True)
+    for r in rows:
+        print(json.dumps(r), flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump({"note": "2 processes on ONE MI355X (IPC-mapped, no xGMI link): kernel + handshake floor; "
+                               "per-call us from hipGraph replays of 50 calls", "H": H, "rows": rows}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -261,6 +261,37 @@ at::Tensor gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at
   return out;
 }
 
+// One-wave-per-SIMD 256 x 256 variant (csrc/gemm4w.hip), same contract as gemm() with bn = 256.
+at::Tensor gemm4w(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t epi,
+                  const c10::optional<at::Tensor>& out_, int64_t splits) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_LASTDIM(x); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "x [M,K], w [N,K]");
+  check_rows16(x, "x"); check_rows16(w, "w");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(lk_gemm4w_supported(M, N, K, (int)epi, (int)splits), "gemm4w: unsupported shape M", M, " N", N, " K", K,
+              " epi", epi, " splits", splits);
+  if (epi >= 2) {
+    TORCH_CHECK(bias.has_value(), "gemm4w: this epilogue needs a bias");
+    CHECK_CUDA(*bias); CHECK_BF16(*bias); CHECK_CONTIG(*bias);
+    TORCH_CHECK(bias->numel() == N && reinterpret_cast<uintptr_t>(bias->data_ptr()) % 16 == 0, "gemm4w: bias [N], 16-B aligned");
+  }
+  const int n_out = epi == 1 ? N / 2 : N;
+  at::Tensor out = out_ ? *out_ : at::empty({M, n_out}, x.options());
+  CHECK_BF16(out); CHECK_LASTDIM(out);
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == n_out, "out shape");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0 && out.stride(0) % 8 == 0, "out alignment (16 B)");
+  at::Tensor ws;
+  if (splits > 1) ws = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
+  int rc = lk_gemm4w(bp(x), x.stride(0), bp(w), epi >= 2 ? bp(*bias) : nullptr, M, N, K, (int)epi, bp(out),
+                     out.stride(0), cur_stream(), (int)splits, splits > 1 ? ws.data_ptr<float>() : nullptr);
+  CHECK_RC(rc, "gemm4w");
+  return out;
+}
+
+bool gemm4w_supported(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t splits) {
+  return lk_gemm4w_supported((int)M, (int)N, (int)K, (int)epi, (int)splits) != 0;
+}
+
 bool gemm_supported(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bn, int64_t splits) {
   return lk_gemm_supported((int)M, (int)N, (int)K, (int)epi, (int)bn, (int)splits) != 0;
 }
@@ -632,6 +663,19 @@ struct XgmiAr {
                                rank, world, bp(in), bp(out), in.numel(), err, cur_stream());
     CHECK_RC(rc, "xgmi_allreduce");
   }
+  // out = RMSNorm(allreduce(x) + residual) * w with residual updated in place (one kernel)
+  void all_reduce_rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, double eps, at::Tensor& out) {
+    CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(residual); CHECK_BF16(w); CHECK_BF16(out);
+    CHECK_CONTIG(x); CHECK_CONTIG(residual); CHECK_CONTIG(w); CHECK_CONTIG(out);
+    TORCH_CHECK(x.dim() == 2 && residual.sizes() == x.sizes() && out.sizes() == x.sizes() && w.numel() == x.size(1),
+                "xgmi_ar_rmsnorm: x / residual / out [T, H], w [H]");
+    TORCH_CHECK(x.size(1) % 8 == 0 && (size_t)x.numel() * 2 <= bytes, "xgmi_ar_rmsnorm: H % 8 and the staging size");
+    for (int r = 0; r < world; ++r) TORCH_CHECK(pdata[r] && psig[r], "xgmi_ar: open() not called");
+    int rc = lk_xgmi_allreduce_rmsnorm(reinterpret_cast<bf16_t* const*>(pdata.data()),
+                                       reinterpret_cast<unsigned* const*>(psig.data()), rank, world, bp(x), bp(residual),
+                                       bp(w), bp(out), (int)x.size(0), (int)x.size(1), (float)eps, err, cur_stream());
+    CHECK_RC(rc, "xgmi_allreduce_rmsnorm");
+  }
   int error() const {
     int h = 0;
     TORCH_CHECK(hipMemcpy(&h, err, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess, "xgmi_ar: read error word");
@@ -651,6 +695,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("handles", &XgmiAr::handles)
       .def("open", &XgmiAr::open)
       .def("all_reduce", &XgmiAr::all_reduce)
+      .def("all_reduce_rmsnorm", &XgmiAr::all_reduce_rmsnorm)
       .def("error", &XgmiAr::error)
       .def_readonly("bytes", &XgmiAr::bytes);
   m.doc() = "gfx950 (MI355X) HIP kernel library";
@@ -663,6 +708,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ws_linear", &ws_linear, "", py::arg("x"), py::arg("w"), py::arg("swiglu") = false, py::arg("bn") = 0,
         py::arg("splits") = 0, py::arg("out") = py::none());
   m.def("ws_plan", &ws_plan);
+  m.def("gemm4w", &gemm4w, "", py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("epi") = 0,
+        py::arg("out") = py::none(), py::arg("splits") = 1);
+  m.def("gemm4w_supported", &gemm4w_supported, "", py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"),
+        py::arg("splits") = 1);
   m.def("gemm", &gemm, "", py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("epi") = 0,
         py::arg("bn") = 256, py::arg("out") = py::none(), py::arg("variant") = 1,
         py::arg("splits") = 1);

@@ -46,6 +46,9 @@ int lk_ws_scores_f32(const bf16_t* x, long ldx, const bf16_t* w, int M, long N, 
 // xgmi_allreduce.hip (one-shot all-reduce over IPC-mapped peer buffers, K14)
 int lk_xgmi_ar_sig_words();
 int lk_xgmi_ar_max_ranks();
+int lk_xgmi_allreduce_rmsnorm(bf16_t* const* data, unsigned* const* sig, int rank, int world, const bf16_t* in,
+                              bf16_t* residual, const bf16_t* w, bf16_t* out, int T, int H, float eps, int* err,
+                              hipStream_t st);
 int lk_xgmi_allreduce(bf16_t* const* data, unsigned* const* sig, int rank, int world, const bf16_t* in,
                       bf16_t* out, long n, int* err, hipStream_t st);
 
@@ -54,6 +57,9 @@ int lk_xgmi_allreduce(bf16_t* const* data, unsigned* const* sig, int rank, int w
 // ks > 1: split-K over ks K-ranges, fp32 partials in ws [ks, M, N], then a reduce applies the
 // epilogue (not SwiGLU) -- for shapes with fewer tiles than CUs
 int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks = 1);
+int lk_gemm4w_supported(int M, int N, int K, int epi, int ks);
+int lk_gemm4w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi,
+              bf16_t* out, long ldo, hipStream_t st, int ks, float* ws);
 int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
             int variant, bf16_t* out, long ldo, hipStream_t st, int ks = 1, float* ws = nullptr);
 

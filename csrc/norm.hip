@@ -7,6 +7,7 @@
 // "add + norm" that replaces two separate elementwise passes).
 #include "common.h"
 #include "kernels.h"
+#include "rowcfg.h"
 
 namespace {
 
@@ -202,31 +203,7 @@ __global__ __launch_bounds__(NW * 64) void embed_ln_kernel(
   }
 }
 
-// pick (waves, vectors-per-thread) so that a row is covered with all values in registers
-struct RowCfg {
-  int nw, maxv;
-};
-RowCfg row_cfg(int H) {
-  const int nvec = H / 8;
-  int nw = nvec >= 1024 ? 4 : (nvec >= 512 ? 4 : (nvec >= 256 ? 4 : (nvec >= 128 ? 2 : 1)));
-  int maxv = (nvec + nw * 64 - 1) / (nw * 64);
-  return {nw, maxv};
-}
-
 }  // namespace
-
-#define ROW_DISPATCH(H, KERNEL_CALL)                                           \
-  do {                                                                         \
-    RowCfg cfg_ = row_cfg(H);                                                  \
-    if (cfg_.nw == 1 && cfg_.maxv == 1) { KERNEL_CALL(1, 1); }                 \
-    else if (cfg_.nw == 1 && cfg_.maxv == 2) { KERNEL_CALL(2, 1); }            \
-    else if (cfg_.nw == 2 && cfg_.maxv == 1) { KERNEL_CALL(1, 2); }            \
-    else if (cfg_.nw == 4 && cfg_.maxv == 1) { KERNEL_CALL(1, 4); }            \
-    else if (cfg_.nw == 4 && cfg_.maxv == 2) { KERNEL_CALL(2, 4); }            \
-    else if (cfg_.nw == 4 && cfg_.maxv <= 4) { KERNEL_CALL(4, 4); }            \
-    else if (cfg_.nw == 4 && cfg_.maxv <= 8) { KERNEL_CALL(8, 4); }            \
-    else { return -1; }                                                        \
-  } while (0)
 
 int lk_rmsnorm(bf16_t* out, bf16_t* residual, const bf16_t* x, const bf16_t* w, long rows, int H,
                float eps, long xs, long os, long rs, hipStream_t st) {

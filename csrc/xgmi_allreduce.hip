@@ -13,6 +13,12 @@
 //      writes the bf16 result (in place is fine: a slice is read before it is written);
 //   4. barrier-out: the same handshake on a second flag set, so no rank overwrites its
 //      staging buffer (next call) while a peer may still be reading it.
+// The TP decode layer's fused form (xgmi_ar_rmsnorm_kernel): the row-parallel o / down
+// partial sums are all-reduced, added to the residual stream and RMS-normalised in the SAME
+// kernel -- each workgroup owns whole rows, so after the handshake it sums its rows over the
+// ranks, rounds them to bf16 (the plain all-reduce's output), adds the residual, writes the
+// new residual and the normed row: bit-identical to all-reduce -> rmsnorm(x, residual) with
+// one launch and one pass over the rows instead of three.
 // Flags are per-workgroup monotonic epochs kept in device memory (one counter per
 // workgroup, advanced by the kernel itself), so a captured hipGraph replays correctly
 // with no host-side state.  Every spin is bounded: a peer that never arrives sets the
@@ -21,11 +27,14 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "rowcfg.h"
 
 namespace {
 
 constexpr int kMaxRanks = 8;
-constexpr int kArBlocks = 32;    // workgroups per call (slices)
+constexpr int kArBlocks = 256;   // max workgroups per call (the plain all-reduce uses <= 32 slices; the fused
+                                 // all-reduce + RMSNorm one row per workgroup up to 256 rows)
+constexpr int kArSlices = 32;    // workgroups of the plain all-reduce
 constexpr int kArThreads = 512;
 // signal buffer (uncached): [2 phases][kArBlocks][kMaxRanks] flags + [kArBlocks] epoch counters
 constexpr int kSigWords = 2 * kArBlocks * kMaxRanks + kArBlocks;
@@ -113,7 +122,116 @@ __global__ __launch_bounds__(kArThreads) void xgmi_allreduce_kernel(ArPeers p, i
   handshake(p, rank, world, 1, epoch, err);
 }
 
+// Stage the block's rows, handshake, then per row: x = bf16(sum over ranks in rank order),
+// res = bf16(x + res) (written back), out = bf16(bf16(res * rsqrt(mean(res^2) + eps)) * w).
+// The thread -> column slicing and the reduction order are rmsnorm_kernel's (rowcfg.h).
+template <int MAXV, int NW>
+__global__ __launch_bounds__(NW * 64) void xgmi_ar_rmsnorm_kernel(ArPeers p, int rank, int world,
+                                                                   const bf16_t* __restrict__ in,
+                                                                   bf16_t* __restrict__ residual,
+                                                                   const bf16_t* __restrict__ w,
+                                                                   bf16_t* __restrict__ out, int T, int H, float eps,
+                                                                   int* err) {
+  __shared__ float red[NW];
+  __shared__ unsigned s_epoch;
+  const int nb = gridDim.x;
+  const int r0 = (int)((long)blockIdx.x * T / nb), r1 = (int)((long)(blockIdx.x + 1) * T / nb);
+  unsigned* ctr = p.sig[rank] + 2 * kArBlocks * kMaxRanks + blockIdx.x;
+  if (threadIdx.x == 0) {
+    s_epoch = *ctr + 1;
+    *ctr = s_epoch;
+  }
+  __syncthreads();
+  const unsigned epoch = s_epoch;
+  const int nvec = H >> 3;
+  // 1. stage this block's rows
+  bf16_t* mine = p.data[rank];
+  for (long v = (long)r0 * nvec + threadIdx.x; v < (long)r1 * nvec; v += NW * 64)
+    *reinterpret_cast<short8*>(mine + v * 8) = *reinterpret_cast<const short8*>(in + v * 8);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // 2. barrier-in: every peer staged the same rows
+  if (!handshake(p, rank, world, 0, epoch, err)) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // 3. reduce + residual + RMSNorm, row by row
+  for (int row = r0; row < r1; ++row) {
+    float v[MAXV][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = threadIdx.x + i * NW * 64;
+      if (c < nvec) {
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < world; ++r) {
+          float x[8];
+          load8(p.data[r] + (long)row * H + c * 8, x);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += x[j];
+        }
+        float rr[8];
+        bf16_t* rp = residual + (long)row * H + c * 8;
+        load8(rp, rr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = bf2f(f2bf(acc[j])) + rr[j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = bf2f(f2bf(v[i][j]));
+        store8(rp, v[i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+      }
+    }
+    ss = block_sum<NW>(ss, red);
+    const float inv = rsqrtf(ss / (float)H + eps);
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = threadIdx.x + i * NW * 64;
+      if (c < nvec) {
+        float g[8], y[8];
+        load8(w + c * 8, g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = bf2f(f2bf(v[i][j] * inv)) * g[j];
+        store8(out + (long)row * H + c * 8, y);
+      }
+    }
+  }
+  __syncthreads();
+  // 4. barrier-out: every peer finished reading this block's rows of our staging buffer
+  handshake(p, rank, world, 1, epoch, err);
+}
+
 }  // namespace
+
+// out = RMSNorm(allreduce(in) + residual) * w, residual updated in place; in / residual / out
+// [T, H] contiguous, T * H * 2 <= staging bytes (checked by the caller).  Same launch on every
+// rank (block count depends on T only), so the per-block epochs stay in step with the plain
+// all-reduce's.
+int lk_xgmi_allreduce_rmsnorm(bf16_t* const* data, unsigned* const* sig, int rank, int world, const bf16_t* in,
+                              bf16_t* residual, const bf16_t* w, bf16_t* out, int T, int H, float eps, int* err,
+                              hipStream_t st) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || H % 8 || T < 0) return -1;
+  if (T == 0) return 0;
+  ArPeers p{};
+  for (int r = 0; r < world; ++r) {
+    p.data[r] = data[r];
+    p.sig[r] = sig[r];
+  }
+  const int blocks = std::min(kArBlocks, T);
+#define CALL(MV, NW) \
+  xgmi_ar_rmsnorm_kernel<MV, NW><<<blocks, NW * 64, 0, st>>>(p, rank, world, in, residual, w, out, T, H, eps, err)
+  ROW_DISPATCH(H, CALL);
+#undef CALL
+  LK_CHECK_LAUNCH();
+  return 0;
+}
 
 int lk_xgmi_ar_sig_words() { return kSigWords; }
 int lk_xgmi_ar_max_ranks() { return kMaxRanks; }
@@ -130,7 +248,7 @@ int lk_xgmi_allreduce(bf16_t* const* data, unsigned* const* sig, int rank, int w
     p.sig[r] = sig[r];
   }
   const long nv = n / 8;
-  const int blocks = (int)std::min<long>(kArBlocks, std::max<long>(1, (nv + kArThreads - 1) / kArThreads));
+  const int blocks = (int)std::min<long>(kArSlices, std::max<long>(1, (nv + kArThreads - 1) / kArThreads));
   xgmi_allreduce_kernel<<<blocks, kArThreads, 0, st>>>(p, rank, world, in, out, n, err);
   LK_CHECK_LAUNCH();
   return 0;

@@ -125,13 +125,10 @@ class LlamaModel(nn.Module):
                 a = ops.linear_swiglu(x, L.gate_up)
                 x = ops.linear_add_rmsnorm(a, L.down, res, nxt, cfg.norm_eps)
                 continue
-            o = ops.linear(attn_out, L.o)
-            self.tp.all_reduce_(o)
-            x = ops.rmsnorm(o, L.post_norm, cfg.norm_eps, residual=res)
+            # row-parallel tails: all-reduce + residual add + RMSNorm (one kernel on the xGMI path)
+            x = self.tp.all_reduce_rmsnorm(ops.linear(attn_out, L.o), res, L.post_norm, cfg.norm_eps)
             a = ops.linear_swiglu(x, L.gate_up)
-            d = ops.linear(a, L.down)
-            self.tp.all_reduce_(d)
-            x = ops.rmsnorm(d, nxt, cfg.norm_eps, residual=res)
+            x = self.tp.all_reduce_rmsnorm(ops.linear(a, L.down), res, nxt, cfg.norm_eps)
         if meta.logits_idx is not None:
             x = x.index_select(0, meta.logits_idx)
         return x

@@ -45,6 +45,19 @@ class TPGroup:
             dist.all_reduce(t, group=self.group)
         return t
 
+    def all_reduce_rmsnorm(self, x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
+                           eps: float) -> torch.Tensor:
+        """RMSNorm(allreduce(x) + residual) * w, residual updated in place: the tail of every
+        row-parallel projection.  With the one-shot xGMI path attached this is ONE kernel
+        (csrc/xgmi_allreduce.hip xgmi_ar_rmsnorm_kernel); otherwise RCCL all-reduce + the
+        fused add+norm kernel."""
+        from .. import ops
+
+        if self.size > 1 and self.xgmi is not None and self.xgmi.eligible_rows(x, residual):
+            return self.xgmi.all_reduce_rmsnorm_(x, residual, w, eps)
+        self.all_reduce_(x)
+        return ops.rmsnorm(x, w, eps, residual=residual)
+
     def reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:
         """Sum over ranks of t [size*n, ...], this rank's rows [rank*n, (rank+1)*n)."""
         if self.size == 1:

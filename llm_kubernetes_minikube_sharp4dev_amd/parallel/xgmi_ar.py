@@ -38,6 +38,19 @@ class XgmiAllReduce:
         self.state.all_reduce(t, t)
         return t
 
+    def eligible_rows(self, x: torch.Tensor, residual: torch.Tensor) -> bool:
+        return (self.eligible(x) and x.dim() == 2 and residual.is_contiguous() and residual.shape == x.shape
+                and residual.dtype == torch.bfloat16 and x.shape[1] % 8 == 0)
+
+    def all_reduce_rmsnorm_(self, x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                            out: torch.Tensor | None = None) -> torch.Tensor:
+        """RMSNorm(allreduce(x) + residual) * w in ONE kernel (residual updated in place):
+        the TP decode layer's "row-parallel GEMM -> all-reduce -> add -> norm" tail."""
+        if out is None:
+            out = torch.empty_like(x)
+        self.state.all_reduce_rmsnorm(x, residual, w.contiguous(), float(eps), out)
+        return out
+
     def error(self) -> int:
         """Non-zero if a handshake ever timed out (a peer missing a call)."""
         return self.state.error()

@@ -166,10 +166,10 @@ def test_repeat_penalty_window_longer_than_256(hip, last_n):
     only_old[:, 450] = 5
     lg = torch.full((B, V), -10.0)
     lg[:, 5] = 9.0
-    lg[:, 750] = 4.0
+    lg[:, 950] = 4.0  # not in the ring (700-799): unpenalised
     got2 = ops.sample(lg.to(DEV), _prm(B, temp=0.0, pen=3.0, last_n=last_n, reset=0).to(DEV),
                       only_old.to(DEV), torch.full((B,), 1000, dtype=torch.int32, device=DEV))
-    assert (got2.cpu() == 750).all()  # token 5 sits 549 entries back in the window: penalised
+    assert (got2.cpu() == 950).all()  # token 5 sits 549 entries back in the window: penalised
 
 
 def test_sampler_ring_covers_max_model_len(hip):

@@ -110,3 +110,74 @@ def test_xgmi_allreduce_missing_peer_times_out_with_error():
         r1 = torch.load(os.path.join(d, "t1.pt"), weights_only=True)
     assert r0["first_ok"] and r1["first_ok"]
     assert r0["error"] == 1 and r0["seconds"] < 60, r0
+
+
+def _fused_worker(rank, world, port, out_dir):
+    """Fused all-reduce + residual + RMSNorm vs the unfused chain (same one-shot all-reduce,
+    then ops.rmsnorm with the residual): bit-identical outputs and residuals, eager and
+    replayed from a hipGraph, at decode row counts and both Llama widths."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from llm_kubernetes_minikube_sharp4dev_amd import ops
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp import TPGroup
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.xgmi_ar import XgmiAllReduce
+
+    tp = TPGroup(rank, world, dist.group.WORLD, ctrl=dist.group.WORLD, ranks=list(range(world)))
+    ar = XgmiAllReduce(tp, 8 << 20)
+    tp.xgmi = ar
+    ok = []
+    for T, H in ((1, 8192), (7, 4096), (64, 8192), (256, 8192), (100, 4096)):
+        g = torch.Generator().manual_seed(T * 31 + H)
+        xs = [torch.randn(T, H, generator=g).to(torch.bfloat16) for _ in range(world)]
+        res0 = torch.randn(T, H, generator=g).to(torch.bfloat16)
+        w = (torch.rand(H, generator=g) + 0.5).to(torch.bfloat16).cuda()
+        x = xs[rank].cuda()
+        # unfused: one-shot all-reduce, then the add + norm kernel
+        xu, ru = x.clone(), res0.cuda()
+        ar.all_reduce_(xu)
+        yu = ops.rmsnorm(xu, w, 1e-5, residual=ru)
+        # fused
+        rf = res0.cuda()
+        yf = tp.all_reduce_rmsnorm(x.clone(), rf, w, 1e-5)
+        torch.cuda.synchronize()
+        ok.append((T, H, bool(torch.equal(yf.cpu(), yu.cpu())), bool(torch.equal(rf.cpu(), ru.cpu()))))
+    # graph capture + replay of the fused call
+    T, H = 64, 8192
+    xin = torch.zeros(T, H, dtype=torch.bfloat16, device="cuda")
+    res = torch.zeros(T, H, dtype=torch.bfloat16, device="cuda")
+    w = torch.ones(H, dtype=torch.bfloat16, device="cuda")
+    out = torch.empty(T, H, dtype=torch.bfloat16, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ar.all_reduce_rmsnorm_(xin, res, w, 1e-5, out)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        ar.all_reduce_rmsnorm_(xin, res, w, 1e-5, out)
+    for it in range(3):
+        g = torch.Generator().manual_seed(1000 + it)
+        xs = [torch.randn(T, H, generator=g).to(torch.bfloat16) for _ in range(world)]
+        r0 = torch.randn(T, H, generator=g).to(torch.bfloat16)
+        xin.copy_(xs[rank].cuda())
+        res.copy_(r0.cuda())
+        gr.replay()
+        torch.cuda.synchronize()
+        tot = sum(v.float() for v in xs).to(torch.bfloat16)
+        ru = r0.cuda()
+        yu = ops.rmsnorm(tot.cuda(), w, 1e-5, residual=ru)
+        ok.append(("graph", it, bool(torch.equal(out.cpu(), yu.cpu())), bool(torch.equal(res.cpu(), ru.cpu()))))
+    ok.append(("err", 0, ar.error() == 0, ar.error() == 0))
+    torch.save(ok, os.path.join(out_dir, f"f{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_xgmi_allreduce_rmsnorm_fused_bit_identical():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_fused_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        for r in range(2):
+            ok = torch.load(os.path.join(d, f"f{r}.pt"), weights_only=True)
+            assert all(o[-1] and o[-2] for o in ok), f"rank {r}: {ok}"
