@@ -109,6 +109,10 @@ def parse():
     ap.add_argument("--via-http", action="store_true",
                     help="the .NET-facing path: Ollama-compatible server + Minimal_RAG app as separate processes, "
                          "/agent_rag driven over HTTP at concurrency 1, 8, 128 (benchmarks/http_bench.py)")
+    ap.add_argument("--frontends", type=int, default=0,
+                    help="with --via-http: split server, this many HTTP front-end processes before the GPU engine core")
+    ap.add_argument("--http-levels", default=None, help="with --via-http: concurrency levels (default 1,8,128)")
+    ap.add_argument("--http-requests", default=None, help="with --via-http: requests per level")
     ap.add_argument("--tokenizer", default=None,
                     help="tokenizer.json to use instead of the built-in one (e.g. benchmarks/data/"
                          "bpe_runbooks_r1.json, the round-1 tokenizer trained on the synthetic corpus itself, "
@@ -131,7 +135,9 @@ def main():
 
         cmd = [sys.executable, os.path.join(ROOT, "benchmarks", "http_bench.py"), "--docs", str(args.docs),
                "--max-new-tokens", str(args.max_new_tokens), "--model", args.model, "--embedder", args.embedder,
-               "--kv-gb", str(args.kv_gb)] + (["--json-out", args.json_out] if args.json_out else [])
+               "--kv-gb", str(args.kv_gb)] + (["--json-out", args.json_out] if args.json_out else []) + \
+            (["--frontends", str(args.frontends)] if args.frontends else []) + \
+            (["--concurrency", args.http_levels, "--requests", args.http_requests] if args.http_levels else [])
         raise SystemExit(subprocess.call(cmd))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

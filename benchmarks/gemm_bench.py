@@ -29,7 +29,7 @@ EPI = {"none": 0, "swiglu": 1, "bias": 2, "gelu": 3, "relu": 4}
 # the LM head is not here (M <= 256: weight-streaming regime), bge-base encoder layers
 LLAMA = [(6144, 4096, "none"), (4096, 4096, "none"), (28672, 4096, "swiglu"), (4096, 14336, "none")]
 # K-loop schedules of csrc/gemm.hip (0 / 1 / 2) and "4w" = the one-wave-per-SIMD kernel csrc/gemm4w.hip
-VARIANTS = [v if v == "4w" else int(v) for v in os.environ.get("LK_GEMM_VARIANTS", "0,1").split(",")]
+VARIANTS = [v if v.startswith("4w") else int(v) for v in os.environ.get("LK_GEMM_VARIANTS", "0,1").split(",")]
 SPLITS = [int(v) for v in os.environ.get("LK_GEMM_SPLITS", "1").split(",")]
 BGE = [(2304, 768, "bias"), (768, 768, "bias"), (3072, 768, "gelu"), (768, 3072, "bias")]
 
@@ -117,13 +117,13 @@ def main():
         best = None
         t_lib = []
         cfgs = [(v, bn, sp) for v in VARIANTS for bn in bns for sp in SPLITS
-                if (L.gemm4w_supported(M, N, K, EPI[epi], sp) and bn == 256 if v == "4w"
+                if (L.gemm4w_supported(M, N, K, EPI[epi], sp) and bn == 256 if str(v).startswith("4w")
                     else L.gemm_supported(M, N, K, EPI[epi], bn, sp))]
         t_ours = {c: [] for c in cfgs}
 
         def mk(c):
-            if c[0] == "4w":
-                return lambda: L.gemm4w(x, wnext(), b, EPI[epi], None, c[2])
+            if str(c[0]).startswith("4w"):  # "4w" = LDS-DMA ring, "4w1" = register staging
+                return lambda: L.gemm4w(x, wnext(), b, EPI[epi], None, c[2], int(c[0][2:] or 0))
             return lambda: L.gemm(x, wnext(), b, EPI[epi], c[1], None, c[0], c[2])
         fns = {c: mk(c) for c in cfgs}
         for bn in cfgs:

@@ -96,6 +96,8 @@ def main():
     ap.add_argument("--embedder", default="bge-base")
     ap.add_argument("--kv-gb", type=float, default=48.0)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--frontends", type=int, default=0,
+                    help="split server: HTTP front-end processes in front of the GPU engine core (serve --frontends)")
     a = ap.parse_args()
     levels = [int(x) for x in a.concurrency.split(",")]
     counts = [int(x) for x in a.requests.split(",")]
@@ -108,7 +110,8 @@ def main():
     logs = [open(os.path.join(ROOT, "gpurun_out", f"http_{n}.log"), "w") for n in ("server", "rag_app")]
     srv = subprocess.Popen([sys.executable, "-m", mod, "serve", "--port", str(p1),
                             "--alias", f"llama3.1:8b={a.model}", "--alias", f"nomic-embed-text={a.embedder}",
-                            "--preload", "llama3.1:8b", "--preload", "nomic-embed-text"],
+                            "--preload", "llama3.1:8b", "--preload", "nomic-embed-text"]
+                           + (["--frontends", str(a.frontends)] if a.frontends else []),
                            cwd=ROOT, env=env, stdout=logs[0], stderr=subprocess.STDOUT, start_new_session=True)
     app = None
     try:
@@ -156,6 +159,8 @@ def main():
                "dtype": "bf16", "data": f"synthetic ({a.docs} runbook docs; random-init weights)",
                "p50_latency_ms": top["p50_latency_ms"],
                "config": {"model": f"{a.model} (bf16) as llama3.1:8b + {a.embedder} as nomic-embed-text",
+                          "server": (f"split: GPU engine core + {a.frontends} HTTP front-end processes"
+                                     if a.frontends else "one process (HTTP + engine)"),
                           "sampling": "Ollama server defaults (no options sent): temperature 0.8, top-k 40, "
                                       "top-p 0.9, repeat penalty 1.1 / 64",
                           "num_predict": a.max_new_tokens, "levels": res}}

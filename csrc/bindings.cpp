@@ -263,7 +263,7 @@ at::Tensor gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at
 
 // One-wave-per-SIMD 256 x 256 variant (csrc/gemm4w.hip), same contract as gemm() with bn = 256.
 at::Tensor gemm4w(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t epi,
-                  const c10::optional<at::Tensor>& out_, int64_t splits) {
+                  const c10::optional<at::Tensor>& out_, int64_t splits, int64_t variant) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_LASTDIM(x); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "x [M,K], w [N,K]");
   check_rows16(x, "x"); check_rows16(w, "w");
@@ -283,7 +283,8 @@ at::Tensor gemm4w(const at::Tensor& x, const at::Tensor& w, const c10::optional<
   at::Tensor ws;
   if (splits > 1) ws = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
   int rc = lk_gemm4w(bp(x), x.stride(0), bp(w), epi >= 2 ? bp(*bias) : nullptr, M, N, K, (int)epi, bp(out),
-                     out.stride(0), cur_stream(), (int)splits, splits > 1 ? ws.data_ptr<float>() : nullptr);
+                     out.stride(0), cur_stream(), (int)splits, splits > 1 ? ws.data_ptr<float>() : nullptr,
+                     (int)variant);
   CHECK_RC(rc, "gemm4w");
   return out;
 }
@@ -709,7 +710,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("splits") = 0, py::arg("out") = py::none());
   m.def("ws_plan", &ws_plan);
   m.def("gemm4w", &gemm4w, "", py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("epi") = 0,
-        py::arg("out") = py::none(), py::arg("splits") = 1);
+        py::arg("out") = py::none(), py::arg("splits") = 1, py::arg("variant") = 0);
   m.def("gemm4w_supported", &gemm4w_supported, "", py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"),
         py::arg("splits") = 1);
   m.def("gemm", &gemm, "", py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("epi") = 0,

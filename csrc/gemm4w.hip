@@ -71,7 +71,10 @@ LK_DEVICE void mfma(floatx4& acc, const short8& a, const short8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
-template <int EPI>
+// MODE 0: LDS-DMA ring (4 slots of 32-deep slices, DMA issued 4 slices ahead);
+// MODE 1: register staging (buffer_load_dwordx4 to VGPRs 4 slices ahead, two staging sets,
+//         ds_write_b128 into a 2-slot ring two slices ahead): no LDS-DMA issue on the MFMA waves
+template <int EPI, int MODE>
 __device__ __forceinline__ void gemm4w_body(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W,
                                             const bf16_t* __restrict__ bias, int M, int K, int I,
                                             bf16_t* __restrict__ out, long ldo, int TM, int TN, int group_m,
@@ -157,11 +160,11 @@ __device__ __forceinline__ void gemm4w_body(const bf16_t* __restrict__ X, long l
     const unsigned so = (unsigned)(s0 + s + 4) * (kBKS * 2);
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
-      if constexpr (RD) {
+      if constexpr (RD && MODE != 2 && MODE != 4) {
         nx[m] = *reinterpret_cast<const short8*>(nb + (wr * 128 + m * 16) * kRow);
         nw[m] = *reinterpret_cast<const short8*>(nb + kRegion + (wc * 128 + m * 16) * kRow);
       }
-      if constexpr (DMA) {
+      if constexpr (DMA && MODE != 3 && MODE != 4) {
         if (m < 4)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(db + m * 16 * kRow), 16, xoff[m & 3], so, 0, 0);
         else
@@ -185,6 +188,7 @@ __device__ __forceinline__ void gemm4w_body(const bf16_t* __restrict__ X, long l
   using V1 = std::integral_constant<int, kDmaPerWave>;
   using V2 = std::integral_constant<int, 2 * kDmaPerWave>;
 
+  if constexpr (MODE != 1) {  // MODE 0 (+ the timing-only ablations 2-4 of its loop)
   // prologue: slices 0..3 in flight, slice 0 landed and read
 #pragma unroll
   for (int s = 0; s < kSlots; ++s) issue(s);
@@ -215,6 +219,89 @@ __device__ __forceinline__ void gemm4w_body(const bf16_t* __restrict__ X, long l
   step(T{}, F{}, fx0, fw0, fx1, fw1, s + 2);
   sync(V0{});
   step(F{}, F{}, fx1, fw1, fx0, fw0, s + 3);
+  } else {
+  // ---- register staging.  Slice t is loaded (8 x 16 B per lane: 4 X, 4 W row groups) into
+  // staging set t & 1 at step t - 4, written to LDS slot t & 1 at step t - 2 (that slot's
+  // previous slice, t - 2, was read during step t - 3, before barrier t - 2), published by
+  // barrier t - 1 and read during step t - 1.  hipcc counts these plain loads itself (vmcnt
+  // before each ds_write), so no wait here is hand-placed.
+  uint4_t st0[8], st1[8];
+  const unsigned wofs = (unsigned)((16 * 4 * w + lrow) * kRow + ((lc ^ fsw(lrow)) << 4));
+  unsigned xo[4], wo[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // source offsets without the chunk swizzle (applied on the write)
+    const int row = 16 * (4 * w + i) + lrow;
+    xo[i] = (unsigned)(((long)tm * kBM + row) * ldx * 2) + (unsigned)(lc << 4);
+    wo[i] = (unsigned)(wrow(row) * K * 2) + (unsigned)(lc << 4);
+  }
+  auto gload = [&](uint4_t(&st)[8], int t, int i) {
+    const int so = (s0 + t) * (kBKS * 2);
+    if (i < 4) st[i] = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo[i & 3], so, 0));
+    else st[i] = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(wrs, wo[i & 3], so, 0));
+  };
+  auto lwrite = [&](const uint4_t(&st)[8], int t, int i) {
+    unsigned char* b = smem + (t & 1) * kSlice + wofs + (i < 4 ? 0 : kRegion) + (i & 3) * 16 * kRow;
+    *reinterpret_cast<uint4_t*>(b) = st[i];
+  };
+  // slice s: 64 MFMAs of (fx, fw) with the 16 fragment reads of s + 1 (RD), the 8 LDS writes of
+  // s + 2 (WR, staging set (s + 2) & 1 = s & 1) and the 8 loads of s + 4 into that set (LD)
+  auto rstep = [&](auto rd_t, auto wr_t, auto ld_t, short8(&fx)[8], short8(&fw)[8], short8(&nx)[8],
+                   short8(&nw)[8], uint4_t(&st)[8], int s) {
+    constexpr bool RD = decltype(rd_t)::value, WR = decltype(wr_t)::value, LD = decltype(ld_t)::value;
+    const unsigned char* nb = smem + ((s + 1) & 1) * kSlice + fofs;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      if constexpr (RD) {
+        nx[m] = *reinterpret_cast<const short8*>(nb + (wr * 128 + m * 16) * kRow);
+        nw[m] = *reinterpret_cast<const short8*>(nb + kRegion + (wc * 128 + m * 16) * kRow);
+      }
+      if constexpr (WR) lwrite(st, s + 2, m);
+      if constexpr (LD) gload(st, s + 4, m);
+#pragma unroll
+      for (int n = 0; n < 8; ++n) mfma(acc[m][n], fw[n], fx[m]);
+    }
+  };
+  auto rsync = [&]() {
+    wait_lgkm0();
+    barrier_raw();
+  };
+#pragma unroll
+  for (int i = 0; i < 8; ++i) gload(st0, 0, i);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) gload(st1, 1, i);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) lwrite(st0, 0, i);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) lwrite(st1, 1, i);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) gload(st0, 2, i);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) gload(st1, 3, i);
+  rsync();
+  {
+    const unsigned char* b0 = smem + fofs;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      fx0[m] = *reinterpret_cast<const short8*>(b0 + (wr * 128 + m * 16) * kRow);
+      fw0[m] = *reinterpret_cast<const short8*>(b0 + kRegion + (wc * 128 + m * 16) * kRow);
+    }
+  }
+  int s = 0;
+  for (; s + 6 <= ns; s += 2) {
+    rsync();
+    rstep(T{}, T{}, T{}, fx0, fw0, fx1, fw1, st0, s);
+    rsync();
+    rstep(T{}, T{}, T{}, fx1, fw1, fx0, fw0, st1, s + 1);
+  }
+  rsync();
+  rstep(T{}, T{}, F{}, fx0, fw0, fx1, fw1, st0, s);
+  rsync();
+  rstep(T{}, T{}, F{}, fx1, fw1, fx0, fw0, st1, s + 1);
+  rsync();
+  rstep(T{}, F{}, F{}, fx0, fw0, fx1, fw1, st0, s + 2);
+  rsync();
+  rstep(F{}, F{}, F{}, fx1, fw1, fx0, fw0, st1, s + 3);
+  }
   // MFMA results -> VALU reads of the accumulators: the asm MFMAs are invisible to hipcc's
   // hazard recognizer, so wait out the longest MFMA -> read latency here
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
@@ -298,13 +385,13 @@ __device__ __forceinline__ void gemm4w_body(const bf16_t* __restrict__ X, long l
   }
 }
 
-template <int EPI>
+template <int EPI, int MODE>
 __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const bf16_t* __restrict__ X, long ldx,
                                                         const bf16_t* __restrict__ W,
                                                         const bf16_t* __restrict__ bias, int M, int K, int I,
                                                         bf16_t* __restrict__ out, long ldo, int TM, int TN,
                                                         int group_m) {
-  gemm4w_body<EPI>(X, ldx, W, bias, M, K, I, out, ldo, TM, TN, group_m, blockIdx.x);
+  gemm4w_body<EPI, MODE>(X, ldx, W, bias, M, K, I, out, ldo, TM, TN, group_m, blockIdx.x);
 }
 
 int group_rows4() {
@@ -316,16 +403,28 @@ int group_rows4() {
   return g;
 }
 
+template <int EPI, int MODE>
+void launch4m(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
+              long ldo, int TM, int TN, int ks, hipStream_t st) {
+  constexpr int lds = MODE != 1 ? kLds : 2 * kSlice;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4w_kernel<EPI, MODE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  gemm4w_kernel<EPI, MODE><<<dim3(TM * TN, ks), 256, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN,
+                                                               group_rows4());
+}
+int g_mode4 = 0;  // kernel variant of this call (lk_gemm4w's `variant`)
 template <int EPI>
 void launch4(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
              long ldo, int TM, int TN, int ks, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4w_kernel<EPI>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
-    attr = true;
-  }
-  gemm4w_kernel<EPI><<<dim3(TM * TN, ks), 256, kLds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, group_rows4());
+  if (g_mode4 == 1) launch4m<EPI, 1>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
+  else if (g_mode4 == 2) launch4m<EPI, 2>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
+  else if (g_mode4 == 3) launch4m<EPI, 3>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
+  else if (g_mode4 == 4) launch4m<EPI, 4>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
+  else launch4m<EPI, 0>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
 }
 
 // split-K reduction (same rounding as the fused epilogues)
@@ -365,7 +464,11 @@ int lk_gemm4w_supported(int M, int N, int K, int epi, int ks) {
 
 // Same contract as lk_gemm with a fixed 256 x 256 tile (bn = 256).
 int lk_gemm4w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi,
-              bf16_t* out, long ldo, hipStream_t st, int ks, float* ws) {
+              bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, int variant) {
+  // variants 2-4: timing-only ablations of variant 0's loop (2: no fragment reads, 3: no
+  // LDS-DMA, 4: neither) -- WRONG results by construction, for the PMC / microbench only
+  if (variant < 0 || variant > 4) return -1;
+  g_mode4 = variant;
   if (!lk_gemm4w_supported(M, N, K, epi, ks) || ldx % 8 || ldo % 8 || reinterpret_cast<uintptr_t>(out) % 16 ||
       (bias != nullptr && reinterpret_cast<uintptr_t>(bias) % 16))
     return -1;
@@ -375,7 +478,7 @@ int lk_gemm4w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, in
     if (max_rows < kBM) return -1;
     for (long m0 = 0; m0 < M; m0 += max_rows) {
       const int mc = (int)min((long)M - m0, max_rows);
-      const int rc = lk_gemm4w(x + m0 * ldx, ldx, w, bias, mc, N, K, epi, out + m0 * ldo, ldo, st, 1, nullptr);
+      const int rc = lk_gemm4w(x + m0 * ldx, ldx, w, bias, mc, N, K, epi, out + m0 * ldo, ldo, st, 1, nullptr, variant);
       if (rc) return rc;
     }
     return 0;

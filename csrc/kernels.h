@@ -59,7 +59,7 @@ int lk_xgmi_allreduce(bf16_t* const* data, unsigned* const* sig, int rank, int w
 int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks = 1);
 int lk_gemm4w_supported(int M, int N, int K, int epi, int ks);
 int lk_gemm4w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi,
-              bf16_t* out, long ldo, hipStream_t st, int ks, float* ws);
+              bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, int variant = 0);
 int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
             int variant, bf16_t* out, long ldo, hipStream_t st, int ks = 1, float* ws = nullptr);
 

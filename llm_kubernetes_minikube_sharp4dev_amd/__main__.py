@@ -1,7 +1,11 @@
 """Command line.
 
   serve           Ollama-compatible server on :11434 (one GPU; ``--gpus N`` starts N
-                  replica processes + the DP router in front of them)
+                  replica processes + the DP router in front of them; ``--frontends F``
+                  splits it: engine-core process(es) on the GPU(s) + F HTTP front-end
+                  processes sharing the port, routing over every core)
+  serve-core      one engine core (GPU process of the split server)
+  serve-frontend  one HTTP front-end of the split server
   rag-app         Minimal_RAG port (:5103): /health, /rag/search, /agent_rag
   agent-app       Minimal_Agent port (:5217): /health, /agent
   all             server + both apps in one process sharing the engines (in-process
@@ -58,6 +62,8 @@ def _uvicorn(app, host, port, name="http"):
 
 
 def cmd_serve(args):
+    if args.frontends > 0:
+        return _serve_split(args)
     if args.gpus > 1:
         return _serve_replicas(args)
     from .serving.model_manager import ModelManager
@@ -69,6 +75,107 @@ def cmd_serve(args):
         kind, _ = mgr.resolve(m)
         (mgr.generator if kind == "generate" else mgr.embedder)(m)
     _uvicorn(create_app(mgr), args.host, args.port, "server")
+
+
+def _model_args(args) -> list:
+    return sum([["--alias", a] for a in args.alias or []], []) + \
+        sum([["--checkpoint", c] for c in args.checkpoint or []], []) + \
+        sum([["--preload", p] for p in args.preload or []], []) + (["--config", args.config] if args.config else [])
+
+
+def _supervise(procs):
+    """Block until a child exits (then stop the rest) or a signal arrives."""
+    import signal
+
+    stop = []
+    signal.signal(signal.SIGTERM, lambda *a: stop.append(1))
+    try:
+        while not stop and all(p.poll() is None for p in procs):
+            time.sleep(0.5)
+    except KeyboardInterrupt:
+        pass
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+    return 0
+
+
+def _serve_split(args):
+    """Engine core(s) + HTTP front-ends.  One GPU: this process is the core and starts the
+    front-ends; ``--gpus N``: N core processes (one per GPU) and the front-ends, supervised by
+    this process, which never touches the GPU."""
+    from .serving.remote import core_socket_path
+
+    mod = "llm_kubernetes_minikube_sharp4dev_amd"
+    paths = [core_socket_path(args.port, g) for g in range(args.gpus)]
+    fe_env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", CUDA_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
+    fe_cmd = [sys.executable, "-m", mod, "serve-frontend", "--host", args.host, "--port", str(args.port),
+              "--cores", ",".join(paths)] + _model_args(args)
+    if args.gpus == 1:
+        from .serving.engine_core import EngineCore
+
+        mgr = _manager(args)
+        core = EngineCore(mgr, paths[0])
+        fes = [subprocess.Popen(fe_cmd, env=fe_env) for _ in range(args.frontends)]
+        try:
+            return _supervise(fes)
+        finally:
+            core.close()
+            mgr.shutdown()
+    procs = []
+    for g in range(args.gpus):
+        env = dict(os.environ, HIP_VISIBLE_DEVICES=str(g), CUDA_VISIBLE_DEVICES=str(g))
+        procs.append(subprocess.Popen([sys.executable, "-m", mod, "serve-core", "--socket", paths[g]] +
+                                      _model_args(args), env=env))
+    procs += [subprocess.Popen(fe_cmd, env=fe_env) for _ in range(args.frontends)]
+    return _supervise(procs)
+
+
+def _manager(args):
+    from .serving.model_manager import ModelManager
+
+    mgr = ModelManager(_cfg(args), device=getattr(args, "device", None), aliases=_kv(args.alias),
+                       checkpoints=_kv(args.checkpoint))
+    for m in args.preload or []:
+        kind, _ = mgr.resolve(m)
+        (mgr.generator if kind == "generate" else mgr.embedder)(m)
+    return mgr
+
+
+def cmd_serve_core(args):
+    from .serving.engine_core import EngineCore
+
+    mgr = _manager(args)
+    core = EngineCore(mgr, args.socket)
+    try:
+        import signal
+
+        signal.sigwait({signal.SIGTERM, signal.SIGINT})
+    finally:
+        core.close()
+        mgr.shutdown()
+
+
+def cmd_serve_frontend(args):
+    import uvicorn
+
+    from .serving.remote import create_frontend_app, reuseport_socket
+
+    app = create_frontend_app(args.cores.split(","), _cfg(args), _kv(args.alias), _kv(args.checkpoint),
+                              preload=args.preload)
+    from .utils.pyprof import thread_profile
+
+    sock = reuseport_socket(args.host, args.port)
+    cfg = uvicorn.Config(app, log_level="warning", timeout_keep_alive=120, backlog=4096, timeout_graceful_shutdown=5)
+    with thread_profile(f"frontend_{os.getpid()}") as dump:  # LK_PYPROFILE=<dir>
+        app.router.on_shutdown.append(dump)
+        uvicorn.Server(cfg).run(sockets=[sock])
 
 
 def _serve_replicas(args):
@@ -250,7 +357,22 @@ def main(argv=None):
     p.add_argument("--alias", action="append", help="client-name=preset (e.g. llama3.1:8b=opt-125m)")
     p.add_argument("--checkpoint", action="append", help="name-or-preset=safetensors dir")
     p.add_argument("--preload", action="append")
+    p.add_argument("--frontends", type=int, default=0,
+                   help="split server: HTTP front-end processes (SO_REUSEPORT) in front of the engine core(s)")
     p.set_defaults(fn=cmd_serve)
+    p = common(sub.add_parser("serve-core"), 0)
+    p.add_argument("--socket", required=True)
+    p.add_argument("--device", default=None)
+    p.add_argument("--alias", action="append")
+    p.add_argument("--checkpoint", action="append")
+    p.add_argument("--preload", action="append")
+    p.set_defaults(fn=cmd_serve_core)
+    p = common(sub.add_parser("serve-frontend"), 11434)
+    p.add_argument("--cores", required=True, help="comma-separated engine-core socket paths")
+    p.add_argument("--alias", action="append")
+    p.add_argument("--checkpoint", action="append")
+    p.add_argument("--preload", action="append")
+    p.set_defaults(fn=cmd_serve_frontend)
     for name, port, fn in (("rag-app", 5103, cmd_rag_app), ("agent-app", 5217, cmd_agent_app)):
         p = common(sub.add_parser(name), port)
         p.add_argument("--ollama-url", default=None)

@@ -193,6 +193,33 @@ class Tokenizer:
         ids = [i for i in ids if 0 <= i < self.vocab_size]
         return self.tok.decode(ids, skip_special_tokens=skip_special)
 
+    def token_bytes_table(self) -> Optional[list]:
+        """Raw bytes of every token id for byte-level BPE tokenizers (None otherwise): lets
+        :class:`IncrementalDetokenizer` stream text in O(1) per token instead of re-decoding
+        the whole output.  Special tokens map to b"" (decode skips them)."""
+        if getattr(self, "_bytes_table", False) is not False:
+            return self._bytes_table
+        table = None
+        try:
+            import json as _json
+
+            dec = _json.loads(self.tok.to_str()).get("decoder") or {}
+            if dec.get("type") == "ByteLevel":
+                b2u = _bytes_to_unicode()
+                u2b = {u: b for b, u in b2u.items()}
+                special = {t.content for t in self.tok.get_added_tokens_decoder().values() if t.special}
+                table = []
+                for i in range(self.vocab_size):
+                    t = self.tok.id_to_token(i)
+                    if t is None or t in special:
+                        table.append(b"")
+                    else:
+                        table.append(bytes(u2b[c] for c in t) if all(c in u2b for c in t) else t.encode("utf-8"))
+        except Exception:  # pragma: no cover - any tokenizer shape we do not understand
+            table = None
+        self._bytes_table = table
+        return table
+
     def piece(self, i: int) -> str:
         """Decoded text of a single token (for constrained decoding)."""
         if self._piece_cache is None:
@@ -229,16 +256,37 @@ class Tokenizer:
         return [head + b + tail for b in bodies]
 
 
+def _bytes_to_unicode() -> dict:
+    """GPT-2 / Llama-3 byte-level BPE alphabet: byte -> printable unicode character."""
+    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("¡"), ord("¬") + 1)) + list(range(ord("®"), ord("ÿ") + 1))
+    cs = bs[:]
+    n = 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    return dict(zip(bs, (chr(c) for c in cs)))
+
+
 class IncrementalDetokenizer:
     """Streams text for growing id lists without re-decoding emitted text and without
-    splitting multi-byte UTF-8 characters across chunks."""
+    splitting multi-byte UTF-8 characters across chunks.  Byte-level tokenizers take the
+    O(1)-per-token path (token bytes -> incremental UTF-8 decoder); others re-decode."""
 
     def __init__(self, tok: Tokenizer):
+        import codecs
+
         self.tok = tok
         self.ids: list[int] = []
         self.sent = ""
+        tb = tok.token_bytes_table() if hasattr(tok, "token_bytes_table") else None
+        self.table = tb
+        self.udec = codecs.getincrementaldecoder("utf-8")("replace") if tb is not None else None
 
     def push(self, tid: int) -> str:
+        if self.table is not None:
+            return self.udec.decode(self.table[tid]) if 0 <= tid < len(self.table) else ""
         self.ids.append(tid)
         text = self.tok.decode(self.ids)
         if text.endswith("�"):

@@ -105,6 +105,7 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
         if fmt:
             from ..engine.constrained import json_logits_processor
 
+            sp.format = fmt  # a remote engine core rebuilds the processor from the spec
             sp.logits_processor = json_logits_processor(h.tokenizer, fmt if isinstance(fmt, dict) else None)
         return sp
 

@@ -455,7 +455,8 @@ def test_gemm4w(hip, M, NK):
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
     assert hip.gemm4w_supported(M, N, K, 0)
-    _close(hip.gemm4w(x, w), x.float() @ w.float().t(), 0.02, 0.01, f"gemm4w M{M} N{N} K{K}")
+    for v in (0, 1):
+        _close(hip.gemm4w(x, w, variant=v), x.float() @ w.float().t(), 0.02, 0.01, f"gemm4w v{v} M{M} N{N} K{K}")
 
 
 def test_gemm4w_asymmetric_layout(hip):
@@ -463,10 +464,10 @@ def test_gemm4w_asymmetric_layout(hip):
     M, N, K = 512, 512, 256
     x = torch.eye(M, K, device=DEV, dtype=torch.bfloat16)
     w = (torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K) % 97 - 48).to(torch.bfloat16)
-    y = hip.gemm4w(x, w)
     exp = torch.zeros(M, N)
     exp[:K] = w.float().t().cpu()
-    assert torch.equal(y.float().cpu(), exp)
+    for v in (0, 1):
+        assert torch.equal(hip.gemm4w(x, w, variant=v).float().cpu(), exp), v
 
 
 @pytest.mark.parametrize("M", [300, 2048])
@@ -477,7 +478,8 @@ def test_gemm4w_swiglu(hip, M, IK):
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(2 * I, K, device=DEV, dtype=torch.bfloat16) * 0.05
     a_ref = ref.silu_mul((x.float() @ w.float().t()).to(torch.bfloat16))
-    _close(hip.gemm4w(x, w, None, 1), a_ref, 0.03, 0.01, f"gemm4w swiglu M{M} I{I}")
+    for v in (0, 1):
+        _close(hip.gemm4w(x, w, None, 1, variant=v), a_ref, 0.03, 0.01, f"gemm4w v{v} swiglu M{M} I{I}")
 
 
 @pytest.mark.parametrize("M", [7, 300, 4000])
@@ -494,7 +496,8 @@ def test_gemm4w_bias_epilogues(hip, M, NK, epi):
         y = torch.nn.functional.gelu(y)
     elif epi == 4:
         y = torch.relu(y)
-    _close(hip.gemm4w(x, w, b, epi), y, 0.03, 0.01, f"gemm4w epi{epi} M{M} N{N}")
+    for v in (0, 1):
+        _close(hip.gemm4w(x, w, b, epi, variant=v), y, 0.03, 0.01, f"gemm4w v{v} epi{epi} M{M} N{N}")
 
 
 @pytest.mark.parametrize("MNK", [(2048, 4096, 4096), (1000, 768, 3072), (4096, 1280, 8192)])
@@ -510,7 +513,9 @@ def test_gemm4w_splitk(hip, MNK, splits, epi):
     if epi:
         y = (y + b.float()).to(torch.bfloat16).float()
     if hip.gemm4w_supported(M, N, K, epi, splits):
-        _close(hip.gemm4w(x, w, b, epi, None, splits), y, 0.03, 0.01, f"gemm4w split{splits} epi{epi} M{M} N{N} K{K}")
+        for v in (0, 1):
+            _close(hip.gemm4w(x, w, b, epi, None, splits, v), y, 0.03, 0.01,
+                   f"gemm4w v{v} split{splits} epi{epi} M{M} N{N} K{K}")
 
 
 def test_gemm_splitk_dispatch(hip):
