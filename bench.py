@@ -62,6 +62,9 @@ def parse():
                          "completions; batch: a step = one synchronous batch of `batch` requests")
     ap.add_argument("--workload", choices=sorted(METRICS), default="rag")
     ap.add_argument("--docs", type=int, default=100_000, help="synthetic runbook documents in the knowledge base")
+    ap.add_argument("--long-evidence", action="store_true",
+                    help="corpus of ~1150-char sections (one chunk each): /agent_rag prompts of 6 evidence chunks "
+                         "near the 1500-char evidence cap, ~3k tokens (SURVEY 3.3)")
     ap.add_argument("--max-new-tokens", type=int, default=48)
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--embedder", default="bge-base")
@@ -156,7 +159,8 @@ def main():
     from llm_kubernetes_minikube_sharp4dev_amd.rag.corpus import build_chunks
 
     ncpu = os.cpu_count() or 8
-    chunks = build_chunks(args.docs, args.seed, workers=max(1, min(16, ncpu // max(1, world))))
+    chunks = build_chunks(args.docs, args.seed, workers=max(1, min(16, ncpu // max(1, world))),
+                          section_chars=1150 if args.long_evidence else 0)
     log(rank, f"corpus: {args.docs} docs -> {len(chunks)} chunks ({time.perf_counter() - t_setup:.1f}s)")
 
     import torch
@@ -456,7 +460,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16" if on_gpu else "fp32",
-            "data": f"synthetic ({args.docs} runbook docs -> {n} chunks; random-init weights)",
+            "data": f"synthetic ({args.docs} runbook docs{', ~1150-char sections (long evidence)' if args.long_evidence else ''} "
+                    f"-> {n} chunks; random-init weights)",
             "p50_latency_ms": round(p50, 1) if p50 is not None else None,
             "p90_latency_ms": round(p90, 1) if p90 is not None else None,
             # completions whose tool call executed (HTTP 200) per second: with random weights the

@@ -29,6 +29,7 @@
 //     one lane, bias / GELU / ReLU fused as in gemm.hip;
 //   * tiles in the same XCD-aware grouped order as gemm.hip; split-K by fp32 partials.
 #include <type_traits>
+#include <utility>
 
 #include "common.h"
 #include "kernels.h"
@@ -64,6 +65,16 @@ LK_DEVICE void barrier_raw() {
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("" ::: "memory");
+}
+
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>): a compile-time loop
+template <class Fn, int... I>
+LK_DEVICE void unroll_impl(Fn&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class Fn>
+LK_DEVICE void unroll(Fn&& f) {
+  unroll_impl(f, std::make_integer_sequence<int, N>{});
 }
 
 // acc += A(16x32) . B(32x16), acc pinned to AGPRs; volatile keeps the issue order
@@ -128,8 +139,10 @@ __device__ __forceinline__ void gemm4w_body(const bf16_t* __restrict__ X, long l
     xoff[i] = (unsigned)(((long)tm * kBM + row) * ldx * 2) + ch;
     woff[i] = (unsigned)(wrow(row) * K * 2) + ch;
   }
-  auto issue = [&](int s) {  // slice s -> ring slot s % 4
-    unsigned char* base = smem + (s & (kSlots - 1)) * kSlice + 16 * 4 * w * kRow;
+  // ring slots of the LDS-DMA mode (a 5-slot / 160 KB ring measured 2-3 % slower)
+  constexpr int RS = kSlots;
+  auto issue = [&](int s) {  // slice s -> ring slot s % RS
+    unsigned char* base = smem + (s % RS) * kSlice + 16 * 4 * w * kRow;
     const unsigned so = (unsigned)(s0 + s) * (kBKS * 2);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -155,9 +168,9 @@ __device__ __forceinline__ void gemm4w_body(const bf16_t* __restrict__ X, long l
   // are template parameters: a runtime condition would put a branch around every issue.
   auto step = [&](auto rd_t, auto dma_t, short8(&fx)[8], short8(&fw)[8], short8(&nx)[8], short8(&nw)[8], int s) {
     constexpr bool RD = decltype(rd_t)::value, DMA = decltype(dma_t)::value;
-    const unsigned char* nb = smem + ((s + 1) & (kSlots - 1)) * kSlice + fofs;
-    unsigned char* db = smem + ((s + 4) & (kSlots - 1)) * kSlice + 16 * 4 * w * kRow;
-    const unsigned so = (unsigned)(s0 + s + 4) * (kBKS * 2);
+    const unsigned char* nb = smem + ((s + 1) % RS) * kSlice + fofs;
+    unsigned char* db = smem + ((s + RS) % RS) * kSlice + 16 * 4 * w * kRow;
+    const unsigned so = (unsigned)(s0 + s + RS) * (kBKS * 2);
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       if constexpr (RD && MODE != 2 && MODE != 4) {
@@ -188,11 +201,80 @@ __device__ __forceinline__ void gemm4w_body(const bf16_t* __restrict__ X, long l
   using V1 = std::integral_constant<int, kDmaPerWave>;
   using V2 = std::integral_constant<int, 2 * kDmaPerWave>;
 
-  if constexpr (MODE != 1) {  // MODE 0 (+ the timing-only ablations 2-4 of its loop)
-  // prologue: slices 0..3 in flight, slice 0 landed and read
+  if constexpr (MODE == 5) {
+  // ---- 64-deep K-tiles, 128-B LDS rows (every DMA issue moves 8 rows x one full 128-B line:
+  // the 32-deep slices' half-line pieces measured 31 % of the loop in the ablations), a 2-slot
+  // ring (2 x 64 KB).  Fragments go per 32-deep half (kk); K-tile t:
+  //   half (t,0): MFMAs of frags (t,0) | read frags (t,1)
+  //   vmcnt(0) (own DMA of t+1 landed), lgkmcnt(0), barrier: t+1 readable, slot t%2 free
+  //   half (t,1): MFMAs of frags (t,1) | read frags (t+1,0), 16 DMA issues of tile t+2 -> slot t%2
+  constexpr int R2 = 128, REG2 = 256 * R2, SL2 = 2 * REG2;
+  const int lr8 = lane >> 3, lc8 = lane & 7;
+  auto swz2 = [](int row) { return (row >> 1) & 7; };
+  unsigned xo2[8], wo2[8];
 #pragma unroll
-  for (int s = 0; s < kSlots; ++s) issue(s);
-  wait_vm<3 * kDmaPerWave>();
+  for (int i = 0; i < 8; ++i) {  // instruction i of wave w: rows 64w + 8i .. +7 of each operand
+    const int row = 64 * w + 8 * i + lr8;
+    const unsigned ch = (unsigned)((lc8 ^ swz2(row)) << 4);
+    xo2[i] = (unsigned)(((long)tm * kBM + row) * ldx * 2) + ch;
+    wo2[i] = (unsigned)(wrow(row) * K * 2) + ch;
+  }
+  const int rs2 = swz2(r);
+  auto frag = [&](const unsigned char* slot, int row0, int kk) {
+    return *reinterpret_cast<const short8*>(slot + (row0 + r) * R2 + (((4 * kk + g) ^ rs2) << 4));
+  };
+  auto rd_half = [&](int t, int kk, short8(&fx)[8], short8(&fw)[8], int m) {
+    const unsigned char* sl = smem + (t & 1) * SL2;
+    fx[m] = frag(sl, wr * 128 + m * 16, kk);
+    fw[m] = frag(sl + REG2, wc * 128 + m * 16, kk);
+  };
+  auto dma2 = [&](int t, int i) {  // i < 8: X rows, else W rows
+    unsigned char* d = smem + (t & 1) * SL2 + (i < 8 ? 0 : REG2) + (64 * w + 8 * (i & 7)) * R2;
+    const unsigned so = (unsigned)(kt0 + t) * 128;
+    if (i < 8) __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)d, 16, xo2[i & 7], so, 0, 0);
+    else __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)d, 16, wo2[i & 7], so, 0, 0);
+  };
+  // the 64 MFMAs of one half (fx, fw), with the fragment reads of the next half (RD: tile nt,
+  // half nkk) and 16 DMA issues of tile t+2 (DMA) interleaved, 8 MFMAs per row m
+  auto half = [&](auto rd_t, auto dma_t, short8(&fx)[8], short8(&fw)[8], short8(&nx)[8], short8(&nw)[8], int nt,
+                  int nkk, int t) {
+    constexpr bool RD = decltype(rd_t)::value, DMA = decltype(dma_t)::value;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      if constexpr (RD) rd_half(nt, nkk, nx, nw, m);
+      if constexpr (DMA) {
+        dma2(t + 2, 2 * m);
+        dma2(t + 2, 2 * m + 1);
+      }
+#pragma unroll
+      for (int n = 0; n < 8; ++n) mfma(acc[m][n], fw[n], fx[m]);
+    }
+  };
+  auto ktile = [&](auto rd_t, auto dma_t, int t) {
+    half(T{}, F{}, fx0, fw0, fx1, fw1, t, 1, t);
+    wait_vm<0>();
+    wait_lgkm0();
+    barrier_raw();
+    half(rd_t, dma_t, fx1, fw1, fx0, fw0, t + 1, 0, t);
+  };
+  // prologue: tiles 0 and 1 in flight, tile 0 landed, frags (0,0) read
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma2(0, (i & 1) ? 8 + (i >> 1) : (i >> 1));
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma2(1, (i & 1) ? 8 + (i >> 1) : (i >> 1));
+  wait_vm<16>();
+  barrier_raw();
+#pragma unroll
+  for (int m = 0; m < 8; ++m) rd_half(0, 0, fx0, fw0, m);
+  int t = 0;
+  for (; t + 2 < nk; ++t) ktile(T{}, T{}, t);
+  ktile(T{}, F{}, t);        // nk - 2
+  ktile(F{}, F{}, t + 1);    // nk - 1
+  } else if constexpr (MODE != 1) {  // MODE 0 (+ the timing-only ablations 2-4 of its loop)
+  // prologue: slices 0 .. RS-1 in flight, slice 0 landed and read (ns >= RS + (RS & 1))
+#pragma unroll
+  for (int s = 0; s < RS; ++s) issue(s);
+  wait_vm<(RS - 1) * kDmaPerWave>();
   barrier_raw();
   {
     const unsigned char* b0 = smem + fofs;
@@ -202,23 +284,28 @@ __device__ __forceinline__ void gemm4w_body(const bf16_t* __restrict__ X, long l
       fw0[m] = *reinterpret_cast<const short8*>(b0 + kRegion + (wc * 128 + m * 16) * kRow);
     }
   }
-  // steady state: every slice reads the next one's fragments and issues the DMA of s + 4
+  // steady state: every slice reads the next one's fragments and issues the DMA of s + RS
+  using VS = std::integral_constant<int, (RS - 2) * kDmaPerWave>;
   int s = 0;
-  for (; s + 6 <= ns; s += 2) {
-    sync(V2{});
+  for (; s + RS + 2 <= ns; s += 2) {
+    sync(VS{});
     step(T{}, T{}, fx0, fw0, fx1, fw1, s);
-    sync(V2{});
+    sync(VS{});
     step(T{}, T{}, fx1, fw1, fx0, fw0, s + 1);
   }
-  // drain: the last 4 slices (ns >= 4: K-tiles per split >= 2), no DMA left to issue
-  sync(V2{});
-  step(T{}, F{}, fx0, fw0, fx1, fw1, s);
-  sync(V1{});
-  step(T{}, F{}, fx1, fw1, fx0, fw0, s + 1);
-  sync(V0{});
-  step(T{}, F{}, fx0, fw0, fx1, fw1, s + 2);
-  sync(V0{});
-  step(F{}, F{}, fx1, fw1, fx0, fw0, s + 3);
+  // drain: the last TL = RS + (RS & 1) slices; tail slice i issues a DMA while i < TL - RS and
+  // may leave min(TL - 2 - i, RS - 2) later slices in flight at its barrier
+  constexpr int TL = RS + (RS & 1);
+  auto tail = [&](auto i_t) {
+    constexpr int i = decltype(i_t)::value;
+    constexpr int left = (TL - 2 - i) < (RS - 2) ? (TL - 2 - i) : (RS - 2);
+    sync(std::integral_constant<int, (left > 0 ? left : 0) * kDmaPerWave>{});
+    using RDT = std::integral_constant<bool, (i < TL - 1)>;
+    using DMT = std::integral_constant<bool, (i < TL - RS)>;
+    if constexpr (i % 2 == 0) step(RDT{}, DMT{}, fx0, fw0, fx1, fw1, s + i);
+    else step(RDT{}, DMT{}, fx1, fw1, fx0, fw0, s + i);
+  };
+  unroll<TL>(tail);
   } else {
   // ---- register staging.  Slice t is loaded (8 x 16 B per lane: 4 X, 4 W row groups) into
   // staging set t & 1 at step t - 4, written to LDS slot t & 1 at step t - 2 (that slot's
@@ -406,7 +493,7 @@ int group_rows4() {
 template <int EPI, int MODE>
 void launch4m(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
               long ldo, int TM, int TN, int ks, hipStream_t st) {
-  constexpr int lds = MODE != 1 ? kLds : 2 * kSlice;
+  constexpr int lds = MODE == 5 ? 2 * 2 * 256 * 128 : MODE != 1 ? kLds : 2 * kSlice;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4w_kernel<EPI, MODE>),
@@ -424,6 +511,7 @@ void launch4(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int
   else if (g_mode4 == 2) launch4m<EPI, 2>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
   else if (g_mode4 == 3) launch4m<EPI, 3>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
   else if (g_mode4 == 4) launch4m<EPI, 4>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
+  else if (g_mode4 == 5) launch4m<EPI, 5>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
   else launch4m<EPI, 0>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
 }
 
@@ -467,7 +555,7 @@ int lk_gemm4w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, in
               bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, int variant) {
   // variants 2-4: timing-only ablations of variant 0's loop (2: no fragment reads, 3: no
   // LDS-DMA, 4: neither) -- WRONG results by construction, for the PMC / microbench only
-  if (variant < 0 || variant > 4) return -1;
+  if (variant < 0 || variant > 5) return -1;
   g_mode4 = variant;
   if (!lk_gemm4w_supported(M, N, K, epi, ks) || ldx % 8 || ldo % 8 || reinterpret_cast<uintptr_t>(out) % 16 ||
       (bias != nullptr && reinterpret_cast<uintptr_t>(bias) % 16))

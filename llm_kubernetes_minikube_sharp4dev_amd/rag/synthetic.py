@@ -70,8 +70,26 @@ def _sentence(rng: random.Random, n_min=8, n_max=22) -> str:
     return s[0].upper() + s[1:] + "."
 
 
-def make_document(i: int, seed: int = 0, target_chars: int = 1200) -> str:
+def _long_section(rng: random.Random, title: str, chars: int) -> str:
+    body = []
+    while len(title) + sum(len(b) + 1 for b in body) < chars:
+        body.append(_sentence(rng))
+    text = f"## {title}\n" + " ".join(body)
+    return text[:chars].rstrip() + ".\n"
+
+
+def make_document(i: int, seed: int = 0, target_chars: int = 1200, section_chars: int = 0) -> str:
+    """One runbook.  ``section_chars`` > 0: the long-evidence regime -- every section grown to
+    about that many characters (set it just under the 1200-char header-split cap of
+    ``RagIndex.cs:92-95`` so each section stays ONE chunk, and the /agent_rag prompt carries
+    6 evidence chunks near the 1500-char evidence cap of ``Minimal_RAG/Program.cs:159``)."""
     rng = random.Random(seed * 1_000_003 + i)
+    if section_chars > 0:
+        slug, title, tags = TOPICS[i % len(TOPICS)]
+        secs = [f"---\ntitle: \"{title} #{i}\"\nslug: \"{slug}-{i}\"\nallowed_namespaces: [\"dev\", \"staging\"]\n---\n"]
+        for name in ("Obiettivo", "Procedura", "Note operative", "Verifiche", "Rollback"):
+            secs.append(_long_section(rng, f"{name} ({slug})", section_chars))
+        return "\n".join(secs)
     slug, title, tags = TOPICS[i % len(TOPICS)]
     parts = []
     if rng.random() < 0.5:

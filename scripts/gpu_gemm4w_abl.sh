@@ -10,7 +10,7 @@ L = ops.lib()
 for (M, N, K) in [(8192, 4096, 14336), (8192, 4096, 4096)]:
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
-    fns = {f"4w_v{v}": (lambda v=v: L.gemm4w(x, w, None, 0, None, 1, v)) for v in (0, 2, 3, 4, 1)}
+    fns = {f"4w_v{v}": (lambda v=v: L.gemm4w(x, w, None, 0, None, 1, v)) for v in (0, 6, 5, 7)}
     fns["8w_s2"] = lambda: L.gemm(x, w, None, 0, 256, None, 2, 1)
     fns["lib"] = lambda: F.linear(x, w)
     for f in fns.values():

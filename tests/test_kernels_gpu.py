@@ -455,7 +455,7 @@ def test_gemm4w(hip, M, NK):
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
     assert hip.gemm4w_supported(M, N, K, 0)
-    for v in (0, 1):
+    for v in (0, 1, 5):
         _close(hip.gemm4w(x, w, variant=v), x.float() @ w.float().t(), 0.02, 0.01, f"gemm4w v{v} M{M} N{N} K{K}")
 
 
@@ -466,7 +466,7 @@ def test_gemm4w_asymmetric_layout(hip):
     w = (torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K) % 97 - 48).to(torch.bfloat16)
     exp = torch.zeros(M, N)
     exp[:K] = w.float().t().cpu()
-    for v in (0, 1):
+    for v in (0, 1, 5):
         assert torch.equal(hip.gemm4w(x, w, variant=v).float().cpu(), exp), v
 
 
@@ -478,7 +478,7 @@ def test_gemm4w_swiglu(hip, M, IK):
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(2 * I, K, device=DEV, dtype=torch.bfloat16) * 0.05
     a_ref = ref.silu_mul((x.float() @ w.float().t()).to(torch.bfloat16))
-    for v in (0, 1):
+    for v in (0, 1, 5):
         _close(hip.gemm4w(x, w, None, 1, variant=v), a_ref, 0.03, 0.01, f"gemm4w v{v} swiglu M{M} I{I}")
 
 
@@ -496,7 +496,7 @@ def test_gemm4w_bias_epilogues(hip, M, NK, epi):
         y = torch.nn.functional.gelu(y)
     elif epi == 4:
         y = torch.relu(y)
-    for v in (0, 1):
+    for v in (0, 1, 5):
         _close(hip.gemm4w(x, w, b, epi, variant=v), y, 0.03, 0.01, f"gemm4w v{v} epi{epi} M{M} N{N}")
 
 
@@ -513,7 +513,7 @@ def test_gemm4w_splitk(hip, MNK, splits, epi):
     if epi:
         y = (y + b.float()).to(torch.bfloat16).float()
     if hip.gemm4w_supported(M, N, K, epi, splits):
-        for v in (0, 1):
+        for v in (0, 1, 5):
             _close(hip.gemm4w(x, w, b, epi, None, splits, v), y, 0.03, 0.01,
                    f"gemm4w v{v} split{splits} epi{epi} M{M} N{N} K{K}")
 
