@@ -2,7 +2,9 @@
 """Per-call latency of the TP decode tail on one MI355X: two processes share the GPU and map
 each other's IPC buffers (the xGMI code path, minus the link): fused all-reduce + residual +
 RMSNorm (one kernel) vs one-shot all-reduce then the add+norm kernel, for B x 8192 bf16
-messages (B = 1 .. 256, the 70B TP=8 decode batch).  Each call is timed from a captured
+messages (B = 1 .. 256, the 70B TP=8 decode batch; 1024 / 4096, prefill chunks), and the
+two-shot (reduce-scatter + all-gather) forms.  With two ranks on one GPU there are no links:
+this is the kernel + handshake floor, not the xGMI transfer time.  Each call is timed from a captured
 hipGraph of 50 back-to-back calls (launch overhead excluded, as in the decode graphs).
 
     python benchmarks/xgmi_ar_bench.py [--json out.json]
@@ -23,7 +25,7 @@ import torch.distributed as dist  # noqa: E402
 import torch.multiprocessing as mp  # noqa: E402
 
 H = 8192
-BS = [1, 4, 16, 64, 128, 256]
+BS = [1, 4, 16, 64, 128, 256, 1024, 4096]
 REPS = 50
 
 
@@ -44,9 +46,12 @@ def _worker(rank, world, port, out):
     from llm_kubernetes_minikube_sharp4dev_amd.parallel.xgmi_ar import XgmiAllReduce
 
     tp = TPGroup(rank, world, dist.group.WORLD, ctrl=dist.group.WORLD, ranks=list(range(world)))
-    ar = XgmiAllReduce(tp, 8 << 20)
+    ar = XgmiAllReduce(tp, 64 << 20, two_shot=False)
+    ar2 = XgmiAllReduce(tp, 64 << 20, two_shot=True)
     rows = []
-    for B in BS:
+    # the sweep runs twice and the second pass is kept: the first call sequence of the process
+    # (B = 1 came first) read 3x slow on the first box, a warm-up artifact
+    for B in BS + BS:
         x = torch.randn(B, H, device="cuda").to(torch.bfloat16)
         res = torch.randn(B, H, device="cuda").to(torch.bfloat16)
         w = torch.ones(H, device="cuda", dtype=torch.bfloat16)
@@ -55,6 +60,8 @@ def _worker(rank, world, port, out):
             "fused": lambda: ar.all_reduce_rmsnorm_(x, res, w, 1e-5, o),
             "ar_then_norm": lambda: ops.lib().rmsnorm(ar.all_reduce_(x), w, 1e-5, res, o),
             "allreduce_only": lambda: ar.all_reduce_(x),
+            "fused_two_shot": lambda: ar2.all_reduce_rmsnorm_(x, res, w, 1e-5, o),
+            "allreduce_two_shot": lambda: ar2.all_reduce_(x),
         }
         rec = {"B": B, "bytes": B * H * 2}
         for name, fn in arms.items():
@@ -80,8 +87,8 @@ def _worker(rank, world, port, out):
                 b.synchronize()
                 ts.append(a.elapsed_time(b) * 1e3 / REPS)
             rec[name + "_us"] = round(sorted(ts)[len(ts) // 2], 2)
-        rec["error"] = ar.error()
-        rows.append(rec)
+        rec["error"] = ar.error() + ar2.error()
+        rows = [r for r in rows if r["B"] != B] + [rec]
     if rank == 0:
         torch.save(rows, out)
     dist.barrier()

@@ -613,7 +613,8 @@ struct XgmiAr {
     TORCH_CHECK(world >= 1 && world <= lk_xgmi_ar_max_ranks() && rank >= 0 && rank < world, "xgmi_ar: rank/world");
     TORCH_CHECK(bytes_ > 0 && bytes_ % 16 == 0, "xgmi_ar: staging bytes must be a positive multiple of 16");
     const size_t sig_bytes = (size_t)lk_xgmi_ar_sig_words() * sizeof(unsigned);
-    TORCH_CHECK(hipMalloc(&data, bytes) == hipSuccess, "xgmi_ar: hipMalloc staging");
+    // two regions of `bytes`: the staged inputs and (two-shot) the reduced slices
+    TORCH_CHECK(hipMalloc(&data, 2 * bytes) == hipSuccess, "xgmi_ar: hipMalloc staging");
     TORCH_CHECK(hipExtMallocWithFlags(&sig, sig_bytes, hipDeviceMallocUncached) == hipSuccess, "xgmi_ar: signal alloc");
     TORCH_CHECK(hipMalloc(reinterpret_cast<void**>(&err), sizeof(int)) == hipSuccess, "xgmi_ar: hipMalloc err");
     TORCH_CHECK(hipMemset(sig, 0, sig_bytes) == hipSuccess && hipMemset(err, 0, sizeof(int)) == hipSuccess &&
@@ -677,6 +678,30 @@ struct XgmiAr {
                                        bp(w), bp(out), (int)x.size(0), (int)x.size(1), (float)eps, err, cur_stream());
     CHECK_RC(rc, "xgmi_allreduce_rmsnorm");
   }
+  // two-shot (reduce-scatter + all-gather over the peer mappings) all-reduce of x [T, H] into
+  // out, or with residual / w given: residual += sum, out = RMSNorm(residual) * w
+  void all_reduce2(const at::Tensor& x, at::Tensor& out, const c10::optional<at::Tensor>& residual,
+                   const c10::optional<at::Tensor>& w, double eps) {
+    CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_CONTIG(x); CHECK_CONTIG(out);
+    TORCH_CHECK(x.dim() == 2 && out.sizes() == x.sizes() && x.size(1) % 8 == 0, "xgmi_ar2: x / out [T, H], H % 8");
+    TORCH_CHECK((size_t)x.numel() * 2 <= bytes, "xgmi_ar2: message larger than the staging region");
+    TORCH_CHECK(residual.has_value() == w.has_value(), "xgmi_ar2: residual and w together");
+    bf16_t* rp = nullptr;
+    const bf16_t* wp = nullptr;
+    if (residual.has_value()) {
+      CHECK_BF16((*residual)); CHECK_CONTIG((*residual)); CHECK_BF16((*w)); CHECK_CONTIG((*w));
+      TORCH_CHECK(residual->sizes() == x.sizes() && w->numel() == x.size(1), "xgmi_ar2: residual [T, H], w [H]");
+      rp = bp(*residual);
+      wp = bp(*w);
+    }
+    for (int r = 0; r < world; ++r) TORCH_CHECK(pdata[r] && psig[r], "xgmi_ar: open() not called");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "xgmi_ar2: 16-B alignment");
+    int rc = lk_xgmi_allreduce2(reinterpret_cast<bf16_t* const*>(pdata.data()),
+                                reinterpret_cast<unsigned* const*>(psig.data()), (long)(bytes / 2), rank, world, bp(x), rp,
+                                wp, bp(out), (int)x.size(0), (int)x.size(1), (float)eps, rp != nullptr, err,
+                                cur_stream());
+    CHECK_RC(rc, "xgmi_allreduce2");
+  }
   int error() const {
     int h = 0;
     TORCH_CHECK(hipMemcpy(&h, err, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess, "xgmi_ar: read error word");
@@ -697,6 +722,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("open", &XgmiAr::open)
       .def("all_reduce", &XgmiAr::all_reduce)
       .def("all_reduce_rmsnorm", &XgmiAr::all_reduce_rmsnorm)
+      .def("all_reduce2", &XgmiAr::all_reduce2, "", py::arg("x"), py::arg("out"), py::arg("residual") = py::none(),
+           py::arg("w") = py::none(), py::arg("eps") = 1e-5)
       .def("error", &XgmiAr::error)
       .def_readonly("bytes", &XgmiAr::bytes);
   m.doc() = "gfx950 (MI355X) HIP kernel library";

@@ -43,8 +43,11 @@ void lk_wsgemm_set_rot(int rot_mul);  // K-step rotation per column tile (0 = of
 int lk_ws_scores_f32(const bf16_t* x, long ldx, const bf16_t* w, int M, long N, int K, float* out, long ldo,
                      hipStream_t st);
 
-// xgmi_allreduce.hip (one-shot all-reduce over IPC-mapped peer buffers, K14)
+// xgmi_allreduce.hip (one-shot / two-shot all-reduce over IPC-mapped peer buffers, K14)
 int lk_xgmi_ar_sig_words();
+int lk_xgmi_allreduce2(bf16_t* const* data, unsigned* const* sig, long red_off, int rank, int world,
+                       const bf16_t* in, bf16_t* residual, const bf16_t* w, bf16_t* out, int T, int H, float eps,
+                       int norm, int* err, hipStream_t st);
 int lk_xgmi_ar_max_ranks();
 int lk_xgmi_allreduce_rmsnorm(bf16_t* const* data, unsigned* const* sig, int rank, int world, const bf16_t* in,
                               bf16_t* residual, const bf16_t* w, bf16_t* out, int T, int H, float eps, int* err,

@@ -16,5 +16,6 @@ def test_eight_fake_replicas_1000_rps_without_loss():
     r = run(replicas=8, frontends=5, clients=2, concurrency=256, requests=3000, tokens=48, step_s=0.002)
     print(r)
     assert r["lost"] == 0 and r["ok"] == r["requests"]
-    if (os.cpu_count() or 1) >= 8:
+    # the rate needs the host's CPUs to itself: under pytest-xdist the other workers take them
+    if (os.cpu_count() or 1) >= 8 and not os.environ.get("PYTEST_XDIST_WORKER"):
         assert r["req_per_s"] >= 1000, r

@@ -181,3 +181,85 @@ def test_xgmi_allreduce_rmsnorm_fused_bit_identical():
         for r in range(2):
             ok = torch.load(os.path.join(d, f"f{r}.pt"), weights_only=True)
             assert all(o[-1] and o[-2] for o in ok), f"rank {r}: {ok}"
+
+
+def _two_shot_worker(rank, world, port, out_dir):
+    """Two-shot (reduce-scatter + all-gather) forms on an odd world (3 processes on the one GPU):
+    exact integer sums of the plain all-reduce (row counts below, at and above the world size),
+    and the fused residual + RMSNorm form bit-identical to the one-shot fused kernel -- eager,
+    interleaved with one-shot calls (shared per-workgroup epochs), and replayed from a hipGraph."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp import TPGroup
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.xgmi_ar import XgmiAllReduce
+
+    tp = TPGroup(rank, world, dist.group.WORLD, ctrl=dist.group.WORLD, ranks=list(range(world)))
+    two = XgmiAllReduce(tp, 16 << 20, two_shot=True)
+    one = XgmiAllReduce(tp, 16 << 20, two_shot=False)
+    ok = []
+    for T, H in ((1, 8192), (2, 4096), (5, 4096), (64, 8192), (1000, 1024)):
+        x = _vals(T * H, rank).view(T, H).cuda()
+        two.all_reduce_(x)
+        torch.cuda.synchronize()
+        want = sum(_vals(T * H, r).float() for r in range(world)).view(T, H)
+        ok.append(("plain", T, H, bool(torch.equal(x.float().cpu(), want))))
+    x = _vals(24576, rank).cuda()  # 1-D message: viewed as rows of 8
+    two.all_reduce_(x)
+    torch.cuda.synchronize()
+    ok.append(("plain1d", 24576, 0, bool(torch.equal(x.float().cpu(), sum(_vals(24576, r).float() for r in range(world))))))
+    for T, H in ((3, 8192), (64, 8192), (257, 4096), (1024, 8192)):
+        g = torch.Generator().manual_seed(T * 17 + H)
+        xs = [torch.randn(T, H, generator=g).to(torch.bfloat16) for _ in range(world)]
+        res0 = torch.randn(T, H, generator=g).to(torch.bfloat16)
+        w = (torch.rand(H, generator=g) + 0.5).to(torch.bfloat16).cuda()
+        r1, r2 = res0.cuda(), res0.cuda()
+        y1 = one.all_reduce_rmsnorm_(xs[rank].cuda(), r1, w, 1e-5)
+        y2 = two.all_reduce_rmsnorm_(xs[rank].cuda(), r2, w, 1e-5)
+        torch.cuda.synchronize()
+        ok.append(("fused", T, H, bool(torch.equal(y1.cpu(), y2.cpu())) and bool(torch.equal(r1.cpu(), r2.cpu()))))
+    # hipGraph: two-shot fused + a one-shot all-reduce in the same graph, replayed
+    T, H = 96, 8192
+    xin = torch.zeros(T, H, dtype=torch.bfloat16, device="cuda")
+    small = torch.zeros(4096, dtype=torch.bfloat16, device="cuda")
+    res = torch.zeros(T, H, dtype=torch.bfloat16, device="cuda")
+    w = torch.ones(H, dtype=torch.bfloat16, device="cuda")
+    out = torch.empty(T, H, dtype=torch.bfloat16, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        two.all_reduce_rmsnorm_(xin, res, w, 1e-5, out)
+        one.all_reduce_(small)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        two.all_reduce_rmsnorm_(xin, res, w, 1e-5, out)
+        one.all_reduce_(small)
+    for it in range(3):
+        g = torch.Generator().manual_seed(2000 + it)
+        xs = [torch.randn(T, H, generator=g).to(torch.bfloat16) for _ in range(world)]
+        r0 = torch.randn(T, H, generator=g).to(torch.bfloat16)
+        xin.copy_(xs[rank].cuda())
+        res.copy_(r0.cuda())
+        small.copy_(_vals(4096, rank, it).cuda())
+        gr.replay()
+        torch.cuda.synchronize()
+        ref_r = r0.cuda()
+        ref_y = one.all_reduce_rmsnorm_(xs[rank].cuda(), ref_r, w, 1e-5)
+        torch.cuda.synchronize()
+        want_small = sum(_vals(4096, r, it).float() for r in range(world))
+        ok.append(("graph", it, 0, bool(torch.equal(out.cpu(), ref_y.cpu())) and bool(torch.equal(res.cpu(), ref_r.cpu()))
+                   and bool(torch.equal(small.float().cpu(), want_small))))
+    ok.append(("err", 0, 0, two.error() == 0 and one.error() == 0))
+    torch.save(ok, os.path.join(out_dir, f"s{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_xgmi_two_shot_allreduce_and_fused_norm():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_two_shot_worker, args=(3, _free_port(), d), nprocs=3, join=True)
+        for r in range(3):
+            ok = torch.load(os.path.join(d, f"s{r}.pt"), weights_only=True)
+            assert all(o[-1] for o in ok), f"rank {r}: {ok}"
