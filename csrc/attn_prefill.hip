@@ -69,6 +69,9 @@ struct PrefillParams {
   float* part_o;
   float* part_ml;
   float defer;  // PIPE: move the running max only when it grows by more than this (log2 units)
+  // context parallelism: position of sequence b's first query relative to its FIRST KEY (may be
+  // negative or past the keys: this rank holds only a shard of the keys); null = ctx - q_len
+  const int* q_past;
 };
 
 // NW waves per workgroup (4 or 8): WH of them share a row group (one head each), and
@@ -100,7 +103,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
   const int qbeg = p.cu_q[b];
   const int qlen = p.cu_q[b + 1] - qbeg;
   const int ctx = p.ctx_lens ? p.ctx_lens[b] : qlen;
-  const int past = ctx - qlen;
+  const int past = p.q_past ? p.q_past[b] : ctx - qlen;
   const int kend = CAUSAL ? min(ctx, past + q0 + QB) : ctx;
 
   const int qrow = q0 + rg * 32 + r;  // query index within the sequence (this lane's column)
@@ -473,7 +476,7 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
                      const int* block_tables, int bt_stride, const int* cu_q, const int* ctx_lens,
                      const int* tile_seq, const int* tile_q0, int ntiles, bf16_t* out, long os,
                      int Hq, int Hkv, int D, int BS, float scale, int causal, int paged,
-                     float* part_o, float* part_ml, hipStream_t st) {
+                     float* part_o, float* part_ml, const int* q_past, hipStream_t st) {
   if (ntiles == 0) return 0;
   if (Hq % Hkv) return -1;
   // 16-B output stores (permlane-paired epilogue): 16-B aligned output rows
@@ -487,7 +490,7 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
   while ((1 << bs_shift) < BS) ++bs_shift;
   PrefillParams pr{q, qs, k, v, ks, vs, block_tables, bt_stride, cu_q, ctx_lens, tile_seq,
                    tile_q0, out, os, Hq, Hkv, BS, bs_shift, scale * 1.4426950408889634f, part_o, part_ml,
-                   part_o ? 0.f : prefill_defer()};
+                   part_o ? 0.f : prefill_defer(), q_past};
   const int WH = G >= 4 ? 4 : G;
   const int NW = prefill_waves(G, D);
   dim3 grid(ntiles, Hq / WH);

@@ -412,8 +412,13 @@ at::Tensor flash_prefill(const at::Tensor& q, const at::Tensor& k, const at::Ten
                          const c10::optional<at::Tensor>& ctx_lens, const at::Tensor& tile_seq,
                          const at::Tensor& tile_q0, int64_t Hq, int64_t Hkv, int64_t D, double scale,
                          bool causal, const c10::optional<at::Tensor>& out_,
-                         const c10::optional<at::Tensor>& part_o, const c10::optional<at::Tensor>& part_ml) {
+                         const c10::optional<at::Tensor>& part_o, const c10::optional<at::Tensor>& part_ml,
+                         const c10::optional<at::Tensor>& q_past) {
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); CHECK_LASTDIM(q);
+  if (q_past) {
+    CHECK_I32(*q_past);
+    TORCH_CHECK(q_past->numel() >= cu_q.numel() - 1, "q_past: one entry per sequence");
+  }
   CHECK_I32(cu_q); CHECK_I32(tile_seq); CHECK_I32(tile_q0);
   TORCH_CHECK(q.dim() == 2 && q.size(1) >= Hq * D, "q must be [T, >=Hq*D] (head-major rows)");
   check_rows16(q, "q");
@@ -451,7 +456,7 @@ at::Tensor flash_prefill(const at::Tensor& q, const at::Tensor& k, const at::Ten
                             bt_stride, ip(cu_q), ipo(ctx_lens), ip(tile_seq), ip(tile_q0), tile_seq.numel(),
                             partial ? nullptr : bp(out), partial ? 0 : out.stride(0), Hq, Hkv, D, BS, (float)scale,
                             causal ? 1 : 0, paged ? 1 : 0, partial ? part_o->data_ptr<float>() : nullptr,
-                            partial ? part_ml->data_ptr<float>() : nullptr, cur_stream());
+                            partial ? part_ml->data_ptr<float>() : nullptr, ipo(q_past), cur_stream());
   CHECK_RC(rc, "flash_prefill");
   return out;
 }
@@ -760,7 +765,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_split_size", &decode_split_size);
   m.def("paged_decode", &paged_decode, "", py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("max_splits"), py::arg("split"), py::arg("scale"), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("out") = py::none(), py::arg("k_start") = py::none(), py::arg("pp_o") = py::none(), py::arg("pp_ml") = py::none());
   m.def("prefill_rows_per_tile", &prefill_rows_per_tile);
-  m.def("flash_prefill", &flash_prefill, "", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("block_tables"), py::arg("cu_q"), py::arg("ctx_lens"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("out") = py::none(), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none());
+  m.def("flash_prefill", &flash_prefill, "", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("block_tables"), py::arg("cu_q"), py::arg("ctx_lens"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("out") = py::none(), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("q_past") = py::none());
   m.def("knn_topk", &knn_topk, "", py::arg("corpus"), py::arg("cnorm"), py::arg("queries"), py::arg("qnorm"),
         py::arg("K"), py::arg("force_fused") = false);
   m.def("knn_merge", &knn_merge);

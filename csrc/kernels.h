@@ -93,7 +93,7 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
                      const int* block_tables, int bt_stride, const int* cu_q, const int* ctx_lens,
                      const int* tile_seq, const int* tile_q0, int ntiles, bf16_t* out, long os,
                      int Hq, int Hkv, int D, int BS, float scale, int causal, int paged,
-                     float* part_o, float* part_ml, hipStream_t st);
+                     float* part_o, float* part_ml, const int* q_past, hipStream_t st);
 
 // knn.hip
 int lk_knn_nblocks(long N);

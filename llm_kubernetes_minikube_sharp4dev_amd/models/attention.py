@@ -164,19 +164,49 @@ def merge_partials(o: torch.Tensor, lse: torch.Tensor) -> torch.Tensor:
     return (w[..., None] * o).sum(dim=0) / den[..., None]
 
 
-def cp_paged_attention(qkv, k_cache, v_cache, meta: AttnMeta, Hq: int, Hkv: int, D: int, scale: float,
-                       out: torch.Tensor, cp_group) -> torch.Tensor:
-    """Context-parallel attention: every rank attends the (replicated) queries over its
-    local key shard -- prefill rows causally by global position, decode rows over all
-    their keys -- then ONE all-gather of (o, lse) over ``cp_group`` and an LSE merge give
-    each rank the full result.  Collective volume per layer: T x Hq x (D + 1) f32 per
-    rank, independent of the context length (the KV shards never move)."""
-    import torch.distributed as dist
+_LN2 = 0.6931471805599453
 
-    from ..ops import reference as ref
 
+def cp_local_partials(qkv, k_cache, v_cache, meta: AttnMeta, Hq: int, Hkv: int, D: int, scale: float):
+    """This rank's attention partials over its key shard: (o f32 [T, Hq, D] normalised over
+    the shard, lse f32 [T, Hq], natural log; -inf where a query sees no key of the shard).
+
+    On the GPU: two flash-kernel launches in partial mode and no host sync -- prefill rows
+    causally with the mask shifted by the shard's first key position (``q_past`` = global
+    position of the first query - ``cp_key_start_p``), decode rows as one-query sequences over
+    all their local keys -- so the hook runs inside a captured step.  On the CPU: the fp32
+    per-sequence reference (``partial_attention``)."""
     Tp, Bd = meta.num_prefill_tokens, meta.num_decode
     T = Tp + Bd
+    if qkv.is_cuda and ops.use_hip(qkv):
+        dev = qkv.device
+        po = torch.empty(T, Hq, D, dtype=torch.float32, device=dev)
+        pml = torch.empty(T, Hq, 2, dtype=torch.float32, device=dev)
+        if Tp:
+            B = meta.num_prefill_seqs or (meta.cu_q.numel() - 1)
+            starts = meta.cp_key_start_p or [0] * B
+            k0 = torch.tensor(starts, dtype=torch.int32).to(dev, non_blocking=True)
+            q_past = (meta.positions.index_select(0, meta.cu_q[:-1].long()) - k0).to(torch.int32)
+            ts, tq = ops.prefill_tiles(meta.q_lens_cpu, meta.ctx_lens_cpu, Hq // Hkv, True, D)
+            tiles = (torch.from_numpy(ts).to(dev, non_blocking=True), torch.from_numpy(tq).to(dev, non_blocking=True))
+            ops.flash_prefill(qkv[:Tp, : Hq * D], k_cache, v_cache, meta.cu_q, Hq, Hkv, D, scale, True,
+                              block_tables=meta.block_tables_p, ctx_lens=meta.ctx_lens_p, tiles=tiles,
+                              part=(po[:Tp], pml[:Tp]), q_past=q_past)
+        if Bd:
+            # decode rows: one-query "sequences" over all their local keys (no mask)
+            cu = torch.arange(Bd + 1, dtype=torch.int32, device=dev)
+            ts, tq = ops.prefill_tiles([1] * Bd, [1] * Bd, Hq // Hkv, False, D)
+            tiles = (torch.from_numpy(ts).to(dev, non_blocking=True), torch.from_numpy(tq).to(dev, non_blocking=True))
+            ops.flash_prefill(qkv[Tp:T, : Hq * D], k_cache, v_cache, cu, Hq, Hkv, D, scale, False,
+                              block_tables=meta.block_tables_d, ctx_lens=meta.ctx_lens_d, tiles=tiles,
+                              part=(po[Tp:], pml[Tp:]))
+        m, l = pml[..., 0], pml[..., 1]
+        seen = l > 0
+        o = torch.where(seen[..., None], po / l.clamp_min(1e-30)[..., None], torch.zeros_like(po))
+        lse = torch.where(seen, (m + torch.log2(l.clamp_min(1e-30))) * _LN2, torch.full_like(m, float("-inf")))
+        return o, lse
+    from ..ops import reference as ref
+
     q_all = qkv[:T, : Hq * D].reshape(T, Hq, D)
     o_loc = torch.zeros(T, Hq, D, dtype=torch.float32, device=qkv.device)
     l_loc = torch.full((T, Hq), float("-inf"), dtype=torch.float32, device=qkv.device)
@@ -199,6 +229,21 @@ def cp_paged_attention(qkv, k_cache, v_cache, meta: AttnMeta, Hq: int, Hkv: int,
             r = Tp + i
             o_loc[r:r + 1], l_loc[r:r + 1] = partial_attention(q_all[r:r + 1], kb, vb, pos[r:r + 1], starts[i],
                                                                scale)
+    return o_loc, l_loc
+
+
+def cp_paged_attention(qkv, k_cache, v_cache, meta: AttnMeta, Hq: int, Hkv: int, D: int, scale: float,
+                       out: torch.Tensor, cp_group) -> torch.Tensor:
+    """Context-parallel attention: every rank attends the (replicated) queries over its
+    local key shard (:func:`cp_local_partials`) -- prefill rows causally by global position,
+    decode rows over all their keys -- then ONE all-gather of (o, lse) over ``cp_group`` and
+    an LSE merge give each rank the full result.  Collective volume per layer:
+    T x Hq x (D + 1) f32 per rank, independent of the context length (the KV shards never
+    move)."""
+    import torch.distributed as dist
+
+    T = meta.num_prefill_tokens + meta.num_decode
+    o_loc, l_loc = cp_local_partials(qkv, k_cache, v_cache, meta, Hq, Hkv, D, scale)
     C = dist.get_world_size(cp_group)
     packed = torch.cat([o_loc.reshape(T, -1), l_loc], dim=1)         # one collective
     allp = [torch.empty_like(packed) for _ in range(C)]

@@ -154,11 +154,14 @@ def prefill_tiles(q_lens: Sequence[int], ctx_lens: Sequence[int], G: int, causal
 
 def flash_prefill(q, k, v, cu_q, Hq: int, Hkv: int, D: int, scale: float, causal: bool,
                   block_tables=None, ctx_lens=None, q_lens_cpu=None, ctx_lens_cpu=None,
-                  tiles=None, out=None, part=None):
+                  tiles=None, out=None, part=None, q_past=None):
     """Varlen flash attention.  Paged when ``block_tables`` is given (K/V caches
     ``[NB, Hkv, BS, D]``), else dense K/V rows ``[T, >=Hkv*D]`` (encoder).
     ``part`` = (o f32 [T, Hq, D], ml f32 [T, Hq, 2]): write unnormalised partials for a
-    cascade merge instead of ``out`` (GPU only).
+    cascade / context-parallel merge instead of ``out`` (GPU only; ml = (running max, sum) in
+    the log2 domain).  ``q_past`` (int32 [B], GPU only): position of each sequence's first
+    query relative to its first key for the causal mask (a context-parallel key shard), instead
+    of ctx_len - q_len.
 
     ``q_lens_cpu`` / ``ctx_lens_cpu``: host copies of the lengths (the scheduler has
     them), used to build the tile list without a device sync."""
@@ -181,11 +184,13 @@ def flash_prefill(q, k, v, cu_q, Hq: int, Hkv: int, D: int, scale: float, causal
         if out is not None and part is None and (out.data_ptr() % 16 or out.stride(0) % 8):
             # the kernel's output rows leave as 16-byte stores: stage a misaligned view
             y = lib().flash_prefill(q, k, v, block_tables, cu_q, ctx_lens, tiles[0], tiles[1], Hq,
-                                    Hkv, D, scale, causal, None, None, None)
+                                    Hkv, D, scale, causal, None, None, None, q_past)
             out[:, : Hq * D].copy_(y)
             return out
         return lib().flash_prefill(q, k, v, block_tables, cu_q, ctx_lens, tiles[0], tiles[1], Hq,
-                                   Hkv, D, scale, causal, out, pp_o, pp_ml)
+                                   Hkv, D, scale, causal, out, pp_o, pp_ml, q_past)
+    if q_past is not None:
+        raise NotImplementedError("q_past: GPU kernel only")
     y = ref.flash_prefill(q, k, v, block_tables, cu_q, ctx_lens, Hq, Hkv, D, scale, causal)
     if out is not None:
         out[:, : Hq * D].copy_(y)

@@ -7,6 +7,8 @@ timeout -k 10 300 python -u -m pytest tests/test_rccl_gpu.py -x -v --timeout 240
 tail -3 gpurun_out/r3b/rccl.log
 timeout -k 10 300 python -u -m pytest tests/test_xgmi_ar_gpu.py -x -v --timeout 240 --timeout-method thread > gpurun_out/r3b/xgmi_tests.log 2>&1 || { tail -30 gpurun_out/r3b/xgmi_tests.log; exit 1; }
 tail -3 gpurun_out/r3b/xgmi_tests.log
+timeout -k 10 200 python -u -m pytest tests/test_cp_gpu.py -x -v --timeout 120 --timeout-method thread > gpurun_out/r3b/cp_tests.log 2>&1 || { tail -30 gpurun_out/r3b/cp_tests.log; exit 1; }
+tail -3 gpurun_out/r3b/cp_tests.log
 timeout -k 10 300 python -u benchmarks/xgmi_ar_bench.py --json gpurun_out/r3b/xgmi_ar_bench.json > gpurun_out/r3b/xgmi_bench.log 2>&1 || { tail gpurun_out/r3b/xgmi_bench.log; exit 2; }
 grep '"B"' gpurun_out/r3b/xgmi_bench.log
 timeout -k 10 600 python -u bench.py --long-evidence --kv-gb 96 --steps 10 --warmup 3 --json-out gpurun_out/r3b/rag_long.json > gpurun_out/r3b/rag_long.log 2>&1 || { tail gpurun_out/r3b/rag_long.log; exit 3; }

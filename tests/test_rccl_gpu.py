@@ -54,8 +54,13 @@ def _worker(rank, port, out):
         dist.all_reduce(buf)
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
+    # captured as the engine captures its decode graphs (engine/model_runner.py): with the
+    # default "global" capture mode the process group's watchdog thread, polling the events of
+    # earlier eager collectives, hits hipErrorStreamCaptureUnsupported and aborts the process
+    # (seen on MI355X / ROCm 7, first run of this test); "thread_local" confines the capture
+    # rules to the capturing thread
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         dist.all_reduce(buf)
         buf.mul_(2)
     buf.fill_(3)
