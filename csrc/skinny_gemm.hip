@@ -457,7 +457,7 @@ int dispatch_ws(int MT, int BN, const bf16_t* x, long ldx, const bf16_t* w, int 
     launch_ws<mt, bn, SWIGLU>(x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, part, part_ld, n_rows, st); \
     return 0;                                                                                           \
   }
-  LK_WS(4, 64) LK_WS(4, 128) LK_WS(8, 64) LK_WS(8, 128) LK_WS(16, 64) LK_WS(16, 128)
+  LK_WS(4, 64) LK_WS(4, 128) LK_WS(8, 64) LK_WS(8, 128) LK_WS(12, 64) LK_WS(12, 128) LK_WS(16, 64) LK_WS(16, 128)
 #undef LK_WS
   return -2;
 }
@@ -490,6 +490,11 @@ int dispatch_mt(int MT, const bf16_t* x, long ldx, const bf16_t* w, int M, int K
 }
 
 }  // namespace
+
+// padded row tiles of the weight-streaming GEMM: 16-row MFMA tiles, 4 waves splitting M
+// (the X bytes every column block stages grow with the padding: 192 rows for M 129-192
+// instead of 256)
+static int ws_mt(int M) { return M <= 64 ? 4 : M <= 128 ? 8 : M <= 192 ? 12 : 16; }
 
 // wsgemm launch plan for (M, N, K): BN (64/128) and split S maximising CU occupancy
 // (1 block per CU: its LDS ring is 72-144 KB), fewest partial slabs on ties.
@@ -528,7 +533,7 @@ int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, i
   if (S > 1 && part == nullptr) return -1;
   const int I = swiglu ? N / 2 : 0;
   const int n_tiles = (swiglu ? I : N) / per;
-  const int MT = M <= 64 ? 4 : M <= 128 ? 8 : 16;
+  const int MT = ws_mt(M);
   const int ks = K / S;
   float* p = S > 1 ? part : nullptr;
   const int rc = swiglu ? dispatch_ws<true>(MT, BN, x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, p, N, st)
@@ -553,7 +558,7 @@ void lk_wsgemm_set_rot(int rot_mul) { g_ws_rot_mul = rot_mul < 0 ? -1 : rot_mul;
 int lk_wsgemm_part(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, float* part,
                    hipStream_t st) {
   if (M < 1 || M > 256 || S < 2 || K % (S * 64) || (BN != 64 && BN != 128) || N % BN || part == nullptr) return -1;
-  const int MT = M <= 64 ? 4 : M <= 128 ? 8 : 16;
+  const int MT = ws_mt(M);
   const int rc = dispatch_ws<false>(MT, BN, x, ldx, w, M, K, K / S, S, N / BN, 0, nullptr, 0, part, N, st);
   LK_CHECK_LAUNCH();
   return rc;
@@ -567,7 +572,7 @@ int lk_ws_scores_f32(const bf16_t* x, long ldx, const bf16_t* w, int M, long N, 
   const int BN = 128;
   const long tiles = (N + BN - 1) / BN;
   if (tiles > (1L << 30)) return -1;
-  const int MT = M <= 64 ? 4 : M <= 128 ? 8 : 16;
+  const int MT = ws_mt(M);
   const int rc = dispatch_ws<false>(MT, BN, x, ldx, w, M, K, K, 1, (int)tiles, 0, nullptr, 0, out, ldo, st, N);
   LK_CHECK_LAUNCH();
   return rc;

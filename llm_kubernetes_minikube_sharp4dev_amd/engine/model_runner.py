@@ -127,6 +127,31 @@ class ModelRunner:
             # ops._gemm_default was as fast or faster (profiles/r2_gemm.md)
             self.gemm_tuning = ops.tune_gemm(model.gemm_shapes(), int(os.environ.get("LK_GEMM_TUNE_MAX_M", "4096")))
             log.info("prefill GEMM tuned for %d (M bucket, N, K, epilogue) shapes", len(self.gemm_tuning))
+        self.decode_tuning = {}
+        if (self.device.type == "cuda" and os.environ.get("LK_DECODE_TUNE", "1") == "1"
+                and hasattr(model, "decode_gemm_shapes")):
+            self.decode_tuning = self._tune_decode(model)
+
+    @staticmethod
+    def _tune_decode(model) -> dict:
+        """Weight-streaming kernel vs prefill GEMM per decode M bucket and projection
+        (ops.tune_decode, ~1 s).  Under TP the leader's measurements are used by every rank, so
+        the ranks of a group run the same kernels."""
+        tp = getattr(model, "tp", None)
+        lead = tp is None or not tp.enabled or getattr(tp, "simulated", False) or tp.rank == 0
+        res = ops.tune_decode(model.decode_gemm_shapes()) if lead else {}
+        if tp is not None and tp.enabled and not getattr(tp, "simulated", False):
+            import torch.distributed as dist
+
+            box = [dict(ops._DECODE_TABLE) if lead else None]
+            dist.broadcast_object_list(box, src=tp.ranks[0] if tp.ranks else 0, group=tp.ctrl or tp.group)
+            ops._DECODE_TABLE.clear()
+            ops._DECODE_TABLE.update(box[0])
+        picks = {}
+        for (m, n, k, sw), arm in sorted(ops._DECODE_TABLE.items()):
+            picks.setdefault(f"N{n} K{k}{' swiglu' if sw else ''}", []).append(f"{m}:{arm}")
+        log.info("decode GEMM routing (M bucket: kernel): %s", "; ".join(f"{k} {' '.join(v)}" for k, v in picks.items()))
+        return res
 
     @staticmethod
     def block_bytes(model, block_size: int) -> int:

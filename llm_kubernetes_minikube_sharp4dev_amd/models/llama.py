@@ -230,6 +230,12 @@ class LlamaModel(nn.Module):
         L = self.layers[0]
         return [(L.qkv, 0), (L.o, 0), (L.gate_up, 1), (L.down, 0)]
 
+    def decode_gemm_shapes(self):
+        """(weight, swiglu) of the projections a decode step runs, LM head included, for the
+        decode routing tuner (ops.tune_decode)."""
+        L = self.layers[0]
+        return [(L.qkv, False), (L.o, False), (L.gate_up, True), (L.down, False), (self.lm_head, False)]
+
     def kv_cache_shape(self, num_blocks: int, block_size: int):
         return (num_blocks, self.hkv, block_size, self.D)
 

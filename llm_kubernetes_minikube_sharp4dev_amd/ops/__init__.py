@@ -19,7 +19,7 @@ __all__ = [
     "rmsnorm", "layernorm", "embed_layernorm", "silu_mul", "gelu_", "relu_", "rope_kv_",
     "kv_write", "paged_decode", "flash_prefill", "prefill_tiles", "knn_topk", "knn_merge",
     "pool_normalize", "row_norms", "select_tokens", "repeat_penalty_", "sample", "linear", "linear_swiglu",
-    "decode_splits", "rope_cos_sin", "tune_gemm", "gemm", "linear_add_rmsnorm", "linear_rope_kv",
+    "decode_splits", "rope_cos_sin", "tune_gemm", "tune_decode", "gemm", "linear_add_rmsnorm", "linear_rope_kv",
 ]
 
 rope_cos_sin = ref.rope_cos_sin
@@ -273,6 +273,24 @@ WS_MAX_M = int(os.environ.get("LK_WS_MAX_M", "256"))
 WS_SWIGLU_MAX_M = 160
 
 
+# Measured per-shape choice between the weight-streaming kernel and the prefill GEMM for
+# decode batches (``tune_decode``, cold weights, at engine start): the static rule below is
+# wrong in both directions on some shapes (benchmarks/decode_route.py on MI355X,
+# profiles/r3_decode_route/: the 70B TP=8 gate_up shard at M 192-256 ran the prefill GEMM at
+# 0.35x of the ws kernel; the 70B QKV at M 160-256 ran ws at 0.79-0.90x of the GEMM).
+# {(M bucket, N, K, swiglu): "ws" | "gemm"}; buckets are the tuned M values, a batch uses the
+# smallest bucket >= M.
+_DECODE_TABLE: dict = {}
+DECODE_TUNE_MS = (32, 64, 96, 128, 160, 192, 224, 256)
+
+
+def _decode_bucket(M: int) -> Optional[int]:
+    for b in DECODE_TUNE_MS:
+        if M <= b:
+            return b
+    return None
+
+
 def _decode_gemm_kind(x, w, swiglu: bool) -> Optional[str]:
     if not (use_hip(x) and x.dim() == 2 and w.dim() == 2 and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16):
@@ -288,6 +306,11 @@ def _decode_gemm_kind(x, w, swiglu: bool) -> Optional[str]:
         return None
     if M <= SKINNY_MAX_M:
         return "skinny"
+    if _DECODE_TABLE and M > LM_HEAD_SKINNY_MAX_M:
+        b = _decode_bucket(M)
+        choice = _DECODE_TABLE.get((b, N, K, bool(swiglu))) if b is not None else None
+        if choice is not None:
+            return "ws" if choice == "ws" else None
     if N >= 65536 and not swiglu:
         if M <= LM_HEAD_SKINNY_MAX_M:
             return "skinny"
@@ -457,6 +480,56 @@ def tune_gemm(weights, max_m: int, min_m: int = 512, iters: int = 6, cold_bytes:
             out[key] = {f"s{c[0]}/{c[1]}": round(t, 1) for c, t in med.items()}
         del copies
     return out
+
+
+def tune_decode(weights, ms: Sequence[int] = DECODE_TUNE_MS, iters: int = 5, cold_bytes: int = 640 << 20) -> dict:
+    """For each decode-sized M bucket and each (weight, swiglu) pair, time the weight-streaming
+    kernel against the prefill GEMM with the weights arriving from HBM (each launch reads the
+    next of enough copies to overflow the 256 MB MALL, back-to-back launches as in a decode
+    graph) and record the faster in the dispatch table.  Returns {(M, N, K, swiglu): {arm: us}}."""
+    import statistics
+
+    L = lib()
+    out = {}
+    for w, swiglu in weights:
+        N, K = w.shape
+        swiglu = bool(swiglu)
+        copies = [w] + [w.clone() for _ in range(max(1, -(-cold_bytes // (N * K * 2)) - 1))]
+        for M in ms:
+            x = torch.randn(M, K, device=w.device, dtype=torch.bfloat16)
+            arms = {}
+            if M <= 256 and _decode_static_ok(N, K, swiglu):
+                arms["ws"] = lambda x, w: L.ws_linear(x, w, swiglu)
+            epi = 1 if swiglu else 0
+            cfg = _gemm_default(M, N, K, epi)
+            if cfg is not None and L.gemm_supported(M, N, K, epi, cfg[1], cfg[2]):
+                arms["gemm"] = lambda x, w, cfg=cfg: L.gemm(x, w, None, epi, cfg[1], None, cfg[0], cfg[2])
+            if len(arms) < 2:
+                continue
+            ts = {k: [] for k in arms}
+            for k, fn in arms.items():  # warm-up (and first-launch attributes)
+                fn(x, copies[0])
+            torch.cuda.synchronize()
+            for it in range(iters):
+                for k, fn in arms.items():
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record()
+                    for c in copies[1:] + copies[:1]:
+                        fn(x, c)
+                    b.record()
+                    b.synchronize()
+                    ts[k].append(a.elapsed_time(b) * 1e3 / len(copies))
+            med = {k: statistics.median(v) for k, v in ts.items()}
+            _DECODE_TABLE[(M, N, K, swiglu)] = min(med, key=med.get)
+            out[(M, N, K, swiglu)] = {k: round(v, 1) for k, v in med.items()}
+        del copies
+    return out
+
+
+def _decode_static_ok(N: int, K: int, swiglu: bool) -> bool:
+    if K % 256:
+        return False
+    return (N % 2 == 0 and (N // 2) % 64 == 0) if swiglu else N % 128 == 0
 
 
 def linear(x, w, b=None, act: Optional[str] = None):

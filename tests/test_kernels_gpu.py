@@ -355,7 +355,17 @@ def test_skinny_swiglu_matches_unfused(hip, M, IK):
         _close(hip.skinny_linear(x, w, True, 2), a_ref, 0.03, 0.01, "swiglu split 2")
 
 
-def test_linear_dispatch_decode_kernels(hip):
+@pytest.fixture
+def static_decode_routing():
+    """The static decode rule, without measurements an engine in an earlier test recorded."""
+    saved = dict(ops._DECODE_TABLE)
+    ops._DECODE_TABLE.clear()
+    yield
+    ops._DECODE_TABLE.clear()
+    ops._DECODE_TABLE.update(saved)
+
+
+def test_linear_dispatch_decode_kernels(hip, static_decode_routing):
     """Decode-sized projections take the weight-streaming kernel (whose split-K reduce the
     consumer fuses) from M = 1; the LM head at M <= 16 the fragment-load kernel."""
     x = torch.randn(8, 4096, device=DEV, dtype=torch.bfloat16)
@@ -371,7 +381,7 @@ def test_linear_dispatch_decode_kernels(hip):
     _close(ops.linear(x128, w), x128.float() @ w.float().t(), 0.02, 0.01)
 
 
-@pytest.mark.parametrize("M", [1, 2, 8, 16, 33, 64, 65, 100, 128, 129, 200, 256])
+@pytest.mark.parametrize("M", [1, 2, 8, 16, 33, 64, 65, 100, 128, 129, 160, 192, 200, 256])
 @pytest.mark.parametrize("NK", [(6144, 4096), (4096, 4096), (4096, 14336), (1280, 8192), (128256, 4096)])
 def test_ws_linear(hip, M, NK):
     """LDS-DMA staged weight-streaming GEMM (every BN / split plan) vs an fp32 matmul."""
@@ -387,7 +397,7 @@ def test_ws_linear(hip, M, NK):
                 _close(hip.ws_linear(x, w, False, bn, S), y_ref, 0.02, 0.01, f"ws bn{bn} S{S}")
 
 
-@pytest.mark.parametrize("M", [1, 8, 64, 128, 256])
+@pytest.mark.parametrize("M", [1, 8, 64, 128, 150, 192, 256])
 @pytest.mark.parametrize("IK", [(14336, 4096), (3584, 8192)])
 def test_ws_swiglu(hip, M, IK):
     I, K = IK
@@ -739,3 +749,29 @@ def test_select_allowed_matches_masked_select(hip, sample):
     b = hip.select_tokens(masked, temps, 1234, 5, None)
     assert torch.equal(a, b)
     assert int(a[2]) == 77 or sample
+
+
+def test_tune_decode_routes_by_measurement(hip):
+    """ops.tune_decode fills the decode routing table from cold-weight timings, and
+    _decode_gemm_kind / linear follow it for every bucket (results stay exact either way)."""
+    w = torch.randn(7168, 8192, device=DEV, dtype=torch.bfloat16) * 0.02  # 70B TP=8 gate_up shard
+    o = torch.randn(8192, 1024, device=DEV, dtype=torch.bfloat16) * 0.02   # 70B TP=8 o shard
+    saved = dict(ops._DECODE_TABLE)
+    try:
+        ops._DECODE_TABLE.clear()
+        res = ops.tune_decode([(w, True), (o, False)], ms=(64, 192, 256), iters=3, cold_bytes=256 << 20)
+        assert set(res) == {(m, n, k, sw) for m in (64, 192, 256) for (n, k, sw) in ((7168, 8192, True), (8192, 1024, False))}
+        for (m, n, k, sw), arms in res.items():
+            assert set(arms) == {"ws", "gemm"} and all(v > 0 for v in arms.values())
+            pick = ops._DECODE_TABLE[(m, n, k, sw)]
+            assert pick == min(arms, key=arms.get)
+            x = torch.randn(m - 7, k, device=DEV, dtype=torch.bfloat16)  # same bucket
+            kind = ops._decode_gemm_kind(x, w if sw else o, sw)
+            assert kind == ("ws" if pick == "ws" else None)
+            if sw:
+                _close(ops.linear_swiglu(x, w), ref.silu_mul((x.float() @ w.float().t()).to(torch.bfloat16)), 0.03, 0.01)
+            else:
+                _close(ops.linear(x, o), x.float() @ o.float().t(), 0.02, 0.01)
+    finally:
+        ops._DECODE_TABLE.clear()
+        ops._DECODE_TABLE.update(saved)
