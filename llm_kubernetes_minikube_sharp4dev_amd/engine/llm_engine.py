@@ -6,6 +6,7 @@ from __future__ import annotations
 
 import asyncio
 import collections
+import os
 import threading
 import time
 from typing import Callable, Optional
@@ -25,6 +26,11 @@ log = get_logger("engine")
 
 def _plain_greedy(p: SamplingParams) -> bool:
     return p.is_greedy and p.logits_processor is None and (p.repeat_penalty == 1.0 or p.repeat_last_n == 0)
+
+
+# order of the pipelined step's phases: "csl" (default) collect -> sample -> launch, or the
+# round-2 "lcs" launch -> collect -> sample (A/B knob)
+PIPELINE_ORDER = os.environ.get("LK_PIPELINE", "csl")
 
 
 class LLMEngine:
@@ -54,6 +60,7 @@ class LLMEngine:
         self.steps = 0
         self.launches = 0
         self._inflight = None  # the launched-and-sampled step not yet collected (step_pipelined)
+        self._pending = None   # the launched step not yet sampled (step_pipelined, LK_PIPELINE=csl)
         # optional per-step trace: (prefill tokens, decode rows, wall seconds) -- bench.py
         self.step_trace: Optional[list] = None
 
@@ -102,6 +109,13 @@ class LLMEngine:
     #                     grammar masks, scheduling, input building, admission).  A
     #                     request finishing by length is not stepped speculatively; one
     #                     stopping on EOS / a stop string wastes one row of one step.
+    #                     Default order (LK_PIPELINE=csl): collect(N) -> sample(N+1) ->
+    #                     launch(N+2), the same one-step-in-flight invariant rotated so that
+    #                     the caller's per-step work (reaping finished requests, admission)
+    #                     runs AFTER the next forward is enqueued: the device then holds two
+    #                     forwards of work while the host does it, instead of waiting for it
+    #                     (a kernel trace of the headline showed ~0.7 ms of device idle per
+    #                     7 ms decode step with the lcs order, profiles/r3_gaps/).
 
     @torch.inference_mode()
     def step(self) -> list:
@@ -118,18 +132,32 @@ class LLMEngine:
         PREVIOUS launch).  Call :meth:`flush` when done.  Under tensor parallelism the
         worker ranks gather the in-flight inputs from their own copy of greedy ids, or
         from the driver's sampled ids broadcast over the TP group."""
-        nxt = self._launch()
+        if PIPELINE_ORDER == "lcs":
+            nxt = self._launch()
+            out = self._collect(self._inflight) if self._inflight is not None else []
+            self._inflight = self._sample(nxt) if nxt is not None else None
+            return out
         out = self._collect(self._inflight) if self._inflight is not None else []
-        self._inflight = self._sample(nxt) if nxt is not None else None
+        self._inflight = self._sample(self._pending) if self._pending is not None else None
+        self._pending = self._launch()
         return out
+
+    @property
+    def in_flight(self) -> bool:
+        """A pipelined step is launched and not yet collected."""
+        return self._inflight is not None or self._pending is not None
 
     @torch.inference_mode()
     def flush(self) -> list:
-        """Collect the in-flight pipelined step, if any."""
-        if self._inflight is None:
-            return []
-        p, self._inflight = self._inflight, None
-        return self._collect(p)
+        """Collect the in-flight pipelined step(s), if any."""
+        out = []
+        if self._inflight is not None:
+            p, self._inflight = self._inflight, None
+            out = self._collect(p)
+        if self._pending is not None:
+            p, self._pending = self._pending, None
+            out += self._collect(self._sample(p))
+        return out
 
     def _launch(self):
         with self.lock:
@@ -324,7 +352,7 @@ class AsyncLLMEngine:
     def _loop_body(self):
         while not self._stop:
             if not self.engine.has_work():
-                if self.engine._inflight is not None:
+                if self.engine.in_flight:
                     with self.watchdog.busy():
                         self.engine.flush()
                     continue
