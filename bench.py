@@ -431,7 +431,7 @@ def main():
                for k in ("embed_s", "knn_s", "knn_gpu_s", "prompt_s")
                if any(r.timings and k in r.timings for r in results)} if results else {}
         steps_acct = {k: round(statistics.mean(r.timings[k] for r in results if r.timings and r.timings.get(k) is not None), 2)
-                      for k in ("steps_queued", "steps_in_system", "steps_run")
+                      for k in ("steps_queued", "steps_in_system", "steps_run", "jumped_tokens")
                       if any(r.timings and r.timings.get(k) is not None for r in results)}
         par = f"dp{n_replicas}" if args.tp == 1 else f"tp{args.tp}" + (f"xdp{n_replicas}" if n_replicas > 1 else "")
         sim = {}
@@ -491,6 +491,9 @@ def main():
                              "greedy, ignore_eos" + (", tool-call grammar" if args.constrained else "")),
                 "prefix_caching": not args.no_prefix_cache,
                 "hip_graphs": not args.no_graphs,
+                # grammar-forced tokens appended by the host and run as extend chunks (every
+                # token still gets its forward pass; LK_JUMP_FORWARD=0 steps them one by one)
+                "jump_forward": bool(args.constrained and args.sampling == "greedy" and _jump_forward_on()),
                 "avg_cached_prefix_tokens": round(statistics.mean(pre), 1) if pre else 0,
                 "stage_means_s": {k: round(v, 4) for k, v in tim.items()},
                 "engine_steps_per_request": steps_acct,
@@ -508,6 +511,12 @@ def main():
                 f.write(line + "\n")
     if world > 1:
         dist.destroy_process_group()
+
+
+def _jump_forward_on() -> bool:
+    from llm_kubernetes_minikube_sharp4dev_amd.engine import llm_engine
+
+    return llm_engine.JUMP_FORWARD
 
 
 if __name__ == "__main__":

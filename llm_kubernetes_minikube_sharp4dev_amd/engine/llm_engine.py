@@ -32,6 +32,18 @@ def _plain_greedy(p: SamplingParams) -> bool:
 # round-2 "lcs" launch -> collect -> sample (A/B knob)
 PIPELINE_ORDER = os.environ.get("LK_PIPELINE", "csl")
 
+# grammar jump-forward (LK_JUMP_FORWARD=0 disables): tokens a request's grammar leaves exactly
+# one choice for are appended by the host as soon as the token before them is known, and run
+# through the model together as one extend chunk instead of one decode step each
+JUMP_FORWARD = os.environ.get("LK_JUMP_FORWARD", "1") != "0"
+
+
+def _jump_ok(p: SamplingParams) -> bool:
+    """Forced tokens can be appended without sampling: a grammar is set, and no repeat
+    penalty reads the device history ring the sampler kernel appends to (host-appended
+    tokens would be missing from it)."""
+    return p.logits_processor is not None and (p.repeat_penalty == 1.0 or p.repeat_last_n == 0)
+
 
 class LLMEngine:
     def __init__(self, model, tokenizer=None, block_size: int = 16, max_model_len: int = 8192,
@@ -199,7 +211,8 @@ class LLMEngine:
             else:
                 host = ids
             for i, s in enumerate(seqs):
-                s.num_inflight, s.inflight_row = 1, i
+                if not s.discard_rows:  # a row whose token jump-forward already appended stays out
+                    s.num_inflight, s.inflight_row = 1, i
             self.runner.prev_ids = ids
             self.runner.prev_sampled_rows = 0 if greedy else len(rows)
         return (batch, rows, host, ev, ts, t0, t1, time.perf_counter(), ev0)
@@ -215,10 +228,17 @@ class LLMEngine:
                 ids = host.tolist()
                 now = t2 = time.perf_counter()
                 for (seq, _), tid in zip(rows, ids):
+                    if seq.discard_rows:
+                        # the row predicted a token jump-forward appended meanwhile: its KV
+                        # write (the previous token) is what the step was for
+                        seq.discard_rows -= 1
+                        continue
                     seq.num_inflight, seq.inflight_row = 0, -1
                     if seq.finished:
                         continue  # aborted, or stopped while this step was in flight
                     self._append(seq, int(tid), now)
+                    if JUMP_FORWARD and not seq.finished and _jump_ok(seq.params):
+                        self._jump(seq, now)
                     out.append(seq)
             for seq, _, _ in batch.items:
                 if not seq.finished:
@@ -238,6 +258,35 @@ class LLMEngine:
             M.KV_USAGE.set(self.allocator.usage())
             M.RUNNING.set(len(self.scheduler.running))
             return out
+
+    def _jump(self, seq: Sequence, now: float):
+        """Grammar jump-forward: append the tokens ``seq``'s grammar allows exactly one choice
+        for (literal keys, punctuation, the rest of a unique tool name), so the model runs
+        them as one extend chunk -- every forced token still gets its forward pass (its KV
+        feeds the next sampled token) -- instead of spending a decode step on each.  The
+        output is the one step-by-step decoding gives: a one-id mask makes that id the draw.
+        A request's last token is always left to the sampler, so no forward pass of the
+        step-by-step run is dropped.  If the step already in flight is computing the KV of
+        the token just collected, that row's prediction is discarded at its collect."""
+        p = seq.params
+        inflight_kv = seq.num_computed >= seq.length  # the launched step writes the last token's KV
+        room = min(p.max_tokens - len(seq.output_ids), self.max_model_len - seq.length) - 1
+        n = 0
+        while n < room:
+            allowed = p.logits_processor(seq.output_ids)
+            if allowed is None or len(allowed) != 1:
+                break
+            tid = int(allowed[0])
+            if tid in self.eos_ids and not p.ignore_eos:
+                break  # an end of sequence stays a sampled stop
+            self._append(seq, tid, now)
+            n += 1
+            if seq.finished:  # a stop string completed
+                return
+        if n:
+            seq.jumped += n
+            if inflight_kv:
+                seq.discard_rows += 1
 
     def _append(self, seq: Sequence, tid: int, now: float):
         if seq.first_token_at is None:

@@ -33,6 +33,10 @@ class Sequence:
     # value the host has not collected yet, and its row in that step's id tensor
     num_inflight: int = 0
     inflight_row: int = -1
+    # grammar jump-forward (LLMEngine._jump): output tokens appended without sampling, and
+    # launched rows whose predictions are void because such tokens were appended meanwhile
+    jumped: int = 0
+    discard_rows: int = 0
     status: Status = Status.WAITING
     finish_reason: Optional[str] = None
     arrival: float = field(default_factory=time.perf_counter)
@@ -90,7 +94,7 @@ class Sequence:
         n = len(self.output_ids)
         tpot = ((end - self.first_token_at) / (n - 1)) if (self.first_token_at and n > 1) else None
         return {"e2e_s": end - self.arrival, "ttft_s": ttft, "tpot_s": tpot, "prompt_tokens": len(self.prompt_ids),
-                "output_tokens": n, "cached_prefix_tokens": self.num_cached_prefix,
+                "output_tokens": n, "jumped_tokens": self.jumped, "cached_prefix_tokens": self.num_cached_prefix,
                 "preemptions": self.num_preemptions,
                 "steps_queued": (self.step_first - self.step_arrival) if self.step_first is not None else None,
                 "steps_in_system": (self.step_finish - self.step_arrival) if self.step_finish is not None else None,

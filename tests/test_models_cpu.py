@@ -155,6 +155,48 @@ def test_pipelined_steps_match_synchronous():
     assert eng.allocator.usage() == 0.0 or not eng.scheduler.running
 
 
+def test_jump_forward_matches_step_by_step(monkeypatch):
+    """Grammar jump-forward (tokens with a one-id mask appended by the host and run as an
+    extend chunk) gives exactly the step-by-step tokens, synchronous and pipelined, under
+    chunked prefill and preemption, with fewer engine steps per request; the last token
+    of every request is still sampled."""
+    from llm_kubernetes_minikube_sharp4dev_amd.engine import llm_engine
+
+    m = build_decoder("llama-tiny", dtype=torch.float32)
+    V = m.cfg.vocab_size
+    prompts = [list(range(3, 3 + n)) for n in (70, 33, 5, 100, 17)]
+
+    def proc(hist):  # runs of forced tokens (a literal) between free choices
+        n = len(hist)
+        if n % 7 in (2, 3, 4) or (n % 11 == 5):
+            return [(n * 37 + 11) % V]
+        return list(range(1 + (n % 5), V, 3))
+
+    cases = [
+        (lambda: SamplingParams.greedy(20, logits_processor=proc), {}),
+        (lambda: SamplingParams.greedy(20, logits_processor=proc), {"max_num_batched_tokens": 24}),
+        (lambda: SamplingParams.greedy(30, logits_processor=proc), {"num_blocks": 10}),
+    ]
+    for params_fn, kw in cases:
+        monkeypatch.setattr(llm_engine, "JUMP_FORWARD", False)
+        off = _engine(m, **kw).generate(prompts, params_fn())
+        ref = [s.output_ids for s in off]
+        assert all(s.jumped == 0 for s in off)
+        monkeypatch.setattr(llm_engine, "JUMP_FORWARD", True)
+        on = _engine(m, **kw).generate(prompts, params_fn())
+        assert [s.output_ids for s in on] == ref
+        assert all(s.jumped > 0 for s in on)
+        assert sum(s.steps_run for s in on) < sum(s.steps_run for s in off)
+        assert _run_pipelined(_engine(m, **kw), prompts, params_fn) == ref
+        assert _run_pipelined(_engine(m, **kw), prompts, params_fn, stagger=3) == ref
+    # a forced final token is not appended by the host: with every token forced the request
+    # still takes its last token from the sampler (no forward pass of the step-by-step run skipped)
+    eng = _engine(m)
+    s = eng.generate([prompts[2]], SamplingParams.greedy(6, logits_processor=lambda h: [9]))[0]
+    assert s.output_ids == [9] * 6 and s.jumped == 4  # first sampled, 4 jumped, last sampled
+    assert eng.allocator.usage() == 0.0 or not eng.scheduler.running
+
+
 def test_fused_decode_ops_cpu_fallback():
     """ops.linear_add_rmsnorm / ops.linear_rope_kv on CPU tensors are the unfused
     reference ops (the HIP fusions only exist for split-K decode shapes on the GPU)."""
