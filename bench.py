@@ -282,14 +282,17 @@ def main():
         # TP follower: execute the driver's steps (and its barriers) until it says stop
         run_tp_worker(llm, tpg, **runner_kw)
     else:
+        # decode-graph buckets: one row per running request, plus the rows of jump-forward
+        # extend chunks under the tool-call grammar
+        graph_rows = max(args.batch, 1) * (2 if args.constrained and args.sampling == "greedy" else 1)
         if args.tp > 1:
             engine = make_tp_engine(llm, tpg, tok, engine_kw=engine_kw, **runner_kw)
             if runner_kw["use_graphs"]:
-                tp_capture_all(engine, max_batch=max(args.batch, 1), variants=(args.sampling == "greedy" and not args.constrained,))
+                tp_capture_all(engine, max_batch=graph_rows, variants=(args.sampling == "greedy" and not args.constrained,))
         else:
             engine = LLMEngine(llm, tok, **runner_kw, **engine_kw)
             if runner_kw["use_graphs"]:
-                engine.runner.capture_all(max_batch=max(args.batch, 1), variants=(args.sampling == "greedy" and not args.constrained,))
+                engine.runner.capture_all(max_batch=graph_rows, variants=(args.sampling == "greedy" and not args.constrained,))
         k8s = FakeCluster.default()
         rag = RagAgentPipeline(index, engine, tok, k8s, cfg)
         agent = AgentPipeline(engine, tok, k8s, cfg)

@@ -51,14 +51,18 @@ class LLMEngine:
                  enable_prefix_caching: bool = True, use_graphs: bool = True, num_blocks: Optional[int] = None,
                  kv_cache_gb: Optional[float] = None, gpu_memory_fraction: float = 0.85, seed: int = 0,
                  eos_ids: Optional[set] = None, _runner: Optional[ModelRunner] = None, token_align: int = 256,
-                 token_align_wave: int = 0):
+                 token_align_wave: int = 0, prefill_hold: Optional[int] = None):
         self.model = model
         self.tokenizer = tokenizer
         self.runner = _runner or ModelRunner(model, block_size, max_model_len, max_num_seqs, num_blocks,
                                              kv_cache_gb, gpu_memory_fraction, use_graphs)
         self.allocator = make_allocator(self.runner.num_blocks, block_size, enable_prefix_caching)
+        if prefill_hold is None:
+            prefill_hold = int(os.environ.get("LK_PREFILL_HOLD", "0"))
         self.scheduler = Scheduler(self.allocator, block_size, max_num_seqs, max_num_batched_tokens, max_model_len,
-                                   token_align, token_align_wave)
+                                   token_align, token_align_wave, prefill_hold,
+                                   int(os.environ.get("LK_HOLD_MIN_DECODE", "64")),
+                                   float(os.environ.get("LK_HOLD_FILL", "1.0")))
         self.sampler = Sampler(model.cfg.vocab_size, seed, history_len=max_model_len)
         self.max_model_len = max_model_len
         if eos_ids is None:

@@ -33,6 +33,9 @@ from ..utils.logging import get_logger
 
 log = get_logger("engine.runner")
 
+# extend chunks of generated tokens up to this many tokens run as decode rows (0: as prefill)
+EXTEND_AS_DECODE = int(os.environ.get("LK_EXTEND_AS_DECODE", "16"))
+
 
 class _PinnedStager:
     """One host->device copy per step: the step's small host arrays (token ids, positions,
@@ -111,7 +114,8 @@ class ModelRunner:
         # are already served from the 256 MB Infinity Cache, so the extra flash pass and
         # the unconditional merge cost more than the HBM bytes they save.
         self.cascade = self.device.type == "cuda" and os.environ.get("LK_CASCADE", "0") == "1"
-        self.graph_sizes = sorted(b for b in graph_batch_sizes if b <= max_num_seqs)
+        # buckets up to twice the sequence cap: jump-forward extend chunks add decode rows
+        self.graph_sizes = sorted(b for b in graph_batch_sizes if b <= 2 * max_num_seqs)
         self.graphs: dict = {}
         self._graph_pool = None
         self._ws = None
@@ -197,16 +201,32 @@ class ModelRunner:
 
     def _decode_rows(self, dec, width, pad_to=0):
         """(ids, positions, slots, ctx, block tables) of the decode rows; native
-        (csrc/runtime/step_builder.cpp) when the runtime is built."""
-        tables = [s.block_table for s, _, _ in dec]
-        starts = [st for _, st, _ in dec]
-        # an in-flight input token (pipelined stepping) is not on the host yet: 0 here,
-        # gathered on the device from the previous step's ids (StepInputs.gather)
-        toks = [s.token_at(st) if st < s.length else 0 for s, st, _ in dec]
-        lens = [s.length + s.num_inflight for s, _, _ in dec]
+        (csrc/runtime/step_builder.cpp) when the runtime is built.  An item of n > 1 tokens
+        (a short extend chunk: jump-forward tokens) becomes n rows with causal contexts."""
+        if all(n == 1 for _, _, n in dec):
+            tables = [s.block_table for s, _, _ in dec]
+            starts = [st for _, st, _ in dec]
+            # an in-flight input token (pipelined stepping) is not on the host yet: 0 here,
+            # gathered on the device from the previous step's ids (StepInputs.gather)
+            toks = [s.token_at(st) if st < s.length else 0 for s, st, _ in dec]
+            lens = [s.length + s.num_inflight for s, _, _ in dec]
+        else:
+            tables, starts, toks, lens = [], [], [], []
+            for s, st, n in dec:
+                if n == 1:
+                    tables.append(s.block_table)
+                    starts.append(st)
+                    toks.append(s.token_at(st) if st < s.length else 0)
+                    lens.append(s.length + s.num_inflight)
+                    continue
+                for i in range(st, st + n):  # extend tokens are host-known (never in flight)
+                    tables.append(s.block_table)
+                    starts.append(i)
+                    toks.append(s.token_at(i))
+                    lens.append(i + 1)
         if _native_rt is not None:
             return _native_rt.decode_rows(tables, starts, toks, lens, self.bs, width, pad_to)
-        P = max(len(dec), pad_to)
+        P = max(len(tables), pad_to)
         ids = np.zeros(P, dtype=np.int32)
         pos = np.zeros(P, dtype=np.int32)
         slots = np.full(P, -1, dtype=np.int32)
@@ -247,17 +267,30 @@ class ModelRunner:
     def _gather(dec, offset: int):
         """(dst rows, src rows in the previous step's ids) of decode rows whose input
         token is still in flight, or None."""
-        g = [(offset + i, s.inflight_row) for i, (s, st, _) in enumerate(dec) if st >= s.length]
+        g, r = [], offset
+        for s, st, n in dec:
+            if n == 1 and st >= s.length:
+                g.append((r, s.inflight_row))
+            r += n
         if not g:
             return None
         a = np.asarray(g, dtype=np.int64)
         return a[:, 0].copy(), a[:, 1].copy()
 
+    def _as_decode(self, seq, start: int, n: int) -> bool:
+        """Decode rows: one-token steps, and short extend chunks of generated tokens
+        (jump-forward): n causal decode rows over the paged KV beat a flash-prefill tile
+        whose few query rows each walk the whole context in one workgroup."""
+        if seq.is_decode:
+            return True
+        return 1 < n <= EXTEND_AS_DECODE and start >= len(seq.prompt_ids) and seq.num_inflight == 0
+
     def _prepare(self, items):
-        if self.use_graphs and items and all(s.is_decode for s, _, _ in items) and len(items) <= self.graph_sizes[-1]:
+        if (self.use_graphs and items and all(self._as_decode(*it) for it in items)
+                and sum(n for _, _, n in items) <= self.graph_sizes[-1]):
             return self._prepare_graph(items)
-        pre = [it for it in items if not it[0].is_decode]
-        dec = [it for it in items if it[0].is_decode]
+        pre = [it for it in items if not self._as_decode(*it)]
+        dec = [it for it in items if self._as_decode(*it)]
         ids, pos, slots = [], [], []
         q_lens, ctx, tables = [], [], []
         rows = []
@@ -280,26 +313,35 @@ class ModelRunner:
             ids.extend(d_ids.tolist())
             pos.append(d_pos)
             slots.append(d_slots)
-            for seq, _, _ in dec:
-                rows.append((seq, r))
-                r += 1
-        shared = self._shared_len(tables_d, ctx_d, len(dec)) if dec else 0
+            for seq, start, n in dec:
+                r += n
+                if start + n == seq.length + seq.num_inflight:
+                    rows.append((seq, r - 1))
+        nd = len(ctx_d) if dec else 0
+        shared = self._shared_len(tables_d, ctx_d, nd) if dec else 0
         si = StepInputs(decode_graph=0, ids=np.asarray(ids, dtype=np.int32), positions=np.concatenate(pos),
                         slots=np.concatenate(slots), q_lens=q_lens, ctx_lens=ctx,
                         tables_p=self._bt(tables, max(len(t) for t in tables)) if pre else None,
                         ctx_d=ctx_d, tables_d=tables_d,
-                        num_decode=len(dec), logits_rows=np.asarray([row for _, row in rows], dtype=np.int64),
-                        gather=self._gather(dec, r - len(dec)) if dec else None, shared_len=shared)
+                        num_decode=nd, logits_rows=np.asarray([row for _, row in rows], dtype=np.int64),
+                        gather=self._gather(dec, r - nd) if dec else None, shared_len=shared)
         return si, rows
 
     def _prepare_graph(self, items):
-        B = len(items)
+        """Decode rows (one-token steps and short extend chunks, expanded to causal rows)
+        for the hipGraph of the smallest bucket that holds them; the graph computes every
+        row's logits, the step keeps the rows that end a sequence's new tokens."""
+        B = sum(n for _, _, n in items)
         Bg = self._graph_bucket(B)
         ids, pos, slots, ctx, bt = self._decode_rows(items, self.max_blocks, Bg)
-        rows = [(seq, i) for i, (seq, _, _) in enumerate(items)]
+        rows, r = [], 0
+        for seq, start, n in items:
+            r += n
+            if start + n == seq.length + seq.num_inflight:
+                rows.append((seq, r - 1))
         si = StepInputs(decode_graph=Bg, ids=ids, positions=pos, slots=slots, ctx_d=ctx, tables_d=bt,
-                        num_decode=B, logits_rows=np.arange(B, dtype=np.int64), gather=self._gather(items, 0),
-                        shared_len=self._shared_len(bt, ctx, B))
+                        num_decode=B, logits_rows=np.asarray([row for _, row in rows], dtype=np.int64),
+                        gather=self._gather(items, 0), shared_len=self._shared_len(bt, ctx, B))
         return si, rows
 
     # ----------------------------------------------------------- execution (device)
@@ -418,10 +460,10 @@ class ModelRunner:
         po, pm = self._decode_ws(B)
         # the graph's inputs are slices of ONE device buffer, refilled by one pinned copy per
         # replay: int32 [ids | pos | slots | ctx | block table | shared_len], then room for
-        # the int64 in-flight gather rows (dst, src) of up to B rows
+        # the int64 in-flight gather rows (dst, src) and sampled rows of up to B rows
         nb = self.max_blocks
         n32 = 4 * B + B * nb + 1
-        _, nbytes = _PinnedStager.layout([np.zeros(n32, np.int32), np.zeros(B, np.int64), np.zeros(B, np.int64)])
+        _, nbytes = _PinnedStager.layout([np.zeros(n32, np.int32)] + [np.zeros(B, np.int64)] * 3)
         raw = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
         i32 = raw[: 4 * n32].view(torch.int32)
         st = {
@@ -484,6 +526,10 @@ class ModelRunner:
         arrays = [static]
         if si.gather is not None:
             arrays += [si.gather[0], si.gather[1]]
+        # extend rows: only the last row of each chunk is sampled
+        subset = len(si.logits_rows) != si.num_decode
+        if subset:
+            arrays.append(np.ascontiguousarray(si.logits_rows, dtype=np.int64))
         if self._stager is not None:
             views = self._stager.upload(arrays, dst=st["raw"])
         else:  # pageable copies (LK_PINNED_STAGE=0)
@@ -493,6 +539,8 @@ class ModelRunner:
         if si.gather is not None:
             self._apply_gather(st["ids"], views[1], views[2])
         st["graph"].replay()
+        if subset:
+            return st["logits"].index_select(0, views[-1])
         return st["logits"][: si.num_decode]
 
 

@@ -34,8 +34,18 @@ class ScheduledBatch:
 class Scheduler:
     def __init__(self, allocator, block_size: int, max_num_seqs: int = 256,
                  max_num_batched_tokens: int = 65536, max_model_len: int = 8192, token_align: int = 256,
-                 token_align_wave: int = 0):
+                 token_align_wave: int = 0, prefill_hold: int = 0, hold_min_decode: int = 64,
+                 hold_fill: float = 1.0):
         self.alloc = allocator
+        # prefill hold-back: while at least hold_min_decode decode rows keep the GPU busy, new
+        # prefill waits (up to prefill_hold consecutive steps) until it fills the step's token
+        # budget (hold_fill x max_num_batched_tokens): the prefill GEMMs then run on whole waves
+        # of 256x256 tiles instead of a partial step's 1.3-1.8 waves, and the small remainders
+        # of an admission chunk ride in the next full step instead of a step of their own
+        self.prefill_hold = prefill_hold
+        self.hold_min_decode = hold_min_decode
+        self.hold_fill = hold_fill
+        self._held = 0  # consecutive steps that held prefill back
         # mixed steps: trim prefill chunks so the step's row count is a multiple of the
         # prefill GEMM's 256-row macro tile (a 3852-row step runs 16 row tiles, the 16th
         # nearly empty); the trimmed tokens lead the next step
@@ -97,17 +107,47 @@ class Scheduler:
                 seq.num_cached_prefix = max(seq.num_cached_prefix, seq.num_computed)
 
     # -------------------------------------------------------------- schedule
+    @staticmethod
+    def _generating(seq: Sequence) -> bool:
+        """Decode rows and extend chunks of generated tokens (not prompt prefill)."""
+        return seq.is_decode or (seq.num_computed >= len(seq.prompt_ids) and seq.output_ids)
+
+    def _hold_prefill(self) -> bool:
+        if not self.prefill_hold or self._held >= self.prefill_hold:
+            return False
+        dec = pre = 0
+        for s in self.running:
+            if s.done_after_inflight:
+                continue
+            if self._generating(s):
+                dec += s.pending
+            else:
+                pre += s.pending
+        if dec < self.hold_min_decode or not (pre or self.waiting):
+            return False
+        room = self.max_num_seqs - len(self.running)
+        for k, s in enumerate(self.waiting):
+            if k >= room:
+                break
+            pre += s.length - s.num_computed
+        return dec + pre < self.hold_fill * self.max_tokens
+
     def schedule(self) -> ScheduledBatch:
         batch = ScheduledBatch()
         budget = self.max_tokens
-        # decode first, then in-flight prefill chunks (stable within each class)
-        self.running.sort(key=lambda s: 0 if s.is_decode else 1)
+        # decode first, then extend chunks of generated tokens, then in-flight prefill chunks
+        # (stable within each class)
+        self.running.sort(key=lambda s: 0 if s.is_decode else (1 if self._generating(s) else 2))
+        hold = self._hold_prefill()
+        self._held = self._held + 1 if hold else 0
         i = 0
         while i < len(self.running) and budget > 0:
             seq = self.running[i]
             if seq.done_after_inflight or seq.length + seq.num_inflight >= self.max_model_len:
                 i += 1  # finishes when its in-flight token is collected
                 continue
+            if hold and not self._generating(seq):
+                break  # prefill chunks sort last: all held this step
             n = min(seq.pending, budget)
             if not self._ensure(seq, seq.num_computed + n):
                 victim = self.running.pop()
@@ -118,7 +158,7 @@ class Scheduler:
             batch.items.append((seq, seq.num_computed, n))
             budget -= n
             i += 1
-        while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs:
+        while not hold and self.waiting and budget > 0 and len(self.running) < self.max_num_seqs:
             seq = self.waiting[0]
             if seq.num_inflight:
                 break  # preempted with a token in flight: re-admit once it is collected

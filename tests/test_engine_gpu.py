@@ -138,6 +138,37 @@ def test_cascade_decode_engine_matches_plain(monkeypatch):
     _assert_same_or_near_tie(hf, prompts, run(True, True), ref)
 
 
+@pytest.mark.parametrize("ext_as_decode", [16, 0])
+def test_jump_forward_matches_step_by_step_gpu(monkeypatch, ext_as_decode):
+    """Grammar jump-forward on the GPU path (hipGraph decode + pipelined steps): forced
+    tokens appended by the host and run as extend chunks -- causal paged-decode rows, or a
+    flash-prefill chunk -- give the step-by-step tokens (up to a near-tie: the extend's
+    attention sums in another kernel) in fewer engine steps."""
+    from llm_kubernetes_minikube_sharp4dev_amd.engine import llm_engine, model_runner
+
+    hf, m = _gpu_llama()
+    monkeypatch.setattr(model_runner, "EXTEND_AS_DECODE", ext_as_decode)
+
+    def proc(hist):  # literal runs between free choices, like the tool-call grammar
+        n = len(hist)
+        return [(n * 37 + 11) % 512] if n % 7 in (2, 3, 4) else list(range(1 + (n % 5), 512, 3))
+
+    def run(jf):
+        monkeypatch.setattr(llm_engine, "JUMP_FORWARD", jf)
+        eng = _engine(m, use_graphs=True)
+        eng.runner.capture_all(max_batch=8)
+        seqs = [eng.add_request(p, SamplingParams.greedy(20, logits_processor=proc)) for p in PROMPTS]
+        while eng.has_work():
+            eng.step_pipelined()
+        eng.flush()
+        return seqs
+
+    off, on = run(False), run(True)
+    assert all(s.jumped > 0 for s in on) and all(len(s.output_ids) == 20 for s in on)
+    assert sum(s.steps_run for s in on) < sum(s.steps_run for s in off)
+    _assert_same_or_near_tie(hf, PROMPTS, [s.output_ids for s in on], [s.output_ids for s in off])
+
+
 def test_bert_gpu_matches_hf_fp32():
     cfg = transformers.BertConfig(vocab_size=300, hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
                                   intermediate_size=1024, max_position_embeddings=128, hidden_act="gelu")

@@ -155,12 +155,15 @@ def test_pipelined_steps_match_synchronous():
     assert eng.allocator.usage() == 0.0 or not eng.scheduler.running
 
 
-def test_jump_forward_matches_step_by_step(monkeypatch):
+@pytest.mark.parametrize("ext_as_decode", [16, 0])
+def test_jump_forward_matches_step_by_step(monkeypatch, ext_as_decode):
     """Grammar jump-forward (tokens with a one-id mask appended by the host and run as an
-    extend chunk) gives exactly the step-by-step tokens, synchronous and pipelined, under
-    chunked prefill and preemption, with fewer engine steps per request; the last token
-    of every request is still sampled."""
-    from llm_kubernetes_minikube_sharp4dev_amd.engine import llm_engine
+    extend chunk -- as causal decode rows, or as a prefill chunk) gives exactly the
+    step-by-step tokens, synchronous and pipelined, under chunked prefill and preemption,
+    with fewer engine steps per request; the last token of every request is still sampled."""
+    from llm_kubernetes_minikube_sharp4dev_amd.engine import llm_engine, model_runner
+
+    monkeypatch.setattr(model_runner, "EXTEND_AS_DECODE", ext_as_decode)
 
     m = build_decoder("llama-tiny", dtype=torch.float32)
     V = m.cfg.vocab_size
@@ -195,6 +198,35 @@ def test_jump_forward_matches_step_by_step(monkeypatch):
     s = eng.generate([prompts[2]], SamplingParams.greedy(6, logits_processor=lambda h: [9]))[0]
     assert s.output_ids == [9] * 6 and s.jumped == 4  # first sampled, 4 jumped, last sampled
     assert eng.allocator.usage() == 0.0 or not eng.scheduler.running
+
+
+def test_prefill_hold_back_same_tokens_fuller_steps(monkeypatch):
+    """Prefill hold-back (LK_PREFILL_HOLD): with enough decode rows running, new prompts wait
+    until they fill the step's token budget (or the hold limit expires): same greedy tokens
+    as the eager scheduler, and every step that carries prefill is full unless the hold
+    expired or nothing else was running."""
+    m = build_decoder("llama-tiny", dtype=torch.float32)
+    monkeypatch.setenv("LK_HOLD_MIN_DECODE", "2")
+    prompts = [list(range(3, 3 + n)) for n in (40, 33, 25, 30, 17, 22, 35, 28)]
+
+    def run(hold):
+        eng = _engine(m, max_num_batched_tokens=64, prefill_hold=hold, token_align=0)
+        eng.step_trace = []
+        seqs = [eng.add_request(p, SamplingParams.greedy(12)) for p in prompts[:3]]
+        it = 0
+        while eng.has_work() or len(seqs) < len(prompts):
+            if it % 3 == 2 and len(seqs) < len(prompts):  # arrivals while others decode
+                seqs.append(eng.add_request(prompts[len(seqs)], SamplingParams.greedy(12)))
+            eng.step()
+            it += 1
+        return [s.output_ids for s in seqs], eng.step_trace
+
+    ref, tr0 = run(0)
+    got, tr1 = run(4)
+    assert got == ref
+    part0 = sum(1 for t in tr0 if 0 < t[0] and t[0] + t[1] < 64)
+    part1 = sum(1 for t in tr1 if 0 < t[0] and t[0] + t[1] < 64)
+    assert part1 < part0, (part0, part1)
 
 
 def test_fused_decode_ops_cpu_fallback():
