@@ -293,6 +293,8 @@ bool gemm4w_supported(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t spli
   return lk_gemm4w_supported((int)M, (int)N, (int)K, (int)epi, (int)splits) != 0;
 }
 
+int64_t gemm_streamk(int64_t mode) { return lk_gemm_streamk((int)mode); }
+
 bool gemm_supported(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bn, int64_t splits) {
   return lk_gemm_supported((int)M, (int)N, (int)K, (int)epi, (int)bn, (int)splits) != 0;
 }
@@ -748,6 +750,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, "", py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("epi") = 0,
         py::arg("bn") = 256, py::arg("out") = py::none(), py::arg("variant") = 1,
         py::arg("splits") = 1);
+  m.def("gemm_streamk", &gemm_streamk,
+        "stream-K policy of the prefill GEMM (mode 0 off / 1 on / -1 keep); returns the waits that gave up since the last call",
+        py::arg("mode") = -1);
   m.def("gemm_supported", &gemm_supported, "", py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bn"),
         py::arg("splits") = 1);
   m.def("silu_mul", &silu_mul, "", py::arg("x"), py::arg("out") = py::none());

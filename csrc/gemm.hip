@@ -45,6 +45,8 @@
 //   * tiles are visited in an XCD-aware order (bijective remap, 4 row tiles x all column
 //     tiles per group), so an XCD's ~32 concurrent tiles share their X / W K-slices in L2.
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "common.h"
 #include "kernels.h"
@@ -85,11 +87,29 @@ struct Geo {
 
 // (kernel bodies are __device__ functions: the buffer-resource type exists for the device
 // target only, and a __global__ whose body names it gets no host launch stub)
+// stream-K (hybrid data-parallel + stream-K, persistent grid): the last `tiles` tiles of the
+// tile order are cut into K-iteration units spread evenly over the grid, ipw units per
+// workgroup; a tile's units owned by workgroups b+1, b+2, ... are summed into the fp32 slot of
+// that workgroup (ws + slot * 256 * BN, one slot per workgroup: only its FIRST segment can
+// start mid-tile) and published with a flag; workgroup b, which owns the tile's first units,
+// adds them and runs the epilogue.  The waits only ever point at higher workgroups, which
+// compute those segments first, so a resident finaliser never waits on work queued behind it.
+struct SkArgs {
+  int tiles;      // tiles in the stream-K region (0: every tile data-parallel)
+  int split;      // max workgroups sharing one stream-K tile (per-XCD units derived in the kernel)
+  float* ws;      // [gridDim.x][256 * BN] fp32 partial tiles
+  int* flags;     // [gridDim.x] 0 / 1: partial slot published (reset by its consumer)
+  int* err;       // set when a wait gives up (never expected: a bound instead of a hang)
+};
+enum { SK_FULL = 0, SK_PARTIAL = 1, SK_FINAL = 2 };
+constexpr int kSysCoherent = 1 | 16;  // buffer cache policy sc0 | sc1: past L1 and L2
+
 template <int NF, int EPI, int PH, int PRIO>
 __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W,
                                            const bf16_t* __restrict__ bias, int M, int K, int I,
                                            bf16_t* __restrict__ out, long ldo, int TM, int TN, int group_m,
-                                           int tile) {
+                                           int tile, int kt0, int nk, int kz, int mode, int fin_end,
+                                           const SkArgs& sk) {
   using G = Geo<NF>;
   constexpr int BN = G::BN, NF0 = G::NF0, NF1 = G::NF1;
   static_assert(EPI != EPI_SWIGLU || NF == 4, "SwiGLU pairs fragments n and n+2");
@@ -142,9 +162,7 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)W, (short)0, (int)min((long)(EPI == EPI_SWIGLU ? 2 * I : TN * BN) * K * 2, 0x7FFFFFF0L), 0x00020000);
   const int lr = lane >> 3, lc = lane & 7;
-  // split-K (gridDim.y = splits): this workgroup's K-tiles [kt0, kt0 + nk)
-  const int nkt = K / kBK, kz = blockIdx.y, ks = gridDim.y;
-  const int kt0 = kz * nkt / ks, nk = (kz + 1) * nkt / ks - kt0;
+  // this workgroup's K-tiles [kt0, kt0 + nk) (split-K: gridDim.y ranges; stream-K: units)
   unsigned aoff[2][2], b0off[2], b1off[G::G_B1];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -336,6 +354,63 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
   }
   if (wr == 0) seg_barrier();  // equal barrier counts for both halves
 
+  if (mode != SK_FULL) {
+    // fp32 tile image, fragment-major: element (f, thread) at f * 512 + tid -> coalesced 16-B rows
+    // slot I/O through a buffer descriptor: one per-lane offset VGPR, the fragment offset in an
+    // SGPR (raw pointers would hold a 64-bit address pair per fragment and spill the body)
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    auto slot_rsrc = [&](int b) {
+      return __builtin_amdgcn_make_buffer_rsrc((void*)(sk.ws + (long)b * kBM * BN), (short)0, kBM * BN * 4, 0x00020000);
+    };
+    const int voff = tid * 16;
+    if (mode == SK_PARTIAL) {
+      const __amdgpu_buffer_rsrc_t rs = slot_rsrc(blockIdx.x);
+      // No release / acquire fences: an agent-scope pair costs an L2 write-back / invalidate of
+      // the XCD (every XCD has its own L2), after which the whole grid's operands come from
+      // beyond L2 again (measured: stream-K 0.45-0.9x of the plain tiling that way).  The
+      // partials are written through to memory (sc0 sc1), the stores' acknowledgement awaited,
+      // and the flag published with a relaxed system-scope store; the consumer reads flag and
+      // partials past L1 and L2 -- no cache maintenance at all.
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < NF; ++n)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[m][n]), rs, voff, (m * NF + n) * 8192,
+                                                 kSysCoherent);
+      __builtin_amdgcn_s_waitcnt(0);  // vmcnt / lgkmcnt / expcnt 0: every partial store acknowledged
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(sk.flags + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      // no early return: the row loops below skip every store of a partial segment (a return
+      // here costs the 8-wave body ~40 VGPRs and spills)
+    }
+    const int fin = mode == SK_FINAL ? blockIdx.x + 8 * (fin_end + 1) : 0;  // fin_end contributors, stride 8
+    for (int b = blockIdx.x + 8; b < fin; b += 8) {
+      if (tid == 0) {
+        int spins = 0;
+        while (__hip_atomic_load(sk.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1 << 24)) {  // ~seconds: report instead of hanging the queue
+            __hip_atomic_store(sk.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+      __syncthreads();
+      const __amdgpu_buffer_rsrc_t rs = slot_rsrc(b);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+#pragma unroll
+        for (int n = 0; n < NF; ++n)
+          acc[m][n] += __builtin_bit_cast(
+              floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, (m * NF + n) * 8192, kSysCoherent));
+        __builtin_amdgcn_sched_barrier(0);  // NF loads in flight at a time: no register spike
+      }
+    }
+    __syncthreads();
+    if (tid == 0)
+      for (int b = blockIdx.x + 8; b < fin; b += 8) __hip_atomic_store(sk.flags + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+
   // ---- epilogue: lane holds row (.. + r); fragment pair (2p, 2p+1) gives it the 8 consecutive
   // columns 32p + 8g .. +7 of its wave's 16NF (the pair_col layout); NF = 3's third fragment
   // the 4 columns 32 + 4g .. +3
@@ -352,7 +427,7 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int row = tm * kBM + wr * 128 + m * 16 + r;
-      if (row >= M) continue;
+      if (row >= M || mode == SK_PARTIAL) continue;
       float* prow = part + (long)row * ldo + tn * BN + wc * 16 * NF;
 #pragma unroll
       for (int n = 0; n < NF; ++n) {
@@ -364,7 +439,7 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int row = tm * kBM + wr * 128 + m * 16 + r;
-      if (row >= M) continue;
+      if (row >= M || mode == SK_PARTIAL) continue;
       float y[8];
 #pragma unroll
       for (int h = 0; h < 2; ++h)
@@ -407,7 +482,7 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int row = tm * kBM + wr * 128 + m * 16 + r;
-      if (row >= M) continue;
+      if (row >= M || mode == SK_PARTIAL) continue;
       bf16_t* orow = out + (long)row * ldo + tn * BN + wc * 16 * NF;
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
@@ -463,13 +538,59 @@ template <int NF, int EPI, int PH, int PRIO>
 __global__ __launch_bounds__(512, 1) void gemm_kernel(const bf16_t* __restrict__ X, long ldx,
                                                       const bf16_t* __restrict__ W,
                                                       const bf16_t* __restrict__ bias, int M, int K, int I,
-                                                      bf16_t* __restrict__ out, long ldo, int TM, int TN, int group_m) {
+                                                      bf16_t* __restrict__ out, long ldo, int TM, int TN, int group_m,
+                                                      SkArgs sk) {
   // gridDim.x == TM * TN: one tile per workgroup; fewer: persistent workgroups walking the
   // tiles b, b + grid, ... (same XCD: the grid is a multiple of 8), the epilogue stores of one
   // tile drained before the next tile's LDS-DMA prologue (vmcnt counts stores too)
-  const int nwg = TM * TN;
-  for (int t = blockIdx.x; t < nwg; t += gridDim.x) {
-    gemm8_body<NF, EPI, PH, PRIO>(X, ldx, W, bias, M, K, I, out, ldo, TM, TN, group_m, t);
+  const int nwg = TM * TN, nkt = K / kBK;
+  const int kz = blockIdx.y, ks = gridDim.y;
+  const int kt0 = kz * nkt / ks, nk = (kz + 1) * nkt / ks - kt0;
+  const int ndp = nwg - sk.tiles;
+  // data-parallel tiles first, then this workgroup's stream-K units -- ONE body call site (two
+  // inlined copies of the 8-wave body do not fit the register file).  The stream-K tiles stay
+  // on the XCD their data-parallel neighbours run on: XCD x (= blockIdx.x % 8) owns the
+  // region's tiles with hardware ids ndp + x + 8 j (the tail of its XCD-contiguous chunk of the
+  // tile order, so they share X rows / W columns in its L2), and its gridDim.x / 8 workgroups
+  // split those tiles' K units evenly; a finaliser's contributors are the next workgroups of
+  // the same XCD (blockIdx.x + 8, + 16, ...).  (Spreading the units over the whole grid
+  // without this ran 0.5-0.8x of the plain tiling: every tile's operands came from beyond L2.)
+  constexpr int NX = 8;
+  const int xcd = blockIdx.x % NX, li = blockIdx.x / NX, P = gridDim.x / NX;
+  const int cx = sk.tiles > xcd ? (sk.tiles - xcd + NX - 1) / NX : 0;
+  // at most sk.split workgroups per tile: a tile cut finer costs its finaliser more partial
+  // reads than the balance gains (K 4096 remainders cut 16 ways ran 0.7x); the rest idle
+  const int psk = min(P, cx * sk.split);
+  const long units = (long)cx * nkt;
+  const int ipw = cx ? (int)((units + psk - 1) / psk) : 0;
+  int t = blockIdx.x;
+  long u = (long)li * ipw;
+  const long end = (cx && li < psk) ? min(units, u + ipw) : 0;
+  while (true) {
+    int tile, a0, n, mode, fin_end = 0;
+    if (t < ndp) {
+      tile = t;
+      a0 = kt0;
+      n = nk;
+      mode = SK_FULL;
+      t += gridDim.x;
+    } else if (u < end) {
+      const int j = (int)(u / nkt), k0 = (int)(u % nkt);
+      const int k1 = (int)min((long)nkt, k0 + (end - u));
+      mode = (k0 == 0 && k1 == nkt) ? SK_FULL : (k0 != 0 ? SK_PARTIAL : SK_FINAL);
+      // a finaliser's contributors: this XCD's workgroups whose ranges start inside the tile's
+      // tail: fin_end of them, local indices li + 1 .. li + fin_end
+      const long tile_end = (long)(j + 1) * nkt;
+      fin_end = (int)min((long)psk, (tile_end + ipw - 1) / ipw) - li - 1;
+      tile = ndp + xcd + NX * j;
+      a0 = k0;
+      n = k1 - k0;
+      u += n;
+    } else {
+      break;
+    }
+    gemm8_body<NF, EPI, PH, PRIO>(X, ldx, W, bias, M, K, I, out, ldo, TM, TN, group_m, tile, a0, n, kz, mode, fin_end,
+                                  sk);
     wait_vm<0>();
   }
 }
@@ -497,6 +618,85 @@ int group_rows() {
   return g;
 }
 
+int cu_count() {
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
+
+// stream-K policy (LK_GEMM_STREAMK=0 disables): a grid whose last wave of tiles would leave
+// CUs idle -- tiles % CUs in (0, 0.85 x CUs) -- runs persistent with that remainder spread as
+// K units over every CU.  Not inside a hipGraph capture (the per-stream workspace is
+// allocated and zeroed on first use, outside any capture).
+int g_streamk = -1;
+long g_sk_launches = 0;  // stream-K grids launched (tests: the policy really engaged)
+struct SkWs {
+  float* ws = nullptr;
+  int* flags = nullptr;
+  int* err = nullptr;
+  long ws_floats = 0;
+  int slots = 0;
+};
+
+std::mutex g_sk_mu;
+std::map<hipStream_t, SkWs> g_sk_pool;
+
+bool sk_plan(int M, int tiles, int nkt, int bn, hipStream_t st, SkArgs* sk, int* grid) {
+  if (g_streamk < 0) {
+    const char* e = getenv("LK_GEMM_STREAMK");
+    g_streamk = e ? atoi(e) : 1;
+  }
+  // prefill-sized GEMMs only (M >= 1024): the small side-stream GEMMs (query encodes) never
+  // share the CUs with a second persistent stream-K grid
+  if (!g_streamk || nkt < 4 || M < 1024) return false;
+  static const int grid_cap = [] {  // LK_GEMM_SK_GRID: persistent grid size override (probes)
+    const char* e = getenv("LK_GEMM_SK_GRID");
+    return e ? atoi(e) : 0;
+  }();
+  const int G = grid_cap > 0 ? min(grid_cap, cu_count()) : cu_count();
+  if (G % 8) return false;  // the kernel splits the grid into 8 XCD groups
+  // only a short tail after at least one whole wave: a large remainder cut into K units breaks
+  // the lockstep K walk that lets an XCD's tiles share K-slices in its L2 (measured: all-stream-K
+  // grids of 144-208 tiles ran 0.55-0.7x of the plain partial wave, which is already ~0.95x
+  // efficient per tile); a tail of <= half a wave after whole waves is what it fixes (K 14336
+  // down projection at 272-336 tiles: 1.10-1.20x)
+  const int rem = tiles % G;
+  if (rem == 0 || tiles < G || 2 * rem > G) return false;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+  std::lock_guard<std::mutex> lock(g_sk_mu);
+  SkWs& w = g_sk_pool[st];
+  const long need = (long)G * kBM * bn;
+  if (w.ws_floats < need || w.slots < G) {
+    if (hipStreamSynchronize(st) != hipSuccess) return false;
+    if (w.ws) (void)hipFree(w.ws);
+    if (w.flags) (void)hipFree(w.flags);
+    w = SkWs{};
+    if (hipMalloc(&w.ws, need * sizeof(float)) != hipSuccess) return false;
+    if (hipMalloc(&w.flags, (G + 1) * sizeof(int)) != hipSuccess) return false;
+    if (hipMemset(w.flags, 0, (G + 1) * sizeof(int)) != hipSuccess) return false;
+    w.err = w.flags + G;
+    w.ws_floats = need;
+    w.slots = G;
+  }
+  static const int split = [] {  // LK_GEMM_SK_SPLIT: max workgroups per stream-K tile
+    const char* e = getenv("LK_GEMM_SK_SPLIT");
+    const int v = e ? atoi(e) : 4;
+    return v >= 1 ? v : 4;
+  }();
+  ++g_sk_launches;
+  sk->tiles = rem;
+  sk->split = split;
+  sk->ws = w.ws;
+  sk->flags = w.flags;
+  sk->err = w.err;
+  *grid = G;
+  return true;
+}
+
 template <int NF, int EPI, int PH, int PRIO = 0>
 void launch_ph(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
                long ldo, int TM, int TN, int ks, hipStream_t st) {
@@ -507,8 +707,11 @@ void launch_ph(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, i
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  gemm_kernel<NF, EPI, PH, PRIO><<<dim3(gemm_grid(TM * TN), ks), 512, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo,
-                                                                              TM, TN, group_rows());
+  SkArgs sk{0, 0, nullptr, nullptr, nullptr};
+  int grid = gemm_grid(TM * TN);
+  if (ks == 1 && EPI != EPI_PARTIAL) sk_plan(M, TM * TN, K / kBK, 64 * NF, st, &sk, &grid);
+  gemm_kernel<NF, EPI, PH, PRIO><<<dim3(grid, ks), 512, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN,
+                                                                   group_rows(), sk);
 }
 // schedule: 0 = 4 phases per K-tile (per-cluster priority), 1 = 2 phases (static priority)
 template <int NF, int EPI>
@@ -561,6 +764,23 @@ int dispatch(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int
 }
 
 }  // namespace
+
+// stream-K waits that gave up since the last call (0 expected), over every stream's workspace;
+// mode >= 0 sets the policy (0 off, 1 on), -1 leaves it; -2 returns the stream-K launches so far
+int lk_gemm_streamk(int mode) {
+  if (mode == -2) return (int)g_sk_launches;
+  if (mode >= 0) g_streamk = mode;
+  std::lock_guard<std::mutex> lock(g_sk_mu);
+  int errs = 0;
+  for (auto& kv : g_sk_pool) {
+    int e = 0;
+    if (kv.second.err && hipMemcpy(&e, kv.second.err, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess && e) {
+      errs += e;
+      (void)hipMemset(kv.second.err, 0, sizeof(int));
+    }
+  }
+  return errs;
+}
 
 int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks) {
   if (M < 1 || K < kBK || K % kBK || (bn != 192 && bn != 256)) return 0;

@@ -60,6 +60,7 @@ int lk_xgmi_allreduce(bf16_t* const* data, unsigned* const* sig, int rank, int w
 // ks > 1: split-K over ks K-ranges, fp32 partials in ws [ks, M, N], then a reduce applies the
 // epilogue (not SwiGLU) -- for shapes with fewer tiles than CUs
 int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks = 1);
+int lk_gemm_streamk(int mode);
 int lk_gemm4w_supported(int M, int N, int K, int epi, int ks);
 int lk_gemm4w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi,
               bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, int variant = 0);

@@ -528,6 +528,65 @@ def test_gemm4w_splitk(hip, MNK, splits, epi):
                    f"gemm4w v{v} split{splits} epi{epi} M{M} N{N} K{K}")
 
 
+@pytest.mark.parametrize("MNKE", [(4352, 4096, 4096, 0), (4300, 6144, 4096, 0), (4352, 28672, 4096, 1),
+                                  (5000, 3072, 768, 3), (4864, 4096, 14336, 0), (1536, 4096, 4096, 2),
+                                  (5376, 4096, 14336, 2)])
+def test_gemm_streamk(hip, MNKE):
+    """Hybrid stream-K (persistent grid: whole waves of tiles data-parallel, a short last wave
+    cut into K units over up to 4 workgroups per tile on the tile's XCD, fp32 partial tiles
+    summed by the owner of each tile's first units) vs the plain tiling and the fp32
+    reference, every epilogue and M tails; no wait ever gives up."""
+    M, N, K, epi = MNKE
+    torch.manual_seed(M + N + K + epi)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16) if epi >= 2 else None
+    y = x.float() @ w.float().t()
+    if epi == 1:
+        y = ref.silu_mul(y.to(torch.bfloat16)).float()
+    elif epi >= 2:
+        y = (y + b.float()).to(torch.bfloat16).float()
+        y = torch.nn.functional.gelu(y) if epi == 3 else y
+    hip.gemm_streamk(0)
+    ran = 0
+    try:
+        for sched, bn in GEMM_CFGS:
+            if not hip.gemm_supported(M, N, K, epi, bn):
+                continue
+            hip.gemm_streamk(0)
+            plain = hip.gemm(x, w, b, epi, bn, None, sched)
+            hip.gemm_streamk(1)
+            n0 = hip.gemm_streamk(-2)
+            sk = hip.gemm(x, w, b, epi, bn, None, sched)
+            engaged = hip.gemm_streamk(-2) > n0
+            sk2 = hip.gemm(x, w, b, epi, bn, None, sched)  # flags reset by the consumers
+            torch.cuda.synchronize()
+            assert hip.gemm_streamk(-1) == 0, "a stream-K wait gave up"
+            _close(sk, y, 0.03, 0.01, f"streamk epi{epi} s{sched}/{bn} M{M} N{N} K{K}")
+            assert torch.equal(sk, sk2), "stream-K not deterministic"
+            _close(sk, plain.float(), 0.02, 0.01, "streamk vs plain")
+            ran += engaged
+        assert ran or M < 2048, "no configuration engaged stream-K"
+    finally:
+        hip.gemm_streamk(1)
+
+
+def test_gemm_streamk_layout(hip):
+    """A = I with an asymmetric B on a stream-K grid (17 x 16 tiles: one whole wave, then 16
+    tiles each cut over 4 workgroups): catches a misplaced partial tile or a wrong owner."""
+    M, N, K = 4352, 4096, 512
+    x = torch.eye(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K) % 97 - 48).to(torch.bfloat16)
+    exp = torch.zeros(M, N)
+    exp[:K] = w.float().t().cpu()
+    hip.gemm_streamk(1)
+    n0 = hip.gemm_streamk(-2)
+    for sched in (0, 1, 2):
+        assert torch.equal(hip.gemm(x, w, None, 0, 256, None, sched).float().cpu(), exp), sched
+    assert hip.gemm_streamk(-2) == n0 + 3, "the stream-K grid did not engage"
+    assert hip.gemm_streamk(-1) == 0
+
+
 def test_gemm_splitk_dispatch(hip):
     """ops.gemm picks split-K for the low-tile-count shapes and stays on one pass elsewhere."""
     assert ops._gemm_default(2048, 4096, 4096, 0)[2] == 2
