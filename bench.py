@@ -249,12 +249,14 @@ def main():
     sync()
     log(rank, f"{args.model} random-init (tp={args.tp}{f', tp-sim {args.tp_sim}' if args.tp_sim > 1 else ''}) "
               f"in {time.perf_counter() - t0:.1f}s")
-    # continuous: 8k-token steps (whole waves of 256x256 tiles on every projection: 6144-row
-    # steps measured 4 % slower) -- on MI355X 8192-token steps with admission chunks of 16
-    # beat 4096 / 8 by 2 % in q/s and p50 on the same box (profiles/r2_sched_sweep.md)
-    # (scaled with the in-flight count: 64 tokens per request in flight, e.g. 4096 at 64 for
-    # the 70B config, where 8192-token steps measured 9 % slower)
-    mbt = args.max_batched_tokens or (min(8192, 64 * max(args.batch, 32)) if args.mode == "continuous" else 65536)
+    # continuous: 4096-token steps.  Round 2 (step-by-step decoding) measured 8192-token steps
+    # 2 % ahead of 4096 (profiles/r2_sched_sweep.md); with grammar jump-forward requests finish
+    # in 22 % fewer steps, admissions arrive in smaller pieces, and 4096-token steps -- prefill
+    # spread over more steps, fewer decode-only weight-streaming steps -- read 98.85 / 100.15
+    # q/s vs 98.27 / 98.63 at 8192 and 93.7 at 3072 on one box (profiles/r3_mbt/); scaled with
+    # the in-flight count below 64 requests (4096 at 64 for the 70B config, where 8192-token
+    # steps measured 9 % slower)
+    mbt = args.max_batched_tokens or (min(4096, 64 * max(args.batch, 32)) if args.mode == "continuous" else 65536)
     runner_kw = dict(block_size=16, max_model_len=8192, max_num_seqs=max(args.batch, 64), kv_cache_gb=args.kv_gb,
                      use_graphs=on_gpu and not args.no_graphs)
     if not on_gpu:
