@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--max-batched-tokens", type=int, default=None,
                     help="token budget per engine step (default: continuous 64 x --batch capped at 8192, "
                          "batch mode 65536)")
+    ap.add_argument("--free-pods", action="store_true",
+                    help="round-2 tool-call grammar: pod names free-form, deployment names not tied to the "
+                         "chosen namespace (more requests end in the reference's 404 -> 500 branch)")
     ap.add_argument("--admit-chunk", type=int, default=None,
                     help="continuous mode: requests retrieved + admitted together (batched embed/kNN); "
                          "default --batch / 8")
@@ -272,11 +275,23 @@ def main():
     if args.constrained:
         from llm_kubernetes_minikube_sharp4dev_amd.engine.constrained import tool_call_processor
 
-        # namespaces from the RAG allowlist, deployment names from the (fake) cluster,
-        # pod names free-form (<= 16 chars) -- keeps a call within --max-new-tokens
-        params.logits_processor = tool_call_processor(
-            tok, max_str=16, enums={"namespace": list(cfg.agent.allowed_namespaces) + ["default"],
-                                    "name": ["echoserver", "api", "web", "worker"]})
+        # namespaces from the RAG allowlist; deployment and pod names those of the chosen
+        # namespace in the (fake) cluster, as a model reading the cluster context would pick them
+        # (round 2 let pod names run free: 17 % of requests then ended in the reference's
+        # get_logs 500 branch on invented pods); other strings free-form (<= 16 chars)
+        from llm_kubernetes_minikube_sharp4dev_amd.k8s.fake import FakeCluster as _FC
+
+        snap, by_ns = _FC.default(), {}
+        for (ns, pod) in sorted(snap.pods):
+            by_ns.setdefault(ns, {"pod": [], "name": []})["pod"].append(pod)
+        for (ns, dep) in sorted(snap.deployments):
+            by_ns.setdefault(ns, {"pod": [], "name": []})["name"].append(dep)
+        enums = {"namespace": list(cfg.agent.allowed_namespaces) + ["default"]}
+        for field in ("pod", "name"):
+            enums[field] = {"__by__": "namespace", **{ns: v[field] for ns, v in by_ns.items()}}
+        if args.free_pods:  # round-2 grammar: deployment names from a flat list, pods free-form
+            enums = {"namespace": enums["namespace"], "name": ["echoserver", "api", "web", "worker"]}
+        params.logits_processor = tool_call_processor(tok, max_str=16, enums=enums)
     results, trace, elapsed, tim_setup = [], [], 0.0, 0.0
     load, load_host, tp_ctrl, prompt_len = None, {}, {}, {}
 

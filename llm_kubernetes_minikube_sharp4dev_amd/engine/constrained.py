@@ -217,8 +217,9 @@ class ToolCallGrammar:
         self.tok = tok
         self.tools = tools or TOOL_FIELDS
         self.max_str = max_str
-        # field name -> allowed string values (e.g. namespace -> the RAG allowlist)
-        self.enums = {k: list(v) for k, v in (enums or {}).items()}
+        # field name -> allowed string values (e.g. namespace -> the RAG allowlist), or a dict
+        # {"__by__": earlier field, value of that field: [values]} (e.g. pod names per namespace)
+        self.enums = {k: (dict(v) if isinstance(v, dict) else list(v)) for k, v in (enums or {}).items()}
         self.tt = _TokenTable.get(tok)
         texts = self.tt.texts
         self.name_tokens = [i for i, t in enumerate(texts) if t and set(t) <= K8S_CHARS]
@@ -262,6 +263,15 @@ class ToolCallGrammar:
             if len(self._free_cache) < 8192:
                 self._free_cache[key] = c
         return c
+
+    def _enum_values(self, name: str, before: str) -> list:
+        """Allowed values of enum field ``name``; a per-key dict picks the list of the value
+        the object already gave its ``__by__`` field (no list for it: no valid value)."""
+        vals = self.enums[name]
+        if not isinstance(vals, dict):
+            return vals
+        m = re.search(r'"%s":"([^"]*)"' % re.escape(vals.get("__by__", "")), before)
+        return list(vals.get(m.group(1), ())) if m else []
 
     def _literal_tokens(self, rest: str) -> list:
         """Tokens for a forced literal: those spelling the LONGEST prefix of ``rest`` the
@@ -352,7 +362,7 @@ class ToolCallGrammar:
                     return self.tt.eos or [0]
                 pos += len(lit)
             elif step[0] == "enum":
-                vals = self.enums[step[1]]
+                vals = self._enum_values(step[1], s[:pos])
                 seg = s[pos:]
                 q2 = seg.find('"')
                 if q2 < 0:  # still choosing the value

@@ -110,3 +110,30 @@ def test_tool_call_grammar_incremental_text_matches_full_decode():
             ref._texts = {}  # no text cache: the full-decode path
             assert list(allowed) == list(ref(list(ids)))
             ids.append(rng.choice(list(allowed)))
+
+
+def test_tool_call_grammar_enum_keyed_by_earlier_field():
+    """An enum given as {"__by__": field, value: [...]} allows only the values listed for the
+    value the object already chose for that field (pods of the chosen namespace); random
+    walks always end in an existing (namespace, pod) / (namespace, deployment) pair."""
+    tok = builtin_tokenizer()
+    pods = {"dev": ["api-1", "api-2"], "staging": ["web-7"]}
+    deps = {"dev": ["api"], "staging": ["web"]}
+    g = ToolCallGrammar(tok, max_str=16, enums={"namespace": ["dev", "staging"],
+                                                 "pod": {"__by__": "namespace", **pods},
+                                                 "name": {"__by__": "namespace", **deps}})
+    rng = random.Random(3)
+    seen = set()
+    for _ in range(150):
+        ids = []
+        for _ in range(48):
+            a = g(ids)
+            ids.append(rng.choice(a))
+        obj = json.loads(tok.decode([i for i in ids if i not in tok.eos_ids]))
+        if obj["action"] == "get_logs":
+            assert obj["pod"] in pods[obj["namespace"]], obj
+            seen.add("get_logs")
+        if obj["action"] == "scale_deployment":
+            assert obj["name"] in deps[obj["namespace"]], obj
+            seen.add("scale")
+    assert seen == {"get_logs", "scale"}
