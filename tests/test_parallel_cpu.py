@@ -55,8 +55,12 @@ def _hf(arch):
 PROMPTS = [[5, 17, 99, 3, 250, 7, 7, 1, 400, 33, 21, 8, 2, 9, 11, 60, 61, 62, 63], [7, 8, 9], list(range(10, 60))]
 
 
-def _proc(hist):  # history-dependent constraint: non-greedy path (driver-side sampling)
-    return list(range(1 + (len(hist) % 5), 512, 3))
+def _proc(hist):  # history-dependent constraint: non-greedy path (driver-side sampling), with
+    # one-choice runs so grammar jump-forward sends extend chunks through the TP step messages
+    n = len(hist)
+    if n % 7 in (2, 3):
+        return [(n * 37 + 11) % 512]
+    return list(range(1 + (n % 5), 512, 3))
 
 
 def _drive(eng, pipelined: bool, constrained: bool):
@@ -300,25 +304,29 @@ def _ctrl_timing_worker(rank, world, port, out_path):
 
     ctrl = _Ctrl(TPGroup(rank, world, dist.group.WORLD))
     si = _rand_step()
-    n = 300
+    n, trials = 100, 3  # best of 3 windows: a loaded CI host (pytest -n) preempts the spinning ranks
     if rank == 0:
         for _ in range(20):
             ctrl.send("step", si)
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(n):
-            ctrl.send("step", si)
-        dist.barrier()
-        torch.save((time.perf_counter() - t0) / n, out_path)
+        best = float("inf")
+        for _ in range(trials):
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(n):
+                ctrl.send("step", si)
+            dist.barrier()
+            best = min(best, (time.perf_counter() - t0) / n)
+        torch.save(best, out_path)
         ctrl.send("stop")
     else:
         for _ in range(20):
             ctrl.recv()
-        dist.barrier()
-        for _ in range(n):
-            cmd, got = ctrl.recv()
-            assert cmd == "step" and got.num_decode == 128
-        dist.barrier()
+        for _ in range(trials):
+            dist.barrier()
+            for _ in range(n):
+                cmd, got = ctrl.recv()
+                assert cmd == "step" and got.num_decode == 128
+            dist.barrier()
         assert ctrl.recv()[0] == "stop"
     dist.destroy_process_group()
 
