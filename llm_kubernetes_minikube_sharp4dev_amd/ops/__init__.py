@@ -91,11 +91,17 @@ def kv_write(k, v, k_cache, v_cache, slots):
     return ref.kv_write(k, v, k_cache, v_cache, slots)
 
 
+# keys per decode workgroup once the batch alone fills the CUs (B * Hkv >= 512); LK_DECODE_SPLIT
+# overrides it (A/B knob: three 256-thread workgroups per CU make 768 slots, so ~1.1-1.5 rounds
+# of unsplit workgroups at the serving batch leave part of the last round idle)
+DECODE_SPLIT_LARGE = int(os.environ.get("LK_DECODE_SPLIT", "1024"))
+
+
 def decode_split_size(B: int, Hkv: int) -> int:
     """Keys per decode workgroup (mirrors lk_decode_split_size): small batches split the
     context finer so 256 CUs stay busy; static per (B, Hkv) for hipGraph capture."""
     bh = B * Hkv
-    return 1024 if bh >= 512 else 512 if bh >= 128 else 256 if bh >= 32 else 128
+    return DECODE_SPLIT_LARGE if bh >= 512 else 512 if bh >= 128 else 256 if bh >= 32 else 128
 
 
 def decode_splits(max_context: int, split: int) -> int:
