@@ -649,9 +649,11 @@ bool sk_plan(int M, int tiles, int nkt, int bn, hipStream_t st, SkArgs* sk, int*
     const char* e = getenv("LK_GEMM_STREAMK");
     g_streamk = e ? atoi(e) : 1;
   }
-  // prefill-sized GEMMs only (M >= 1024): the small side-stream GEMMs (query encodes) never
-  // share the CUs with a second persistent stream-K grid
-  if (!g_streamk || nkt < 4 || M < 1024) return false;
+  // decoder prefill GEMMs only (M >= 1024, K >= 4096): the encoder GEMMs (K 768 / 3072) that
+  // run on side streams (query encodes next to the engine's steps) never put a second
+  // persistent stream-K grid on the CUs -- two such grids whose waiting workgroups filled an
+  // XCD could each wait for a workgroup that cannot be dispatched
+  if (!g_streamk || nkt < 64 || M < 1024) return false;
   static const int grid_cap = [] {  // LK_GEMM_SK_GRID: persistent grid size override (probes)
     const char* e = getenv("LK_GEMM_SK_GRID");
     return e ? atoi(e) : 0;

@@ -529,7 +529,7 @@ def test_gemm4w_splitk(hip, MNK, splits, epi):
 
 
 @pytest.mark.parametrize("MNKE", [(4352, 4096, 4096, 0), (4300, 6144, 4096, 0), (4352, 28672, 4096, 1),
-                                  (5000, 3072, 768, 3), (4864, 4096, 14336, 0), (1536, 4096, 4096, 2),
+                                  (5000, 3072, 4096, 3), (4864, 4096, 14336, 0), (1536, 4096, 4096, 2),
                                   (5376, 4096, 14336, 2)])
 def test_gemm_streamk(hip, MNKE):
     """Hybrid stream-K (persistent grid: whole waves of tiles data-parallel, a short last wave
