@@ -574,7 +574,7 @@ def test_gemm_streamk(hip, MNKE):
 def test_gemm_streamk_layout(hip):
     """A = I with an asymmetric B on a stream-K grid (17 x 16 tiles: one whole wave, then 16
     tiles each cut over 4 workgroups): catches a misplaced partial tile or a wrong owner."""
-    M, N, K = 4352, 4096, 512
+    M, N, K = 4352, 4096, 4096
     x = torch.eye(M, K, device=DEV, dtype=torch.bfloat16)
     w = (torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K) % 97 - 48).to(torch.bfloat16)
     exp = torch.zeros(M, N)
