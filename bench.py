@@ -259,7 +259,11 @@ def main():
     # q/s vs 98.27 / 98.63 at 8192 and 93.7 at 3072 on one box (profiles/r3_mbt/); scaled with
     # the in-flight count below 64 requests (4096 at 64 for the 70B config, where 8192-token
     # steps measured 9 % slower)
-    mbt = args.max_batched_tokens or (min(4096, 64 * max(args.batch, 32)) if args.mode == "continuous" else 65536)
+    # Long-evidence prompts (~2.4k uncached tokens) queue behind a 4096-token budget (31 steps
+    # queued per request): 8192 read 33.0 vs 32.2 q/s there, while the mixed agent + RAG
+    # workload keeps 4096 (148.1 vs 143.3; profiles/r3_budget_wl/)
+    cap = 8192 if args.long_evidence else 4096
+    mbt = args.max_batched_tokens or (min(cap, 64 * max(args.batch, 32)) if args.mode == "continuous" else 65536)
     runner_kw = dict(block_size=16, max_model_len=8192, max_num_seqs=max(args.batch, 64), kv_cache_gb=args.kv_gb,
                      use_graphs=on_gpu and not args.no_graphs)
     if not on_gpu:
