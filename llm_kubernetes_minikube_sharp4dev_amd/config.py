@@ -87,7 +87,10 @@ class EngineConfig:
     gpu_memory_fraction: float = 0.85                  # of the 288 GB HBM3E
     kv_cache_gb: Optional[float] = None                # explicit KV budget (overrides the fraction)
     max_num_seqs: int = 256
-    max_num_batched_tokens: int = 8192                 # per step: whole waves of 256x256 GEMM tiles (profiles/r2_sched_sweep.md)
+    # per step: whole waves of 256x256 GEMM tiles (profiles/r2_sched_sweep.md).  The .NET-facing
+    # server path samples with Ollama's defaults (no grammar, so no jump-forward): round 2's
+    # 8192 stays; the grammar-constrained bench runs 4096 (profiles/r3_mbt/)
+    max_num_batched_tokens: int = 8192
     max_model_len: int = 8192
     enable_prefix_caching: bool = True
     use_hip_graphs: bool = True
