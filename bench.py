@@ -371,12 +371,19 @@ def main():
 
             prof = cProfile.Profile()
             prof.enable()
+        # LK_TRACE_WINDOW=1: marker kernels at both ends of the timed window, so a kernel trace
+        # is summarised over exactly the timed steps (scripts/summarize_trace.py --window)
+        mark = on_gpu and os.environ.get("LK_TRACE_WINDOW", "0") == "1"
+        if mark:
+            _ext.lib().window_mark(1)
         t0 = time.perf_counter()
         if load is not None:
             results.extend(load.run(args.steps * args.batch))
         else:
             for _ in range(args.steps):
                 results.extend(batch_step())
+        if mark:
+            _ext.lib().window_mark(2)
         sync()
         if world > 1:
             tp_barrier(engine)

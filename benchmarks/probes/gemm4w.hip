@@ -1,4 +1,7 @@
 // K2, prefill / encoder regime, one-wave-per-SIMD variant: Y[M, N] = epilogue(X[M, K] . W[N, K]^T).
+// NOT BUILT: the round-3 one-wave-per-SIMD prefill GEMM, kept as a measured probe (it lost
+// 6-12 % to csrc/gemm.hip on the served shapes, profiles/r3_gemm_4wave/README.md).  Moved out of
+// the _C extension in round 4; build it by hand next to csrc/common.h for loop ablations.
 //
 // Why a second prefill kernel: the 8-wave ping-pong of gemm.hip keeps two waves per SIMD and
 // pays for it in barrier waits (PMC, profiles/r2_gemm.md: SQ_WAIT_ANY 176.7 M vs the library's

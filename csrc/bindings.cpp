@@ -261,37 +261,6 @@ at::Tensor gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at
   return out;
 }
 
-// One-wave-per-SIMD 256 x 256 variant (csrc/gemm4w.hip), same contract as gemm() with bn = 256.
-at::Tensor gemm4w(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t epi,
-                  const c10::optional<at::Tensor>& out_, int64_t splits, int64_t variant) {
-  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_LASTDIM(x); CHECK_CONTIG(w);
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "x [M,K], w [N,K]");
-  check_rows16(x, "x"); check_rows16(w, "w");
-  const int M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(lk_gemm4w_supported(M, N, K, (int)epi, (int)splits), "gemm4w: unsupported shape M", M, " N", N, " K", K,
-              " epi", epi, " splits", splits);
-  if (epi >= 2) {
-    TORCH_CHECK(bias.has_value(), "gemm4w: this epilogue needs a bias");
-    CHECK_CUDA(*bias); CHECK_BF16(*bias); CHECK_CONTIG(*bias);
-    TORCH_CHECK(bias->numel() == N && reinterpret_cast<uintptr_t>(bias->data_ptr()) % 16 == 0, "gemm4w: bias [N], 16-B aligned");
-  }
-  const int n_out = epi == 1 ? N / 2 : N;
-  at::Tensor out = out_ ? *out_ : at::empty({M, n_out}, x.options());
-  CHECK_BF16(out); CHECK_LASTDIM(out);
-  TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == n_out, "out shape");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0 && out.stride(0) % 8 == 0, "out alignment (16 B)");
-  at::Tensor ws;
-  if (splits > 1) ws = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
-  int rc = lk_gemm4w(bp(x), x.stride(0), bp(w), epi >= 2 ? bp(*bias) : nullptr, M, N, K, (int)epi, bp(out),
-                     out.stride(0), cur_stream(), (int)splits, splits > 1 ? ws.data_ptr<float>() : nullptr,
-                     (int)variant);
-  CHECK_RC(rc, "gemm4w");
-  return out;
-}
-
-bool gemm4w_supported(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t splits) {
-  return lk_gemm4w_supported((int)M, (int)N, (int)K, (int)epi, (int)splits) != 0;
-}
 
 int64_t gemm_streamk(int64_t mode) { return lk_gemm_streamk((int)mode); }
 
@@ -722,6 +691,7 @@ struct XgmiAr {
 extern "C" const char lk_source_stamp[];
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("window_mark", [](int64_t id) { CHECK_RC(lk_window_mark((int)id, cur_stream()), "window_mark"); });
   m.def("source_stamp", [] { return std::string(lk_source_stamp + 8); });
   py::class_<XgmiAr>(m, "XgmiAr")
       .def(py::init<int, int, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("bytes"))
@@ -743,10 +713,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ws_linear", &ws_linear, "", py::arg("x"), py::arg("w"), py::arg("swiglu") = false, py::arg("bn") = 0,
         py::arg("splits") = 0, py::arg("out") = py::none());
   m.def("ws_plan", &ws_plan);
-  m.def("gemm4w", &gemm4w, "", py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("epi") = 0,
-        py::arg("out") = py::none(), py::arg("splits") = 1, py::arg("variant") = 0);
-  m.def("gemm4w_supported", &gemm4w_supported, "", py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"),
-        py::arg("splits") = 1);
   m.def("gemm", &gemm, "", py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("epi") = 0,
         py::arg("bn") = 256, py::arg("out") = py::none(), py::arg("variant") = 1,
         py::arg("splits") = 1);

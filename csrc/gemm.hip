@@ -98,8 +98,11 @@ struct SkArgs {
   int tiles;      // tiles in the stream-K region (0: every tile data-parallel)
   int split;      // max workgroups sharing one stream-K tile (per-XCD units derived in the kernel)
   float* ws;      // [gridDim.x][256 * BN] fp32 partial tiles
-  int* flags;     // [gridDim.x] 0 / 1: partial slot published (reset by its consumer)
+  int* flags;     // [gridDim.x] the launch epoch once the slot's partial is published
   int* err;       // set when a wait gives up (never expected: a bound instead of a hang)
+  int epoch;      // this launch's publish value (per-stream counter, never 0): a flag left by
+                  // a contributor that published after its finaliser gave up can never
+                  // satisfy a later launch's wait
 };
 enum { SK_FULL = 0, SK_PARTIAL = 1, SK_FINAL = 2 };
 constexpr int kSysCoherent = 1 | 16;  // buffer cache policy sc0 | sc1: past L1 and L2
@@ -379,23 +382,30 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
                                                  kSysCoherent);
       __builtin_amdgcn_s_waitcnt(0);  // vmcnt / lgkmcnt / expcnt 0: every partial store acknowledged
       __syncthreads();
-      if (tid == 0) __hip_atomic_store(sk.flags + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (tid == 0) __hip_atomic_store(sk.flags + blockIdx.x, sk.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       // no early return: the row loops below skip every store of a partial segment (a return
       // here costs the 8-wave body ~40 VGPRs and spills)
     }
     const int fin = mode == SK_FINAL ? blockIdx.x + 8 * (fin_end + 1) : 0;  // fin_end contributors, stride 8
+    // a wait that gives up poisons the tile (NaN) instead of adding a slot that was never
+    // published: wrong output must not pass silently (the engine also polls sk.err)
+    int* bad = reinterpret_cast<int*>(smem);  // the staging LDS is dead after the K loop
+    bool poisoned = false;
     for (int b = blockIdx.x + 8; b < fin; b += 8) {
       if (tid == 0) {
-        int spins = 0;
-        while (__hip_atomic_load(sk.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
+        int spins = 0, gave_up = 0;
+        while (__hip_atomic_load(sk.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != sk.epoch) {
           __builtin_amdgcn_s_sleep(2);
           if (++spins > (1 << 24)) {  // ~seconds: report instead of hanging the queue
             __hip_atomic_store(sk.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            gave_up = 1;
             break;
           }
         }
+        *reinterpret_cast<volatile int*>(bad) = gave_up;
       }
       __syncthreads();
+      if (*reinterpret_cast<volatile int*>(bad)) poisoned = true;
       const __amdgpu_buffer_rsrc_t rs = slot_rsrc(b);
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
@@ -405,10 +415,14 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
               floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, (m * NF + n) * 8192, kSysCoherent));
         __builtin_amdgcn_sched_barrier(0);  // NF loads in flight at a time: no register spike
       }
+      __syncthreads();  // every wave read `bad` before the next contributor's wait rewrites it
     }
-    __syncthreads();
-    if (tid == 0)
-      for (int b = blockIdx.x + 8; b < fin; b += 8) __hip_atomic_store(sk.flags + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (poisoned) {
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < NF; ++n) acc[m][n] = floatx4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+    }
   }
 
   // ---- epilogue: lane holds row (.. + r); fragment pair (2p, 2p+1) gives it the 8 consecutive
@@ -639,6 +653,7 @@ struct SkWs {
   int* err = nullptr;
   long ws_floats = 0;
   int slots = 0;
+  int epoch = 0;
 };
 
 std::mutex g_sk_mu;
@@ -690,6 +705,8 @@ bool sk_plan(int M, int tiles, int nkt, int bn, hipStream_t st, SkArgs* sk, int*
     return v >= 1 ? v : 4;
   }();
   ++g_sk_launches;
+  w.epoch = w.epoch >= 0x7FFFFFF0 ? 1 : w.epoch + 1;
+  sk->epoch = w.epoch;
   sk->tiles = rem;
   sk->split = split;
   sk->ws = w.ws;
@@ -709,7 +726,7 @@ void launch_ph(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, i
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  SkArgs sk{0, 0, nullptr, nullptr, nullptr};
+  SkArgs sk{0, 0, nullptr, nullptr, nullptr, 0};
   int grid = gemm_grid(TM * TN);
   if (ks == 1 && EPI != EPI_PARTIAL) sk_plan(M, TM * TN, K / kBK, 64 * NF, st, &sk, &grid);
   gemm_kernel<NF, EPI, PH, PRIO><<<dim3(grid, ks), 512, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN,

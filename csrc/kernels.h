@@ -61,9 +61,6 @@ int lk_xgmi_allreduce(bf16_t* const* data, unsigned* const* sig, int rank, int w
 // epilogue (not SwiGLU) -- for shapes with fewer tiles than CUs
 int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks = 1);
 int lk_gemm_streamk(int mode);
-int lk_gemm4w_supported(int M, int N, int K, int epi, int ks);
-int lk_gemm4w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi,
-              bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, int variant = 0);
 int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
             int variant, bf16_t* out, long ldo, hipStream_t st, int ks = 1, float* ws = nullptr);
 
@@ -125,3 +122,6 @@ int lk_repeat_penalty(void* logits, int is_bf16, long ls, int B, const int* wind
 // logits (f32, modified in place by the penalty) -> out int32 [B]; the token is appended to the ring.
 int lk_sample(float* logits, long ls, int B, int V, const int* prm, int* hist, int* hist_len, int W,
               unsigned long long seed, int* out, hipStream_t st);
+
+// csrc/marker.hip: a one-wave marker kernel bounding a timed window in kernel traces
+int lk_window_mark(int id, hipStream_t st);

@@ -1,9 +1,10 @@
 """Command line.
 
-  serve           Ollama-compatible server on :11434 (one GPU; ``--gpus N`` starts N
-                  replica processes + the DP router in front of them; ``--frontends F``
-                  splits it: engine-core process(es) on the GPU(s) + F HTTP front-end
-                  processes sharing the port, routing over every core)
+  serve           Ollama-compatible server on :11434.  One GPU: one process.  ``--gpus N``:
+                  the split server by default -- one engine-core process per GPU + 2 HTTP
+                  front-end processes sharing the port (SO_REUSEPORT), each routing over
+                  every core; ``--frontends F`` sets F (also on one GPU); ``--frontends 0``
+                  with ``--gpus N`` keeps the round-2 layout (N replica servers + one proxy)
   serve-core      one engine core (GPU process of the split server)
   serve-frontend  one HTTP front-end of the split server
   rag-app         Minimal_RAG port (:5103): /health, /rag/search, /agent_rag
@@ -62,9 +63,14 @@ def _uvicorn(app, host, port, name="http"):
 
 
 def cmd_serve(args):
+    if args.frontends is None:
+        # several GPUs: the split server (engine core per GPU + 2 SO_REUSEPORT front-ends) by
+        # default, so no single Python loop relays every replica's NDJSON chunks; one GPU: the
+        # one-process server unless asked
+        args.frontends = 2 if args.gpus > 1 else 0
     if args.frontends > 0:
         return _serve_split(args)
-    if args.gpus > 1:
+    if args.gpus > 1:  # --frontends 0: the round-2 single-proxy router over replica servers
         return _serve_replicas(args)
     from .serving.model_manager import ModelManager
     from .serving.ollama_server import create_app
@@ -149,14 +155,20 @@ def _manager(args):
 
 
 def cmd_serve_core(args):
+    import signal
+
     from .serving.engine_core import EngineCore
 
+    # block SIGTERM / SIGINT BEFORE any thread starts (engine loop, socket, embed threads
+    # inherit the mask): otherwise the supervisor's terminate() can land on one of them with
+    # the default action and kill the process without the cleanup below, and Ctrl-C goes to
+    # Python's handler instead of sigwait
+    sigs = {signal.SIGTERM, signal.SIGINT}
+    signal.pthread_sigmask(signal.SIG_BLOCK, sigs)
     mgr = _manager(args)
     core = EngineCore(mgr, args.socket)
     try:
-        import signal
-
-        signal.sigwait({signal.SIGTERM, signal.SIGINT})
+        signal.sigwait(sigs)
     finally:
         core.close()
         mgr.shutdown()
@@ -357,8 +369,9 @@ def main(argv=None):
     p.add_argument("--alias", action="append", help="client-name=preset (e.g. llama3.1:8b=opt-125m)")
     p.add_argument("--checkpoint", action="append", help="name-or-preset=safetensors dir")
     p.add_argument("--preload", action="append")
-    p.add_argument("--frontends", type=int, default=0,
-                   help="split server: HTTP front-end processes (SO_REUSEPORT) in front of the engine core(s)")
+    p.add_argument("--frontends", type=int, default=None,
+                   help="split server: HTTP front-end processes (SO_REUSEPORT) in front of the engine core(s); "
+                        "default 2 with --gpus > 1, else 0 (one process); 0 with --gpus > 1 = single-proxy router")
     p.set_defaults(fn=cmd_serve)
     p = common(sub.add_parser("serve-core"), 0)
     p.add_argument("--socket", required=True)

@@ -37,6 +37,9 @@ PIPELINE_ORDER = os.environ.get("LK_PIPELINE", "csl")
 # through the model together as one extend chunk instead of one decode step each
 JUMP_FORWARD = os.environ.get("LK_JUMP_FORWARD", "1") != "0"
 
+# engine steps between polls of the stream-K GEMM's give-up word
+GEMM_HEALTH_EVERY = int(os.environ.get("LK_GEMM_HEALTH_EVERY", "512"))
+
 
 def _jump_ok(p: SamplingParams) -> bool:
     """Forced tokens can be appended without sampling: a grammar is set, and no repeat
@@ -248,6 +251,8 @@ class LLMEngine:
                 if not seq.finished:
                     self.scheduler.publish_blocks(seq)
             self.steps += 1
+            if self.steps % GEMM_HEALTH_EVERY == 0 and self.model.device.type == "cuda":
+                self._check_gemm_health()
             if self.step_trace is not None:
                 t3 = time.perf_counter()
                 ndec = len(batch.items) - sum(1 for sq, st, n in batch.items if st < len(sq.prompt_ids))
@@ -262,6 +267,19 @@ class LLMEngine:
             M.KV_USAGE.set(self.allocator.usage())
             M.RUNNING.set(len(self.scheduler.running))
             return out
+
+    @staticmethod
+    def _check_gemm_health():
+        """Fail loudly if a stream-K prefill GEMM gave up waiting for a partial tile since the
+        last check (csrc/gemm.hip poisons such a tile with NaN; never expected: the wait is a
+        bound instead of a hang).  One 4-byte device read per GEMM_HEALTH_EVERY steps."""
+        from .. import ops
+
+        if not ops.available():
+            return
+        errs = int(ops.lib().gemm_streamk(-1))
+        if errs:
+            raise RuntimeError(f"stream-K GEMM: {errs} partial-tile wait(s) timed out; outputs were poisoned")
 
     def _jump(self, seq: Sequence, now: float):
         """Grammar jump-forward: append the tokens ``seq``'s grammar allows exactly one choice

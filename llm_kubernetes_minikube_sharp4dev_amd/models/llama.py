@@ -2,7 +2,8 @@
 ``Minimal_RAG/Program.cs:24`` / ``Minimal_Agent_RAG/Program.cs:12`` — and 70B for TP=8).
 
 MI355X layout decisions:
-  * fused QKV and fused gate|up weights -> one hipBLASLt GEMM each instead of 3 / 2;
+  * fused QKV and fused gate|up weights -> one hand-written MFMA GEMM each instead of 3 / 2
+    (csrc/gemm.hip for prefill-sized steps, csrc/skinny_gemm.hip weight streaming for decode);
   * the residual stream is carried separately and folded into the RMSNorm kernel
     (``x = norm(res += y)``), so no standalone add pass ever touches HBM;
   * RoPE and the paged-KV write are one kernel on the QKV output;

@@ -59,6 +59,8 @@ class CoreClient:
         self._rid = itertools.count(1)
         self._task = None
         self.loop = None
+        self.connected = False
+        self.frames = 0           # token frames received (health: the core is stepping)
 
     async def connect(self, retries: int = 600):
         for i in range(retries):
@@ -69,6 +71,7 @@ class CoreClient:
                 await asyncio.sleep(0.5)
         else:
             raise ConnectionError(f"engine core at {self.path} not reachable")
+        self.connected = True
         self.loop = asyncio.get_running_loop()
         self._task = self.loop.create_task(self._read())
 
@@ -83,6 +86,7 @@ class CoreClient:
                 msg = msgpack.unpackb(await self.reader.readexactly(n), raw=False)
                 op = msg[0]
                 if op == "tok":
+                    self.frames += 1
                     for item in msg[1]:
                         q = self.queues.get(item[0])
                         if q is not None:
@@ -98,6 +102,7 @@ class CoreClient:
                     elif op == "err" and msg[1] in self.queues:
                         self.queues[msg[1]].put_nowait([msg[1], [], True, "stop", 0, msg[2]])
         except (asyncio.IncompleteReadError, ConnectionError):
+            self.connected = False
             log.error("engine core %s disconnected", self.path)
             for rid, q in list(self.queues.items()):
                 q.put_nowait([rid, [], True, "stop", 0, "engine core disconnected"])
@@ -176,9 +181,32 @@ class CorePool:
         return cands[next(self._rr) % len(cands)]
 
 
+class _RemoteWatchdog:
+    """The /health view of a remote engine core: the front-end cannot see the core's step
+    loop, so ``steps`` counts the token frames received (one per engine step with output) and
+    ``stalls`` the cores whose connection dropped."""
+
+    def __init__(self, owner: "_RemoteAsync"):
+        self.owner = owner  # the pool is read through the handle (tests swap it)
+
+    @property
+    def steps(self) -> int:
+        return sum(c.frames for c in self.owner.pool.clients)
+
+    @property
+    def stalls(self) -> int:
+        return sum(0 if c.connected else 1 for c in self.owner.pool.clients)
+
+
 class _RemoteAsync:
     def __init__(self, pool: CorePool, model: str, timeout_s: Optional[float]):
         self.pool, self.model, self.request_timeout_s = pool, model, timeout_s
+        self.watchdog = _RemoteWatchdog(self)
+
+    @property
+    def healthy(self) -> bool:
+        """Every engine core connection is up (a core that died closed its socket)."""
+        return all(c.connected for c in self.pool.clients)
 
     async def stream(self, prompt_ids: list, params: SamplingParams, req_id=None, timeout_s=None):
         c = self.pool.pick()
@@ -215,14 +243,41 @@ class RemoteGeneratorHandle:
 
 
 class _RemoteEmbed:
-    def __init__(self, pool: CorePool, model: str):
+    def __init__(self, pool: CorePool, model: str, tokenizer=None, max_len: int = 512):
         self.pool, self.model = pool, model
+        self.tok, self.max_len = tokenizer, max_len
+
+    def tokenize(self, texts: list) -> list:
+        """Token ids as the core's encoder sees them (front-end side: /api/embed reports
+        prompt_eval_count without a round trip)."""
+        return self.tok.encode_for_embedding(list(texts), self.max_len)
 
     def embed_cpu(self, texts: list) -> np.ndarray:
-        """Blocking (called from the HTTP app's embedding batcher threads)."""
+        """Blocking (called from the HTTP app's embedding batcher threads, never from the
+        core connection's own event loop: that would wait on a coroutine the blocked loop can
+        never run)."""
+        if not texts:  # nothing to encode: no round trip (the empty /api/embed input)
+            return np.zeros((0, 0), np.float32)
         c = self.pool.pick()
+        try:
+            running = asyncio.get_running_loop()
+        except RuntimeError:
+            running = None
+        if running is not None and running is c.loop:
+            raise RuntimeError("_RemoteEmbed.embed_cpu called on the core connection's event loop; "
+                               "use embed_async")
         fut = asyncio.run_coroutine_threadsafe(c.request("embed", self.model, list(texts)), c.loop)
-        _, _, data, rows, dim = fut.result()
+        return self._decode(fut.result())
+
+    async def embed_async(self, texts: list) -> np.ndarray:
+        """Non-blocking form for callers on the core connection's loop."""
+        if not texts:
+            return np.zeros((0, 0), np.float32)
+        return self._decode(await self.pool.pick().request("embed", self.model, list(texts)))
+
+    @staticmethod
+    def _decode(msg) -> np.ndarray:
+        _, _, data, rows, dim = msg
         return np.frombuffer(data, dtype=np.float32).reshape(rows, dim) if rows else np.zeros((0, 0), np.float32)
 
 
@@ -282,7 +337,12 @@ class RemoteModelManager(ModelManager):
             if kind != "embed":
                 raise KeyError(f"model '{name}' does not support embeddings")
             meta = self._load_remote(name)
-            h = RemoteEmbedderHandle(name, preset, _RemoteEmbed(self.pool, name), load_s=meta["load_s"])
+            from ..models.configs import ENCODERS
+
+            ck = self.checkpoints.get(name) or self.checkpoints.get(preset)
+            h = RemoteEmbedderHandle(name, preset, _RemoteEmbed(self.pool, name, load_tokenizer(ck),
+                                                                ENCODERS[preset].max_position),
+                                     load_s=meta["load_s"])
             self.embedders[name] = h
             return h
 

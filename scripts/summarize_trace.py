@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 kernel trace (run_kernel_trace.csv) over the last WINDOW
-seconds (the timed region of bench.py) as a markdown table: per-kernel time share,
-call count, mean duration, GPU busy fraction and the idle-gap histogram.
+"""Summarise a rocprofv3 kernel trace (run_kernel_trace.csv) over bench.py's timed window
+as a markdown table: per-kernel time share, call count, mean duration, GPU busy fraction and
+the idle-gap histogram.
 
-    python scripts/summarize_trace.py gpurun_out/prof_c128/run_kernel_trace.csv 4.0 > profiles/x.md
+The window is bounded by the two ``lk_window_mark_kernel`` launches bench.py makes under
+``LK_TRACE_WINDOW=1`` (csrc/marker.hip): exactly the timed steps, no warm-up, no drain.
+Without markers in the trace it falls back to the last WINDOW seconds.
+
+    python scripts/summarize_trace.py run_kernel_trace.csv [WINDOW_S] > profiles/x.md
 """
 import collections
 import csv
@@ -34,18 +38,27 @@ def _cls(name):
     return "other"
 
 
+def window(rows, window_s):
+    """(t0, t1, how): the marker-bounded timed window, else the last window_s seconds."""
+    marks = sorted(int(r["Start_Timestamp"]) for r in rows if "lk_window_mark" in r["Kernel_Name"])
+    if len(marks) >= 2:
+        return marks[0], marks[-1], "between the lk_window_mark kernels (bench.py timed window)"
+    end = max(int(r["End_Timestamp"]) for r in rows)
+    return end - window_s * 1e9, end, f"last {window_s:.1f} s of the trace (no window markers)"
+
+
 def main(path, window_s, top=25):
     rows = list(csv.DictReader(open(path)))
-    end = max(int(r["End_Timestamp"]) for r in rows)
-    t0 = end - window_s * 1e9
+    t0, t1, how = window(rows, window_s)
+    window_s = (t1 - t0) / 1e9
     agg = collections.defaultdict(lambda: [0, 0])
     ev = []
     for r in rows:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        if s < t0:
+        if s < t0 or e > t1 or "lk_window_mark" in r["Kernel_Name"]:
             continue
-        ev.append((s, e))
         name = r["Kernel_Name"].replace("(anonymous namespace)", "anon").split("(")[0][:100]
+        ev.append((s, e, name))
         if BY_GRID:  # one row per (kernel, grid): separates the GEMM shapes of one template
             grid = r.get("Grid_Size") or "x".join(r.get(f"Grid_Size_{a}", "?") for a in "XYZ")
             name += f" grid={grid}"
@@ -53,18 +66,21 @@ def main(path, window_s, top=25):
         a[0] += e - s
         a[1] += 1
     ev.sort()
-    busy, gaps = 0, []
-    cs, ce = ev[0]
-    for s, e in ev[1:]:
+    busy, gaps, big = 0, [], []
+    cs, ce, cn = ev[0]
+    for s, e, n in ev[1:]:
         if s > ce:
             busy += ce - cs
             gaps.append(s - ce)
+            if s - ce >= 1e5:  # itemise every idle gap >= 100 us: (gap, before, after, when)
+                big.append((s - ce, cn, n, (ce - t0) / 1e9))
             cs, ce = s, e
         else:
             ce = max(ce, e)
+        cn = n if e >= ce else cn
     busy += ce - cs
     tot = sum(v[0] for v in agg.values())
-    print(f"Window: last {window_s:.1f} s of the trace; GPU busy {busy / 1e6:.0f} ms "
+    print(f"Window: {window_s:.2f} s, {how}; GPU busy {busy / 1e6:.0f} ms "
           f"({100 * busy / (window_s * 1e9):.1f} %), {len(ev)} kernels\n")
     print("| kernel | total ms | share | calls | mean us |\n|---|---|---|---|---|")
     for k, (t, n) in sorted(agg.items(), key=lambda x: -x[1][0])[:top]:
@@ -84,6 +100,11 @@ def main(path, window_s, top=25):
     print("\n| idle gap | count | total ms |\n|---|---|---|")
     for k in ["<5us", "5-20us", "20-100us", "0.1-1ms", ">1ms"]:
         print(f"| {k} | {b[k]} | {bt[k] / 1e6:.1f} |")
+    if big:
+        print(f"\nIdle gaps >= 100 us ({len(big)}, {sum(g for g, *_ in big) / 1e6:.1f} ms), largest first:\n")
+        print("| gap us | at s | last kernel before | first kernel after |\n|---|---|---|---|")
+        for g, a, n, at in sorted(big, reverse=True)[:40]:
+            print(f"| {g / 1e3:.0f} | {at:.3f} | `{a[:60]}` | `{n[:60]}` |")
 
 
 if __name__ == "__main__":

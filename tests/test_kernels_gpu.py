@@ -455,79 +455,6 @@ def test_gemm_splitk(hip, MNK, splits, epi):
                        f"gemm split{splits} epi{epi} s{sched}/{bn} M{M} N{N} K{K}")
 
 
-@pytest.mark.parametrize("M", [1, 257, 1000, 3584])
-@pytest.mark.parametrize("NK", [(6144, 4096), (4096, 14336), (768, 768), (1280, 8192), (2304, 384), (256, 128)])
-def test_gemm4w(hip, M, NK):
-    """One-wave-per-SIMD 256 x 256 GEMM (csrc/gemm4w.hip: AGPR accumulators, 4-slot LDS-DMA
-    ring of 32-deep slices) vs an fp32 matmul, with M tails and the shortest K (4 slices)."""
-    N, K = NK
-    torch.manual_seed(M + N + 1)
-    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
-    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
-    assert hip.gemm4w_supported(M, N, K, 0)
-    for v in (0, 1, 5):
-        _close(hip.gemm4w(x, w, variant=v), x.float() @ w.float().t(), 0.02, 0.01, f"gemm4w v{v} M{M} N{N} K{K}")
-
-
-def test_gemm4w_asymmetric_layout(hip):
-    """A = I with an asymmetric B: catches a transposed / permuted C write."""
-    M, N, K = 512, 512, 256
-    x = torch.eye(M, K, device=DEV, dtype=torch.bfloat16)
-    w = (torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K) % 97 - 48).to(torch.bfloat16)
-    exp = torch.zeros(M, N)
-    exp[:K] = w.float().t().cpu()
-    for v in (0, 1, 5):
-        assert torch.equal(hip.gemm4w(x, w, variant=v).float().cpu(), exp), v
-
-
-@pytest.mark.parametrize("M", [300, 2048])
-@pytest.mark.parametrize("IK", [(14336, 4096), (3584, 8192), (1536, 768)])
-def test_gemm4w_swiglu(hip, M, IK):
-    I, K = IK
-    torch.manual_seed(5)
-    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
-    w = torch.randn(2 * I, K, device=DEV, dtype=torch.bfloat16) * 0.05
-    a_ref = ref.silu_mul((x.float() @ w.float().t()).to(torch.bfloat16))
-    for v in (0, 1, 5):
-        _close(hip.gemm4w(x, w, None, 1, variant=v), a_ref, 0.03, 0.01, f"gemm4w v{v} swiglu M{M} I{I}")
-
-
-@pytest.mark.parametrize("M", [7, 300, 4000])
-@pytest.mark.parametrize("NK", [(2304, 768), (3072, 768), (768, 3072)])
-@pytest.mark.parametrize("epi", [2, 3, 4])
-def test_gemm4w_bias_epilogues(hip, M, NK, epi):
-    N, K = NK
-    torch.manual_seed(M * 3 + N + epi)
-    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
-    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
-    b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
-    y = (x.float() @ w.float().t() + b.float()).to(torch.bfloat16).float()
-    if epi == 3:
-        y = torch.nn.functional.gelu(y)
-    elif epi == 4:
-        y = torch.relu(y)
-    for v in (0, 1, 5):
-        _close(hip.gemm4w(x, w, b, epi, variant=v), y, 0.03, 0.01, f"gemm4w v{v} epi{epi} M{M} N{N}")
-
-
-@pytest.mark.parametrize("MNK", [(2048, 4096, 4096), (1000, 768, 3072), (4096, 1280, 8192)])
-@pytest.mark.parametrize("splits", [2, 3])
-@pytest.mark.parametrize("epi", [0, 2])
-def test_gemm4w_splitk(hip, MNK, splits, epi):
-    M, N, K = MNK
-    torch.manual_seed(M + splits + epi)
-    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
-    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
-    b = torch.randn(N, device=DEV, dtype=torch.bfloat16) if epi else None
-    y = x.float() @ w.float().t()
-    if epi:
-        y = (y + b.float()).to(torch.bfloat16).float()
-    if hip.gemm4w_supported(M, N, K, epi, splits):
-        for v in (0, 1, 5):
-            _close(hip.gemm4w(x, w, b, epi, None, splits, v), y, 0.03, 0.01,
-                   f"gemm4w v{v} split{splits} epi{epi} M{M} N{N} K{K}")
-
-
 @pytest.mark.parametrize("MNKE", [(4352, 4096, 4096, 0), (4300, 6144, 4096, 0), (4352, 28672, 4096, 1),
                                   (5000, 3072, 4096, 3), (4864, 4096, 14336, 0), (1536, 4096, 4096, 2),
                                   (5376, 4096, 14336, 2)])

@@ -109,3 +109,29 @@ def test_requests_spread_over_cores_and_finish(split):
         h.async_engine.pool = pool
     for h in fe.state.manager.embedders.values():
         h.engine.pool = pool
+
+
+def test_empty_embed_input_and_health(split):
+    """an empty /api/embed input must answer (it used to block the front-end's
+    event loop on a round trip that loop had to run), and /health must work over remote
+    cores (the remote handle had no watchdog: 500)."""
+    c_fe, c_local, *_ = split
+    for body in ({"model": "nomic-embed-text", "input": []}, {"model": "nomic-embed-text", "input": ""}):
+        r = c_fe.post("/api/embed", json=body, timeout=30)
+        assert r.status_code == c_local.post("/api/embed", json=body).status_code
+    h = c_fe.get("/health")
+    assert h.status_code == 200, h.text
+    js = h.json()
+    assert js["status"] == "ok" and js["generators"]["llama3.1:8b"]["healthy"] is True
+    assert js["generators"]["llama3.1:8b"]["stalls"] == 0
+    # the front-end still serves after the empty request
+    assert len(c_fe.post("/api/embeddings", json={"model": "nomic-embed-text", "input": "x"}).json()["embedding"]) == 128
+
+
+def test_api_embed_nonempty_matches_local(split):
+    """/api/embed over remote cores (it used to call a tokenizer the remote handle lacked)."""
+    c_fe, c_local, *_ = split
+    body = {"model": "nomic-embed-text", "input": ["alpha beta", "gamma"]}
+    a, b = c_fe.post("/api/embed", json=body).json(), c_local.post("/api/embed", json=body).json()
+    assert a["prompt_eval_count"] == b["prompt_eval_count"] > 0
+    assert len(a["embeddings"]) == 2 and max(abs(x - y) for x, y in zip(a["embeddings"][1], b["embeddings"][1])) < 1e-5
