@@ -262,6 +262,80 @@ at::Tensor gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at
 }
 
 
+// The fused prefill chain (csrc/gemm.hip LkEpi): epi 0 / 1 / 7 with an optional folded-RMSNorm
+// row scale from ss_in [nt, ld] f32, epi 6 (RESID) updating `resid` in place and writing the
+// per-256-column partial sums of squares into ss_out [N / 256, ld].  Returns `out` (RESID: resid).
+at::Tensor gemm_fused(const at::Tensor& x, const at::Tensor& w, int64_t epi, int64_t bn, const c10::optional<at::Tensor>& out_,
+                      int64_t variant, int64_t splits, const c10::optional<at::Tensor>& ss_in, double eps,
+                      const c10::optional<at::Tensor>& resid, const c10::optional<at::Tensor>& ss_out,
+                      const c10::optional<at::Tensor>& positions, const c10::optional<at::Tensor>& cos_sin,
+                      const c10::optional<at::Tensor>& slots, const c10::optional<at::Tensor>& k_cache,
+                      const c10::optional<at::Tensor>& v_cache, int64_t hq, int64_t hkv, int64_t hd) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_LASTDIM(x); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "x [M,K], w [N,K]");
+  check_rows16(x, "x"); check_rows16(w, "w");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(epi == 0 || epi == 1 || epi == 6 || epi == 7, "gemm_fused: epi must be NONE / SWIGLU / RESID / QKV");
+  TORCH_CHECK(lk_gemm_supported(M, N, K, (int)epi, (int)bn, (int)splits), "gemm_fused: unsupported shape M", M, " N", N,
+              " K", K, " epi", epi, " bn", bn, " splits", splits);
+  LkEpi ea;
+  const int H = K;
+  if (ss_in) {
+    CHECK_CUDA(*ss_in); CHECK_F32(*ss_in); CHECK_CONTIG(*ss_in);
+    TORCH_CHECK(ss_in->dim() == 2 && ss_in->size(0) >= 1 && ss_in->size(0) <= 32 && ss_in->size(1) >= M,
+                "ss_in must be [nt <= 32, >= M] f32");
+    ea.ss_in = ss_in->data_ptr<float>();
+    ea.ss_nt = ss_in->size(0);
+    ea.ss_ld = ss_in->size(1);
+    ea.inv_h = 1.f / (float)H;
+    ea.eps = (float)eps;
+  }
+  at::Tensor out;
+  if (epi == 6) {
+    TORCH_CHECK(resid && ss_out, "RESID needs resid and ss_out");
+    CHECK_CUDA(*resid); CHECK_BF16(*resid); CHECK_LASTDIM(*resid); check_rows16(*resid, "resid");
+    TORCH_CHECK(resid->dim() == 2 && resid->size(0) == M && resid->size(1) == N, "resid must be [M, N]");
+    CHECK_CUDA(*ss_out); CHECK_F32(*ss_out); CHECK_CONTIG(*ss_out);
+    TORCH_CHECK(ss_out->dim() == 2 && ss_out->size(0) == N / 256 && ss_out->size(1) >= M, "ss_out must be [N/256, >= M]");
+    ea.resid = bp(*resid);
+    ea.ldr = resid->stride(0);
+    ea.ss_out = ss_out->data_ptr<float>();
+    ea.ss_out_ld = ss_out->size(1);
+    out = *resid;
+  } else {
+    const int n_out = epi == 1 ? N / 2 : N;
+    out = out_ ? *out_ : at::empty({M, n_out}, x.options());
+    CHECK_BF16(out); CHECK_LASTDIM(out);
+    TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == n_out, "out shape");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0 && out.stride(0) % 8 == 0, "out alignment (16 B)");
+  }
+  if (epi == 7) {
+    TORCH_CHECK(positions && cos_sin, "QKV needs positions and cos_sin");
+    CHECK_I32(*positions); CHECK_CONTIG(*positions); CHECK_F32(*cos_sin); CHECK_CONTIG(*cos_sin);
+    TORCH_CHECK(positions->numel() >= M, "positions [>= M]");
+    TORCH_CHECK(cos_sin->dim() == 2 && cos_sin->size(1) == hd, "cos_sin [max_pos, hd]");
+    TORCH_CHECK(N == (hq + 2 * hkv) * hd && hd % 16 == 0, "QKV: N must be (hq + 2 hkv) * hd");
+    ea.pos = ip(*positions);
+    ea.cos_sin = cos_sin->data_ptr<float>();
+    ea.hq = hq; ea.hkv = hkv; ea.hd = hd;
+    if (k_cache || v_cache) {
+      TORCH_CHECK(k_cache && v_cache && slots, "QKV: k_cache, v_cache and slots together");
+      CHECK_BF16(*k_cache); CHECK_BF16(*v_cache); CHECK_CONTIG(*k_cache); CHECK_CONTIG(*v_cache);
+      CHECK_I32(*slots); CHECK_CONTIG(*slots);
+      TORCH_CHECK(slots->numel() >= M, "slots [>= M]");
+      TORCH_CHECK(k_cache->dim() == 4 && k_cache->size(1) == hkv && k_cache->size(3) == hd && k_cache->sizes() == v_cache->sizes(),
+                  "caches [num_blocks, hkv, bs, hd]");
+      ea.kc = bp(*k_cache); ea.vc = bp(*v_cache); ea.slots = ip(*slots); ea.bs = k_cache->size(2);
+    }
+  }
+  at::Tensor ws;
+  if (splits > 1) ws = at::empty({splits, M, N}, x.options().dtype(at::kFloat));
+  int rc = lk_gemm(bp(x), x.stride(0), bp(w), nullptr, M, N, K, (int)epi, (int)bn, (int)variant, bp(out), out.stride(0),
+                   cur_stream(), (int)splits, splits > 1 ? ws.data_ptr<float>() : nullptr, &ea);
+  CHECK_RC(rc, "gemm_fused");
+  return out;
+}
+
 int64_t gemm_streamk(int64_t mode) { return lk_gemm_streamk((int)mode); }
 
 bool gemm_supported(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bn, int64_t splits) {
@@ -716,6 +790,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, "", py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("epi") = 0,
         py::arg("bn") = 256, py::arg("out") = py::none(), py::arg("variant") = 1,
         py::arg("splits") = 1);
+  m.def("gemm_fused", &gemm_fused, "", py::arg("x"), py::arg("w"), py::arg("epi"), py::arg("bn"), py::arg("out") = py::none(),
+        py::arg("variant") = 2, py::arg("splits") = 1, py::arg("ss_in") = py::none(), py::arg("eps") = 1e-5,
+        py::arg("resid") = py::none(), py::arg("ss_out") = py::none(), py::arg("positions") = py::none(),
+        py::arg("cos_sin") = py::none(), py::arg("slots") = py::none(), py::arg("k_cache") = py::none(),
+        py::arg("v_cache") = py::none(), py::arg("hq") = 0, py::arg("hkv") = 0, py::arg("hd") = 0);
   m.def("gemm_streamk", &gemm_streamk,
         "stream-K policy of the prefill GEMM (mode 0 off / 1 on / -1 keep); returns the waits that gave up since the last call",
         py::arg("mode") = -1);

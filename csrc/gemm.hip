@@ -59,7 +59,18 @@ typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 constexpr int kBM = 256, kBK = 64;
 constexpr int kSlotA = 128 * 128;  // an A slot: 128 rows x 128 B
 
-enum { EPI_NONE = 0, EPI_SWIGLU = 1, EPI_BIAS = 2, EPI_BIAS_GELU = 3, EPI_BIAS_RELU = 4, EPI_PARTIAL = 5 };
+enum { EPI_NONE = 0, EPI_SWIGLU = 1, EPI_BIAS = 2, EPI_BIAS_GELU = 3, EPI_BIAS_RELU = 4, EPI_PARTIAL = 5,
+       EPI_RESID = 6, EPI_QKV = 7 };
+// epilogues that can take the folded-RMSNorm row scale (LkEpi::ss_in)
+constexpr bool scalable(int epi) { return epi == EPI_NONE || epi == EPI_SWIGLU || epi == EPI_QKV; }
+// LDS layout after the K loop (the staging buffers are dead): [0, 64) stream-K give-up word,
+// [64, 64 + 3 KB) row-scale partials (512) + scales (256), then the RESID reduction [4][256]
+constexpr int kLdsScale = 64, kLdsResid = 64 + 768 * 4;
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+LK_DEVICE __amdgpu_buffer_rsrc_t rsrc_of(const void* p, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)min(bytes, 0x7FFFFFF0L), 0x00020000);
+}
 
 LK_DEVICE int swz(int row) { return (row >> 1) & 7; }
 template <int N>
@@ -112,7 +123,7 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
                                            const bf16_t* __restrict__ bias, int M, int K, int I,
                                            bf16_t* __restrict__ out, long ldo, int TM, int TN, int group_m,
                                            int tile, int kt0, int nk, int kz, int mode, int fin_end,
-                                           const SkArgs& sk) {
+                                           const SkArgs& sk, const LkEpi& ea) {
   using G = Geo<NF>;
   constexpr int BN = G::BN, NF0 = G::NF0, NF1 = G::NF1;
   static_assert(EPI != EPI_SWIGLU || NF == 4, "SwiGLU pairs fragments n and n+2");
@@ -131,6 +142,23 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases stay scalar
   const int wr = w >> 2, wc = w & 3;
   const int r = lane & 15, g = lane >> 4;
+
+  // folded RMSNorm, consumer side: thread tid prefetches partials t = (tid >> 8) + 2 i of tile
+  // row tid & 255 BEFORE the K loop (their latency hides under it; they are older than every
+  // LDS-DMA, so the loop's counted vmcnt waits stay exact); the buffer range check returns 0
+  // for t >= ss_nt -- no predicated loads
+  const bool has_scale = scalable(EPI) && ea.ss_in != nullptr;
+  float ssp[16];
+  if constexpr (scalable(EPI)) {
+    if (has_scale) {
+      const __amdgpu_buffer_rsrc_t srs = rsrc_of(ea.ss_in, (long)ea.ss_nt * ea.ss_ld * 4);
+      const unsigned base = (unsigned)(((tid >> 8) * ea.ss_ld + (long)tm * kBM + (tid & 255)) * 4);
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        ssp[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                               srs, base + (unsigned)(i * 2 * ea.ss_ld * 4), 0, 0));
+    }
+  }
 
   // W row feeding B-tile row j
   auto wrow = [&](int j) -> long {
@@ -425,6 +453,25 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
     }
   }
 
+  // ---- row scales of the folded RMSNorm: s[row] = rsqrt(sum of the partials / H + eps), into LDS
+  float* scl = reinterpret_cast<float*>(smem + kLdsScale);
+  if constexpr (scalable(EPI)) {
+    if (has_scale && mode != SK_PARTIAL) {
+      float part = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) part += ssp[i];
+      __syncthreads();  // every wave is past its last staging read
+      scl[tid] = part;
+      __syncthreads();
+      if (tid < 256) scl[512 + tid] = rsqrtf((scl[tid] + scl[tid + 256]) * ea.inv_h + ea.eps);
+      __syncthreads();
+    }
+  }
+  auto row_scale = [&](int lrow) -> float {
+    if constexpr (scalable(EPI)) return has_scale ? scl[512 + lrow] : 1.f;
+    else return 1.f;
+  };
+
   // ---- epilogue: lane holds row (.. + r); fragment pair (2p, 2p+1) gives it the 8 consecutive
   // columns 32p + 8g .. +7 of its wave's 16NF (the pair_col layout); NF = 3's third fragment
   // the 4 columns 32 + 4g .. +3
@@ -454,12 +501,151 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
     for (int m = 0; m < 8; ++m) {
       const int row = tm * kBM + wr * 128 + m * 16 + r;
       if (row >= M || mode == SK_PARTIAL) continue;
+      const float sc = row_scale(wr * 128 + m * 16 + r);
       float y[8];
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) y[4 * h + v] = rbf(lk_silu(rbf(acc[m][h][v]))) * rbf(acc[m][h + 2][v]);
+        for (int v = 0; v < 4; ++v)
+          y[4 * h + v] = rbf(lk_silu(rbf(acc[m][h][v] * sc))) * rbf(acc[m][h + 2][v] * sc);
       put8(out + (long)row * ldo + tn * 128 + wc * 32 + 8 * g, y);
+    }
+  } else if constexpr (EPI == EPI_RESID) {
+    // producer side of the folded norm: r = bf16(r + bf16(acc)) in place, then the partial sum
+    // of squares of the new r over this tile's BN columns (lanes r + 16 g, then the 4 wc waves)
+    if (mode != SK_PARTIAL) {
+      constexpr int NP = NF / 2;
+      const __amdgpu_buffer_rsrc_t rrs = rsrc_of(ea.resid, (long)M * ea.ldr * 2);  // rows >= M: 0 / dropped
+      float ssm[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const long row = (long)tm * kBM + wr * 128 + m * 16 + r;
+        const long cb = (long)tn * BN + wc * 16 * NF;
+        u32x4_t rv[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          rv[p] = __builtin_amdgcn_raw_buffer_load_b128(rrs, (unsigned)((row * ea.ldr + cb + 32 * p + 8 * g) * 2), 0, 0);
+        u32x2_t rv3;
+        if constexpr (NF == 3) rv3 = __builtin_amdgcn_raw_buffer_load_b64(rrs, (unsigned)((row * ea.ldr + cb + 32 + 4 * g) * 2), 0, 0);
+        float ss = 0.f;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          const unsigned rw[4] = {rv[p].x, rv[p].y, rv[p].z, rv[p].w};
+          float y[8];
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const int j = 4 * h + v;
+              const float res = bf2f((bf16_t)((rw[j >> 1] >> (16 * (j & 1))) & 0xFFFF));
+              y[j] = rbf(rbf(acc[m][2 * p + h][v]) + res);
+              ss += y[j] * y[j];
+            }
+          u32x4_t pk;
+          pk.x = pack_bf2(y[0], y[1]);
+          pk.y = pack_bf2(y[2], y[3]);
+          pk.z = pack_bf2(y[4], y[5]);
+          pk.w = pack_bf2(y[6], y[7]);
+          __builtin_amdgcn_raw_buffer_store_b128(pk, rrs, (unsigned)((row * ea.ldr + cb + 32 * p + 8 * g) * 2), 0, 0);
+        }
+        if constexpr (NF == 3) {
+          const unsigned rw[2] = {rv3.x, rv3.y};
+          float y[4];
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const float res = bf2f((bf16_t)((rw[v >> 1] >> (16 * (v & 1))) & 0xFFFF));
+            y[v] = rbf(rbf(acc[m][2][v]) + res);
+            ss += y[v] * y[v];
+          }
+          u32x2_t pk;
+          pk.x = pack_bf2(y[0], y[1]);
+          pk.y = pack_bf2(y[2], y[3]);
+          __builtin_amdgcn_raw_buffer_store_b64(pk, rrs, (unsigned)((row * ea.ldr + cb + 32 + 4 * g) * 2), 0, 0);
+        }
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        ssm[m] = ss;
+      }
+      float* red = reinterpret_cast<float*>(smem + kLdsResid);  // [4 wc][256 tile rows]
+      __syncthreads();  // every wave is past its last staging read
+      if (g == 0) {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) red[wc * 256 + wr * 128 + m * 16 + r] = ssm[m];
+      }
+      __syncthreads();
+      if (tid < 256) {
+        const int row = tm * kBM + tid;
+        if (row < M) ea.ss_out[(long)tn * ea.ss_out_ld + row] = (red[tid] + red[256 + tid]) + (red[512 + tid] + red[768 + tid]);
+      }
+    }
+  } else if constexpr (EPI == EPI_QKV) {
+    // RoPE (interleaved pairs) on the q / k heads + the paged-KV scatter, on the bf16-rounded
+    // (row-scaled) projection: the values "GEMM -> rope_kv_" would leave
+    const int qcols = ea.hq * ea.hd, kcols = ea.hkv * ea.hd, half = ea.hd >> 1;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int row = tm * kBM + wr * 128 + m * 16 + r;
+      if (row >= M || mode == SK_PARTIAL) continue;
+      const float sc = row_scale(wr * 128 + m * 16 + r);
+      const int pos = ea.pos[row];
+      const int slot = ea.slots ? ea.slots[row] : -1;
+      const float* cs = ea.cos_sin + (long)pos * ea.hd;
+      bf16_t* orow = out + (long)row * ldo;
+      auto group = [&](int c, float* y, int n) {  // n = 8 or 4 consecutive columns c..c+n-1
+        for (int j = 0; j < n; ++j) y[j] = rbf(y[j] * sc);
+        if (c < qcols + kcols) {
+          const int i0 = (c % ea.hd) >> 1;  // first rotation pair
+          float cv[4], sv[4];
+          if (n == 8) {
+            const floatx4 c4 = *reinterpret_cast<const floatx4*>(cs + i0);
+            const floatx4 s4 = *reinterpret_cast<const floatx4*>(cs + half + i0);
+            for (int q = 0; q < 4; ++q) { cv[q] = c4[q]; sv[q] = s4[q]; }
+          } else {
+            const float2 c2 = *reinterpret_cast<const float2*>(cs + i0);
+            const float2 s2 = *reinterpret_cast<const float2*>(cs + half + i0);
+            cv[0] = c2.x; cv[1] = c2.y; sv[0] = s2.x; sv[1] = s2.y;
+          }
+          for (int q = 0; q < n / 2; ++q) {
+            const float a = y[2 * q], b = y[2 * q + 1];
+            y[2 * q] = a * cv[q] - b * sv[q];
+            y[2 * q + 1] = b * cv[q] + a * sv[q];
+          }
+        }
+        uint4_t pk;
+        pk.x = pack_bf2(y[0], y[1]);
+        pk.y = pack_bf2(y[2], y[3]);
+        if (n == 8) {
+          pk.z = pack_bf2(y[4], y[5]);
+          pk.w = pack_bf2(y[6], y[7]);
+          *reinterpret_cast<uint4_t*>(orow + c) = pk;
+        } else {
+          *reinterpret_cast<uint2*>(orow + c) = make_uint2(pk.x, pk.y);
+        }
+        if (c >= qcols && slot >= 0 && ea.kc != nullptr) {
+          const bool isv = c >= qcols + kcols;
+          const int cc = c - qcols - (isv ? kcols : 0);
+          const int h = cc / ea.hd, d = cc - h * ea.hd;
+          bf16_t* dst = (isv ? ea.vc : ea.kc) + (((long)(slot / ea.bs) * ea.hkv + h) * ea.bs + slot % ea.bs) * ea.hd + d;
+          if (n == 8) *reinterpret_cast<uint4_t*>(dst) = pk;
+          else *reinterpret_cast<uint2*>(dst) = make_uint2(pk.x, pk.y);
+        }
+      };
+      const int cb = tn * BN + wc * 16 * NF;
+#pragma unroll
+      for (int p = 0; p < NF / 2; ++p) {
+        float y[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) y[4 * h + v] = acc[m][2 * p + h][v];
+        group(cb + 32 * p + 8 * g, y, 8);
+      }
+      if constexpr (NF == 3) {
+        float y[8];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) y[v] = acc[m][2][v];
+        group(cb + 32 + 4 * g, y, 4);
+      }
     }
   } else {
     constexpr int NP = NF / 2;  // fragment pairs
@@ -498,6 +684,11 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
       const int row = tm * kBM + wr * 128 + m * 16 + r;
       if (row >= M || mode == SK_PARTIAL) continue;
       bf16_t* orow = out + (long)row * ldo + tn * BN + wc * 16 * NF;
+      if constexpr (EPI == EPI_NONE) {
+        const float sc = row_scale(wr * 128 + m * 16 + r);
+#pragma unroll
+        for (int n = 0; n < NF; ++n) acc[m][n] *= sc;
+      }
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
         float y[8];
@@ -548,12 +739,35 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   *reinterpret_cast<uint2*>(out + (long)row * ldo + col) = pk;
 }
 
+// split-K reduction for the RESID epilogue: block (tile tn of 256 columns, row), 64 threads x 4
+// columns: r = bf16(r + bf16(sum_z part)) in place, and the tile's partial sum of squares of the
+// new r into ss_out[tn][row] -- the same planes the unsplit RESID epilogue writes
+__global__ __launch_bounds__(64) void splitk_resid_kernel(const float* __restrict__ part, int S, int M, int N,
+                                                          LkEpi ea) {
+  const int tn = blockIdx.x, row = blockIdx.y, col = tn * 256 + 4 * threadIdx.x;
+  const long MN = (long)M * N;
+  floatx4 a = *reinterpret_cast<const floatx4*>(part + (long)row * N + col);
+  for (int z = 1; z < S; ++z) a += *reinterpret_cast<const floatx4*>(part + z * MN + (long)row * N + col);
+  bf16_t* rp = ea.resid + (long)row * ea.ldr + col;
+  const uint2 rv = *reinterpret_cast<const uint2*>(rp);
+  const unsigned rw[2] = {rv.x, rv.y};
+  float y[4], ss = 0.f;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    y[v] = rbf(rbf(a[v]) + bf2f((bf16_t)((rw[v >> 1] >> (16 * (v & 1))) & 0xFFFF)));
+    ss += y[v] * y[v];
+  }
+  *reinterpret_cast<uint2*>(rp) = make_uint2(pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3]));
+  ss = wave_sum(ss);
+  if (threadIdx.x == 0) ea.ss_out[(long)tn * ea.ss_out_ld + row] = ss;
+}
+
 template <int NF, int EPI, int PH, int PRIO>
 __global__ __launch_bounds__(512, 1) void gemm_kernel(const bf16_t* __restrict__ X, long ldx,
                                                       const bf16_t* __restrict__ W,
                                                       const bf16_t* __restrict__ bias, int M, int K, int I,
                                                       bf16_t* __restrict__ out, long ldo, int TM, int TN, int group_m,
-                                                      SkArgs sk) {
+                                                      SkArgs sk, LkEpi ea) {
   // gridDim.x == TM * TN: one tile per workgroup; fewer: persistent workgroups walking the
   // tiles b, b + grid, ... (same XCD: the grid is a multiple of 8), the epilogue stores of one
   // tile drained before the next tile's LDS-DMA prologue (vmcnt counts stores too)
@@ -604,7 +818,7 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const bf16_t* __restrict__
       break;
     }
     gemm8_body<NF, EPI, PH, PRIO>(X, ldx, W, bias, M, K, I, out, ldo, TM, TN, group_m, tile, a0, n, kz, mode, fin_end,
-                                  sk);
+                                  sk, ea);
     wait_vm<0>();
   }
 }
@@ -718,7 +932,7 @@ bool sk_plan(int M, int tiles, int nkt, int bn, hipStream_t st, SkArgs* sk, int*
 
 template <int NF, int EPI, int PH, int PRIO = 0>
 void launch_ph(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
-               long ldo, int TM, int TN, int ks, hipStream_t st) {
+               long ldo, int TM, int TN, int ks, hipStream_t st, const LkEpi& ea) {
   constexpr int lds = 2 * Geo<NF>::BUF;
   static bool attr = false;
   if (!attr) {
@@ -730,25 +944,30 @@ void launch_ph(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, i
   int grid = gemm_grid(TM * TN);
   if (ks == 1 && EPI != EPI_PARTIAL) sk_plan(M, TM * TN, K / kBK, 64 * NF, st, &sk, &grid);
   gemm_kernel<NF, EPI, PH, PRIO><<<dim3(grid, ks), 512, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN,
-                                                                   group_rows(), sk);
+                                                                   group_rows(), sk, ea);
 }
 // schedule: 0 = 4 phases per K-tile (per-cluster priority), 1 = 2 phases (static priority)
 template <int NF, int EPI>
 void launch(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
-            long ldo, int TM, int TN, int sched, hipStream_t st, int ks = 1) {
-  if (sched == 1) launch_ph<NF, EPI, 2, 1>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
-  else if (sched == 2) launch_ph<NF, EPI, 4, 1>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
-  else launch_ph<NF, EPI, 4, 0>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st);
+            long ldo, int TM, int TN, int sched, hipStream_t st, int ks = 1, const LkEpi& ea = LkEpi{}) {
+  if (sched == 1) launch_ph<NF, EPI, 2, 1>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st, ea);
+  else if (sched == 2) launch_ph<NF, EPI, 4, 1>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st, ea);
+  else launch_ph<NF, EPI, 4, 0>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st, ea);
 }
 
 template <int NF>
 int dispatch(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi,
-             int sched, int ks, float* ws, bf16_t* out, long ldo, hipStream_t st) {
+             int sched, int ks, float* ws, bf16_t* out, long ldo, hipStream_t st, const LkEpi& ea) {
   const int TM = (M + kBM - 1) / kBM;
+  constexpr int BN = 64 * NF;
   if (ks > 1) {  // fp32 partials of ks K-ranges into ws [ks, M, N], then the reduce applies the epilogue
-    constexpr int BN = 64 * NF;
-    if (epi == EPI_SWIGLU || N % BN || ws == nullptr || (epi != EPI_NONE && bias == nullptr)) return -1;
+    if (epi == EPI_SWIGLU || epi == EPI_QKV || N % BN || ws == nullptr || (epi >= EPI_BIAS && epi <= EPI_BIAS_RELU && bias == nullptr))
+      return -1;
     launch<NF, EPI_PARTIAL>(x, ldx, w, nullptr, M, K, 0, reinterpret_cast<bf16_t*>(ws), N, TM, N / BN, sched, st, ks);
+    if (epi == EPI_RESID) {
+      splitk_resid_kernel<<<dim3(N / 256, M), 64, 0, st>>>(ws, ks, M, N, ea);
+      return 0;
+    }
     const long n = (long)M * (N / 4);
     const int blocks = (int)((n + 255) / 256);
     switch (epi) {
@@ -765,18 +984,22 @@ int dispatch(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int
       return -1;
     } else {
       if (N % 2 || (N / 2) % 128) return -1;
-      launch<4, EPI_SWIGLU>(x, ldx, w, bias, M, K, N / 2, out, ldo, TM, N / 256, sched, st);
+      launch<4, EPI_SWIGLU>(x, ldx, w, bias, M, K, N / 2, out, ldo, TM, N / 256, sched, st, 1, ea);
       return 0;
     }
   }
-  constexpr int BN = 64 * NF;
   if (N % BN) return -1;
-  if (epi != EPI_NONE && bias == nullptr) return -1;
+  if (epi >= EPI_BIAS && epi <= EPI_BIAS_RELU && bias == nullptr) return -1;
   switch (epi) {
-    case EPI_NONE: launch<NF, EPI_NONE>(x, ldx, w, bias, M, K, 0, out, ldo, TM, N / BN, sched, st); break;
+    case EPI_NONE: launch<NF, EPI_NONE>(x, ldx, w, bias, M, K, 0, out, ldo, TM, N / BN, sched, st, 1, ea); break;
     case EPI_BIAS: launch<NF, EPI_BIAS>(x, ldx, w, bias, M, K, 0, out, ldo, TM, N / BN, sched, st); break;
     case EPI_BIAS_GELU: launch<NF, EPI_BIAS_GELU>(x, ldx, w, bias, M, K, 0, out, ldo, TM, N / BN, sched, st); break;
     case EPI_BIAS_RELU: launch<NF, EPI_BIAS_RELU>(x, ldx, w, bias, M, K, 0, out, ldo, TM, N / BN, sched, st); break;
+    case EPI_RESID:
+      if constexpr (NF != 4) return -1;  // partial planes per 256 columns (same as the split-K reduce)
+      else launch<4, EPI_RESID>(x, ldx, w, nullptr, M, K, 0, out, ldo, TM, N / BN, sched, st, 1, ea);
+      break;
+    case EPI_QKV: launch<NF, EPI_QKV>(x, ldx, w, nullptr, M, K, 0, out, ldo, TM, N / BN, sched, st, 1, ea); break;
     default: return -1;
   }
   return 0;
@@ -803,8 +1026,10 @@ int lk_gemm_streamk(int mode) {
 
 int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks) {
   if (M < 1 || K < kBK || K % kBK || (bn != 192 && bn != 256)) return 0;
-  if (ks < 1 || ks > 8 || K / kBK < 2 * ks || (ks > 1 && (epi == EPI_SWIGLU || N % 4))) return 0;
+  if (ks < 1 || ks > 8 || K / kBK < 2 * ks || (ks > 1 && (epi == EPI_SWIGLU || epi == EPI_QKV || N % 4))) return 0;
   if (epi == EPI_SWIGLU) return bn == 256 && N % 2 == 0 && (N / 2) % 128 == 0;
+  if (epi == EPI_RESID) return bn == 256 && N % 256 == 0;
+  if (epi == EPI_QKV) return N % bn == 0;
   return epi >= EPI_NONE && epi <= EPI_BIAS_RELU && N % bn == 0;
 }
 
@@ -813,7 +1038,14 @@ int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks) {
 // N % bn == 0 (SwiGLU: bn = 256 and I = N/2 % 128 == 0), 16-B aligned X / W rows and
 // 8-B aligned output rows; any M >= 1.
 int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
-            int variant, bf16_t* out, long ldo, hipStream_t st, int ks, float* ws) {
+            int variant, bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, const LkEpi* ea_) {
+  const LkEpi ea = ea_ ? *ea_ : LkEpi{};
+  // fused-chain epilogue arguments (checked here: a bad pointer / shape would fault the device)
+  if (ea.ss_in && (ea.ss_nt < 1 || ea.ss_nt > 32 || ea.ss_ld < M || ea.inv_h <= 0.f)) return -1;
+  if (epi == EPI_RESID && (!ea.resid || !ea.ss_out || ea.ldr % 8 || ea.ss_out_ld < M)) return -1;
+  if (epi == EPI_QKV && (!ea.pos || !ea.cos_sin || ea.hd % 16 || ea.hd <= 0 ||
+                         N != (ea.hq + 2 * ea.hkv) * ea.hd || ((ea.kc || ea.vc) && (!ea.slots || ea.bs < 1))))
+    return -1;
   // 16-B epilogue stores / bias loads: output rows and the bias 16-B aligned
   if (!lk_gemm_supported(M, N, K, epi, bn, ks) || ldx % 8 || ldo % 8 || reinterpret_cast<uintptr_t>(out) % 16 ||
       (bias != nullptr && reinterpret_cast<uintptr_t>(bias) % 16))
@@ -825,14 +1057,15 @@ int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int 
     if (max_rows < kBM) return -1;
     for (long m0 = 0; m0 < M; m0 += max_rows) {
       const int mc = (int)min((long)M - m0, max_rows);
+      if (ea_) return -1;  // the fused-chain epilogues index whole-M side buffers
       const int rc = lk_gemm(x + m0 * ldx, ldx, w, bias, mc, N, K, epi, bn, variant, out + m0 * ldo, ldo, st, 1, nullptr);
       if (rc) return rc;
     }
     return 0;
   }
   if (variant < 0 || variant > 2) return -1;
-  const int rc = bn == 256 ? dispatch<4>(x, ldx, w, bias, M, N, K, epi, variant, ks, ws, out, ldo, st)
-                           : dispatch<3>(x, ldx, w, bias, M, N, K, epi, variant, ks, ws, out, ldo, st);
+  const int rc = bn == 256 ? dispatch<4>(x, ldx, w, bias, M, N, K, epi, variant, ks, ws, out, ldo, st, ea)
+                           : dispatch<3>(x, ldx, w, bias, M, N, K, epi, variant, ks, ws, out, ldo, st, ea);
   LK_CHECK_LAUNCH();
   return rc;
 }

@@ -61,8 +61,36 @@ int lk_xgmi_allreduce(bf16_t* const* data, unsigned* const* sig, int rank, int w
 // epilogue (not SwiGLU) -- for shapes with fewer tiles than CUs
 int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks = 1);
 int lk_gemm_streamk(int mode);
+// Fused prefill-chain epilogues of lk_gemm (the RMSNorm of the pre-norm decoder block folded
+// into its neighbouring GEMMs, the norm weight g folded into the consumer's weight rows):
+//   row scale (any of epi NONE / SWIGLU / QKV, when ss_in is set): acc *= rsqrt(sum_t
+//     ss_in[t * ss_ld + row] / H + eps) before the epilogue -- the consumer side of the norm;
+//   epi RESID (6): r = bf16(r + bf16(acc)) in place in resid [M, ldr], and the per-row partial
+//     sums of squares of the new r over this column tile into ss_out[tn * ss_out_ld + row]
+//     (tn = column tile of 256) -- the producer side; `out` is not written;
+//   epi QKV (7): out = the qkv row, q / k heads rotated with interleaved-pair RoPE (weights
+//     permuted at load: models/llama.py), K / V scattered into the paged cache at slots[row]
+//     (slot < 0: not cached).
+struct LkEpi {
+  const float* ss_in = nullptr;  // [nt][ss_ld] fp32 partial sums of squares (row scale)
+  int ss_nt = 0;                 // partials per row (<= 32)
+  long ss_ld = 0;                // row stride of one partial plane (>= M)
+  float inv_h = 0.f;             // 1 / hidden size
+  float eps = 0.f;
+  bf16_t* resid = nullptr;       // RESID: residual stream, updated in place
+  long ldr = 0;
+  float* ss_out = nullptr;       // RESID: [N / 256][ss_out_ld] partial sums of squares
+  long ss_out_ld = 0;
+  const int* pos = nullptr;      // QKV: positions [M]
+  const float* cos_sin = nullptr;  // QKV: [max_pos, D] = [cos(D/2) | sin(D/2)]
+  const int* slots = nullptr;    // QKV: cache slot per row (block * bs + offset), -1 = skip
+  bf16_t* kc = nullptr;          // QKV: paged caches [num_blocks, hkv, bs, hd]
+  bf16_t* vc = nullptr;
+  int bs = 0, hq = 0, hkv = 0, hd = 0;
+};
 int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
-            int variant, bf16_t* out, long ldo, hipStream_t st, int ks = 1, float* ws = nullptr);
+            int variant, bf16_t* out, long ldo, hipStream_t st, int ks = 1, float* ws = nullptr,
+            const LkEpi* ea = nullptr);
 
 // rope_kv.hip
 int lk_rope_kv(bf16_t* qkv, long qs, const int* positions, const float* cos_sin, long T, int Hq,

@@ -9,6 +9,7 @@ import torch
 from ..parallel.tp import SINGLE, TPGroup
 from .bert import EncoderModel
 from .configs import DECODERS, ENCODERS, DecoderConfig, EncoderConfig, decoder_config, encoder_config
+from . import llama
 from .llama import LlamaModel
 from .opt import OPTModel
 
@@ -30,9 +31,11 @@ def build_decoder(name: str | DecoderConfig, device="cpu", dtype=torch.bfloat16,
     cls = LlamaModel if cfg.arch == "llama" else OPTModel
     m = cls(cfg, tp, dtype, device)
     if checkpoint:
-        m.load_hf_state_dict(_load_safetensors_dir(checkpoint))
+        m.load_hf_state_dict(_load_safetensors_dir(checkpoint))  # folds on the GPU itself
     else:
         m.random_init(seed)
+        if isinstance(m, LlamaModel) and m.device.type == "cuda" and llama.FOLD_NORMS:
+            m.fold_norms()
     return m.eval()
 
 

@@ -7,6 +7,11 @@ MI355X layout decisions:
   * the residual stream is carried separately and folded into the RMSNorm kernel
     (``x = norm(res += y)``), so no standalone add pass ever touches HBM;
   * RoPE and the paged-KV write are one kernel on the QKV output;
+  * on the GPU the RMSNorm weights are folded into the next projection's weight columns at load
+    (``fold_norms``; q / k rows permuted so RoPE rotates adjacent pairs), so a prefill-sized step
+    runs each decoder block as four GEMMs and nothing else (``_forward_chain``): the norm is a
+    per-row rsqrt the consumer GEMM applies in its epilogue from partial sums of squares the
+    producing O / down GEMM wrote, and RoPE + the paged-KV write are the QKV GEMM's epilogue;
   * attention reads K/V from the paged cache (flash prefill / split-K decode);
   * tensor parallel: column-parallel QKV / gate_up, row-parallel o / down with one
     RCCL all-reduce each, vocab-parallel embedding + LM head;
@@ -26,6 +31,10 @@ from .. import ops
 from ..parallel.tp import SINGLE, TPGroup
 from .attention import AttnMeta, paged_attention
 from .configs import DecoderConfig, pad_vocab
+
+# GPU decoders fold their RMSNorm weights into the projections at load (LlamaModel.fold_norms);
+# LK_FOLD_NORMS=0 keeps the checkpoint layout (and with it the unfused prefill path)
+FOLD_NORMS = os.environ.get("LK_FOLD_NORMS", "1") != "0"
 
 
 class LlamaLayerWeights(nn.Module):
@@ -73,6 +82,10 @@ class LlamaModel(nn.Module):
         # steps of at least this many rows run sequence-parallel under TP (None: never)
         sp = os.environ.get("LK_SP_MIN_TOKENS")
         self.sp_min_tokens: Optional[int] = int(sp) if sp else None
+        # RoPE pairs: rotate_half (i, i + D/2) as in HF checkpoints, or adjacent (2i, 2i + 1) once
+        # fold_norms has permuted the q / k rows (what the fused QKV epilogue rotates)
+        self.rope_neox = True
+        self.folded = False
         max_pos = min(cfg.max_position, 1 << 17)
         self.register_buffer("cos_sin", ops.rope_cos_sin(max_pos, self.D, cfg.rope_theta,
                                                          cfg.rope_scaling, device=device),
@@ -91,6 +104,31 @@ class LlamaModel(nn.Module):
             g = torch.Generator(device=gen_dev).manual_seed(seed * 7919 + i * 104729 + self.tp.rank)
             p.copy_(torch.randn(p.shape, generator=g, device=gen_dev, dtype=torch.float32).mul_(std).to(p.dtype))
         self.lm_head[self.vocab_local:].zero_()
+        self.rope_neox, self.folded = True, False
+        return self
+
+    @torch.no_grad()
+    def fold_norms(self):
+        """Fold each block's RMSNorm weights into the projection that consumes the normed
+        activation (qkv <- input_norm, gate_up <- post_norm; the norms become 1) and permute
+        every q / k head's rows from rotate-half order to adjacent RoPE pairs (row 2i <- i,
+        2i + 1 <- i + D/2; q.k products are unchanged because q and k move alike, V untouched).
+        Mathematically the same model; it lets a prefill step skip every norm and RoPE pass
+        (``_forward_chain``).  Idempotent; re-loading weights resets it."""
+        if self.folded:
+            return self
+        D, hqk = self.D, self.hq + self.hkv
+        perm = torch.arange(D, device=self.device).view(2, D // 2).t().reshape(-1)
+        for L in self.layers:
+            H = L.qkv.shape[1]
+            w = L.qkv.view(-1, D, H)
+            w[:hqk] = w[:hqk].index_select(1, perm)
+            for wt, g in ((L.qkv, L.input_norm), (L.gate_up, L.post_norm)):
+                for r0 in range(0, wt.shape[0], 8192):  # chunks: no fp32 copy of a whole matrix
+                    blk = wt[r0:r0 + 8192]
+                    blk.copy_((blk.float() * g.float()[None, :]).to(wt.dtype))
+                g.fill_(1.0)
+        self.rope_neox, self.folded = False, True
         return self
 
     # ------------------------------------------------------------------ forward
@@ -110,6 +148,9 @@ class LlamaModel(nn.Module):
             return self._forward_sp(ids, meta, kv_caches)
         cfg = self.cfg
         res = self.embed_tokens(ids)
+        L0 = self.layers[0]
+        if self.folded and not self.tp.enabled and ops.prefill_chain_ok(res, L0.qkv, L0.o, L0.gate_up, L0.down):
+            return self._forward_chain(res, meta, kv_caches)
         x = ops.rmsnorm(res, self.layers[0].input_norm, cfg.norm_eps)
         attn_out = None
         n = len(self.layers)
@@ -117,7 +158,7 @@ class LlamaModel(nn.Module):
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
             qkv = ops.linear_rope_kv(x, L.qkv, meta.positions, self.cos_sin, self.hq, self.hkv, self.D, kc, vc,
-                                     meta.slots, True, False)
+                                     meta.slots, self.rope_neox, False)
             attn_out = paged_attention(qkv, kc, vc, meta, self.hq, self.hkv, self.D, self.scale, attn_out,
                                        cp_group=self.cp_group)
             nxt = self.layers[li + 1].input_norm if li + 1 < n else self.final_norm
@@ -133,6 +174,32 @@ class LlamaModel(nn.Module):
         if meta.logits_idx is not None:
             x = x.index_select(0, meta.logits_idx)
         return x
+
+    def _forward_chain(self, res: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
+        """Prefill-sized step of a folded model: per block QKV (+ input-norm scale, RoPE, KV
+        write) -> attention -> O (+ residual, sums of squares) -> gate_up (+ post-norm scale,
+        SwiGLU) -> down (+ residual, sums of squares); ``res`` is the residual stream, updated
+        in place.  The first block's input norm and the final norm (logit rows only) are the
+        only standalone norm passes."""
+        cfg = self.cfg
+        T, H = res.shape
+        eps = cfg.norm_eps
+        ss_post = ops.ss_buffer(T, H, res.device)
+        ss_in = ops.ss_buffer(T, H, res.device)
+        x, scale = ops.rmsnorm(res, self.layers[0].input_norm, eps), None
+        attn_out = None
+        for li, L in enumerate(self.layers):
+            kc, vc = kv_caches[li]
+            qkv = ops.linear_qkv_fused(x, L.qkv, scale, eps, meta.positions, self.cos_sin, self.hq, self.hkv,
+                                       self.D, kc, vc, meta.slots)
+            attn_out = paged_attention(qkv, kc, vc, meta, self.hq, self.hkv, self.D, self.scale, attn_out,
+                                       cp_group=self.cp_group)
+            ops.linear_resid(attn_out, L.o, res, ss_post)
+            a = ops.linear_swiglu_scaled(res, L.gate_up, ss_post, eps)
+            ops.linear_resid(a, L.down, res, ss_in)
+            x, scale = res, ss_in
+        h = res if meta.logits_idx is None else res.index_select(0, meta.logits_idx)
+        return ops.rmsnorm(h, self.final_norm, eps)
 
     def _forward_sp(self, ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
         """Sequence-parallel forward: this rank keeps rows [r*n, (r+1)*n) of the
@@ -159,7 +226,7 @@ class LlamaModel(nn.Module):
             qkv = ops.linear(xf, L.qkv)
             kc, vc = kv_caches[li]
             ops.rope_kv_(qkv, meta.positions, self.cos_sin, self.hq, self.hkv, self.D, kc, vc,
-                         meta.slots, True, False)
+                         meta.slots, self.rope_neox, False)
             attn_out = paged_attention(qkv, kc, vc, meta, self.hq, self.hkv, self.D, self.scale, attn_out,
                                        cp_group=self.cp_group)
             o = tp.reduce_scatter_rows(padded(ops.linear(attn_out, L.o)))
@@ -194,6 +261,7 @@ class LlamaModel(nn.Module):
         """Load HuggingFace ``LlamaForCausalLM`` tensors (q/k/v/gate/up fused and
         TP-sliced here)."""
         cfg, tp, D = self.cfg, self.tp, self.D
+        self.rope_neox, self.folded = True, False  # fresh HF-layout weights
 
         def t(name):
             return sd[name].to(self.dtype)
@@ -224,6 +292,8 @@ class LlamaModel(nn.Module):
             key = "lm_head.weight" if "lm_head.weight" in sd else "model.embed_tokens.weight"
             self.lm_head[: self.vocab_local].copy_(t(key)[self.vocab_lo:self.vocab_hi])
         self.lm_head[self.vocab_local:].zero_()
+        if self.device.type == "cuda" and FOLD_NORMS:
+            self.fold_norms()
         return self
 
     def gemm_shapes(self):

@@ -20,6 +20,7 @@ __all__ = [
     "kv_write", "paged_decode", "flash_prefill", "prefill_tiles", "knn_topk", "knn_merge",
     "pool_normalize", "row_norms", "select_tokens", "repeat_penalty_", "sample", "linear", "linear_swiglu",
     "decode_splits", "rope_cos_sin", "tune_gemm", "tune_decode", "gemm", "linear_add_rmsnorm", "linear_rope_kv",
+    "prefill_chain_ok", "linear_resid", "linear_qkv_fused", "linear_swiglu_scaled",
 ]
 
 rope_cos_sin = ref.rope_cos_sin
@@ -617,6 +618,96 @@ def linear_rope_kv(x, w, positions, cos_sin, Hq: int, Hkv: int, D: int, k_cache=
     qkv = linear(x, w)
     rope_kv_(qkv, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache, slots, neox, write_k_inplace)
     return qkv
+
+
+# ---------------------------------------------------------------- fused prefill chain
+# Prefill-sized steps (M > WS_MAX_M rows) of a decoder whose norm weights are folded into its
+# projections (LlamaModel.fold_norms) run the pre-norm block as four GEMMs and nothing else:
+#   QKV     x_or_r W_qkv'^T  * s_in(row)  -> interleaved RoPE, K / V into the paged cache  (epi QKV)
+#   O       r += attn W_o^T, partial sums of squares of r per 256 columns               (epi RESID)
+#   gate_up silu / mul of r W_gu'^T * s_post(row)                                       (epi SWIGLU)
+#   down    r += a W_down^T, partial sums of squares                                    (epi RESID)
+# s(row) = rsqrt(sum of the partials / H + eps) is recomputed by each consumer tile from the
+# producer's partials (no norm pass, no normalised activation in HBM, no RoPE / KV pass).
+# LK_PREFILL_CHAIN=0 keeps the round-3 path (GEMM -> rmsnorm / rope_kv kernels).
+PREFILL_CHAIN = os.environ.get("LK_PREFILL_CHAIN", "1") != "0"
+EPI_RESID, EPI_QKV = 6, 7
+
+
+def _cfg_of(M: int, N: int, K: int, epi: int):
+    """(schedule, bn, splits) of the prefill GEMM for this shape (tuned table, else default)."""
+    cfg = _GEMM_TABLE.get(_gemm_key(M, N, K, epi))
+    return cfg if cfg is not None else _gemm_default(M, N, K, epi)
+
+
+def _resid_cfg(M: int, N: int, K: int):
+    sched = _cfg_of(M, N, K, 0)
+    sched = sched[0] if sched is not None else _gemm_sched(K)
+    return sched, 256, _gemm_splits(M, N, K, 0, 256)
+
+
+def prefill_chain_ok(x, w_qkv, w_o, w_gate_up, w_down) -> bool:
+    """Whether a step of x.shape[0] rows can run the fused chain on the HIP kernels: prefill-sized,
+    every projection on the hand-written GEMM, the QKV GEMM unsplit (its epilogue is in-kernel)."""
+    if not (PREFILL_CHAIN and use_hip(x) and not GEMM_LIBRARY and x.dtype == torch.bfloat16):
+        return False
+    M = x.shape[0]
+    if M <= WS_MAX_M:
+        return False
+    L = lib()
+    N, K = w_qkv.shape
+    c = _cfg_of(M, N, K, 0)
+    if c is None or c[2] != 1 or not L.gemm_supported(M, N, K, EPI_QKV, c[1], 1):
+        return False
+    N, K = w_gate_up.shape
+    c = _cfg_of(M, N, K, 1)
+    if c is None or c[2] != 1 or not L.gemm_supported(M, N, K, 1, c[1], 1):
+        return False
+    for w in (w_o, w_down):
+        N, K = w.shape
+        _, bn, ks = _resid_cfg(M, N, K)
+        if not L.gemm_supported(M, N, K, EPI_RESID, bn, ks):
+            return False
+    return True
+
+
+def ss_buffer(M: int, N: int, device) -> torch.Tensor:
+    """Partial sums of squares of a [M, N] residual: [N / 256, M] f32."""
+    return torch.empty((N // 256, M), dtype=torch.float32, device=device)
+
+
+def linear_resid(x, w, residual, ss_out):
+    """residual += x W^T (bf16 rounding as the unfused linear -> add), and the partial sums of
+    squares of the new residual per 256 columns into ss_out [N / 256, >= M] (one GEMM)."""
+    if not use_hip(x):
+        return ref.linear_resid(x, w, residual, ss_out)
+    M, K = x.shape
+    N = w.shape[0]
+    sched, bn, ks = _resid_cfg(M, N, K)
+    return lib().gemm_fused(x, w, EPI_RESID, bn, None, sched, ks, resid=residual, ss_out=ss_out)
+
+
+def linear_swiglu_scaled(x, w_gate_up, ss, eps: float):
+    """silu(s * x Wg^T) * (s * x Wu^T), s = the folded norm's per-row rsqrt from ``ss``."""
+    if not use_hip(x):
+        return ref.gemm_scaled(x, w_gate_up, ss, x.shape[1], eps, swiglu=True)
+    M, K = x.shape
+    N = w_gate_up.shape[0]
+    sched, bn, _ = _cfg_of(M, N, K, 1)
+    return lib().gemm_fused(x, w_gate_up, 1, bn, None, sched, 1, ss_in=ss, eps=eps)
+
+
+def linear_qkv_fused(x, w, ss, eps: float, positions, cos_sin, Hq: int, Hkv: int, D: int,
+                     k_cache=None, v_cache=None, slots=None):
+    """qkv = s * x W^T (ss None: unscaled), interleaved-pair RoPE on q / k, K / V into the paged
+    cache: the QKV projection, the input norm's scale and rope_kv_ in one GEMM."""
+    if not use_hip(x):
+        return ref.qkv_fused(x, w, ss, x.shape[1], eps, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache, slots)
+    M, K = x.shape
+    N = w.shape[0]
+    sched, bn, _ = _cfg_of(M, N, K, 0)
+    return lib().gemm_fused(x, w, EPI_QKV, bn, None, sched, 1, ss_in=ss, eps=eps, positions=positions,
+                            cos_sin=cos_sin, slots=slots, k_cache=k_cache, v_cache=v_cache, hq=Hq, hkv=Hkv, hd=D)
 
 
 def softmax_scale(D: int) -> float:

@@ -310,3 +310,45 @@ def _topk_stable(l, K):
     """indices of the K largest (value desc, index asc)."""
     vals, idx = torch.sort(l, descending=True, stable=True)
     return idx[:K].tolist()
+
+
+# ---------------------------------------------------------------- fused prefill chain
+# (csrc/gemm.hip LkEpi: the decoder block's RMSNorm folded into its neighbouring GEMMs)
+def ss_partials(r: torch.Tensor, cols: int = 256) -> torch.Tensor:
+    """Per-``cols``-column partial sums of squares of r [M, N]: [N / cols, M] f32."""
+    M, N = r.shape
+    return r.float().pow(2).reshape(M, N // cols, cols).sum(-1).t().contiguous()
+
+
+def row_scale(ss: torch.Tensor, H: int, eps: float) -> torch.Tensor:
+    """[M] f32 rsqrt(mean of squares + eps) from the partials [nt, >= M]."""
+    return torch.rsqrt(ss.float().sum(0) / H + eps)
+
+
+def linear_resid(x, w, residual, ss_out):
+    """residual = bf16(residual + bf16(x w^T)) in place; ss_out [N/256, >= M] = its partials."""
+    y = (x.float() @ w.float().t()).to(x.dtype)
+    residual.copy_((residual.float() + y.float()).to(residual.dtype))
+    M = residual.shape[0]
+    ss_out[:, :M] = ss_partials(residual)
+    return residual
+
+
+def gemm_scaled(x, w, ss, H, eps, swiglu=False):
+    """x w^T with each row scaled by the folded norm's rsqrt (ss None: unscaled); SwiGLU:
+    silu(g) * u on the scaled, bf16-rounded halves."""
+    acc = x.float() @ w.float().t()
+    if ss is not None:
+        acc = acc * row_scale(ss, H, eps)[: x.shape[0], None]
+    if not swiglu:
+        return acc.to(x.dtype)
+    I = w.shape[0] // 2
+    g, u = acc[:, :I].to(x.dtype).float(), acc[:, I:].to(x.dtype).float()
+    return ((g * torch.sigmoid(g)).to(x.dtype).float() * u).to(x.dtype)
+
+
+def qkv_fused(x, w, ss, H, eps, positions, cos_sin, Hq, Hkv, D, k_cache=None, v_cache=None, slots=None):
+    """The QKV GEMM's fused epilogue: scaled, bf16-rounded projection, interleaved-pair RoPE on
+    q and k (written back into the row), K / V into the paged cache."""
+    qkv = gemm_scaled(x, w, ss, H, eps)
+    return rope_kv_(qkv, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache, slots, neox=False, write_k_inplace=True)

@@ -256,3 +256,33 @@ def test_forced_reference_fails_loudly_not_silently():
         assert not ops.use_hip(x)
     finally:
         del os.environ["LK_FORCE_REFERENCE"]
+
+
+def test_fused_prefill_chain_matches_hf(monkeypatch):
+    """A folded GPU model runs prefill-sized steps (> 256 rows) as the fused GEMM chain (RoPE +
+    KV write in the QKV epilogue, norms folded into the GEMMs) -- logits vs HF fp32 -- and the
+    same greedy tokens as the unfused path (LK_PREFILL_CHAIN=0), up to near-ties."""
+    from llm_kubernetes_minikube_sharp4dev_amd import ops
+
+    hf, m = _gpu_llama()
+    assert m.folded and not m.rope_neox
+    prompts = [list(range(3 + i, 3 + i + 90)) for i in range(4)]  # 360 prefill rows in one step
+    calls = []
+    real = m._forward_chain
+    monkeypatch.setattr(m, "_forward_chain", lambda *a, **k: calls.append(1) or real(*a, **k))
+    eng = _engine(m, use_graphs=False)
+    for p in prompts:
+        eng.add_request(p, SamplingParams.greedy(1))
+    eng._drain_inbox()
+    rows, lg = eng.runner.forward_logits(eng.scheduler.schedule().items)
+    assert calls, "prefill chain not taken"
+    for (seq, _), got in zip(rows, lg):
+        with torch.no_grad():
+            want = hf(torch.tensor([seq.prompt_ids])).logits[0, -1]
+        got = got.float().cpu()
+        assert (got - want).abs().max().item() < 0.05 * want.abs().max().item() + 0.05
+        assert torch.nn.functional.cosine_similarity(got, want, dim=0) > 0.999
+    fused = [s.output_ids for s in _engine(m, use_graphs=True).generate(prompts, SamplingParams.greedy(10))]
+    monkeypatch.setattr(ops, "PREFILL_CHAIN", False)
+    plain = [s.output_ids for s in _engine(m, use_graphs=True).generate(prompts, SamplingParams.greedy(10))]
+    _assert_same_or_near_tie(hf, prompts, fused, plain)

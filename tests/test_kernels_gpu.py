@@ -761,3 +761,91 @@ def test_tune_decode_routes_by_measurement(hip):
     finally:
         ops._DECODE_TABLE.clear()
         ops._DECODE_TABLE.update(saved)
+
+
+# ---------------------------------------------------------------- fused prefill chain epilogues
+def _qkv_setup(M, Hq=32, Hkv=8, D=128, H=4096, nb=600, bs=16, seed=0):
+    torch.manual_seed(seed)
+    x = torch.randn(M, H, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn((Hq + 2 * Hkv) * D, H, device=DEV, dtype=torch.bfloat16) * 0.02
+    pos = torch.randint(0, 4000, (M,), device=DEV, dtype=torch.int32)
+    cs = ref.rope_cos_sin(8192, D, 500000.0, device=DEV)
+    perm = torch.randperm(nb * bs, device=DEV)[:M].to(torch.int32)
+    slots = torch.where(torch.rand(M, device=DEV) < 0.1, torch.full_like(perm, -1), perm)
+    kc = torch.zeros(nb, Hkv, bs, D, device=DEV, dtype=torch.bfloat16)
+    return x, w, pos, cs, slots, kc, kc.clone()
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(300, 1024, 512, 1), (1000, 4096, 1024, 1), (2304, 4096, 14336, 3),
+                                          (777, 2048, 4096, 2), (4352, 4096, 4096, 1)])
+def test_gemm_resid_epilogue(hip, M, N, K, splits):
+    """RESID (producer side of the folded norm): r = bf16(r + bf16(x W^T)) in place and the
+    per-256-column partial sums of squares of the new r, in-kernel and through the split-K
+    reduce, M tails; 4352 x 4096 engages stream-K (17 x 16 tiles)."""
+    torch.manual_seed(M + N + splits)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.02
+    r = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    r_ref, ss_ref = r.clone(), torch.zeros(N // 256, M, device=DEV)
+    ref.linear_resid(x, w, r_ref, ss_ref)
+    ss = torch.full((N // 256, M), float("nan"), device=DEV)
+    n0 = hip.gemm_streamk(-2)
+    hip.gemm_fused(x, w, 6, 256, None, 2, splits, resid=r, ss_out=ss)
+    torch.cuda.synchronize()
+    _close(r, r_ref, 0.02, 0.01, f"resid M{M} N{N} K{K} s{splits}")
+    _close(ss, ss_ref, 0.5, 0.01, f"ss partials M{M} N{N}")
+    assert hip.gemm_streamk(-1) == 0
+    if M == 4352:
+        assert hip.gemm_streamk(-2) > n0, "stream-K did not engage"
+
+
+@pytest.mark.parametrize("M", [300, 2048, 4352])
+@pytest.mark.parametrize("scaled", [False, True])
+def test_gemm_swiglu_row_scale(hip, M, scaled):
+    """SwiGLU epilogue with the folded post-norm's row scale s = rsqrt(sum(ss) / H + eps)."""
+    torch.manual_seed(M)
+    H, I = 4096, 1792
+    r = torch.randn(M, H, device=DEV, dtype=torch.bfloat16) * 3
+    w = torch.randn(2 * I, H, device=DEV, dtype=torch.bfloat16) * 0.02
+    ss = ref.ss_partials(r) if scaled else None
+    y = hip.gemm_fused(r, w, 1, 256, None, 2, 1, ss_in=ss, eps=1e-5)
+    y_ref = ref.gemm_scaled(r, w, ss, H, 1e-5, swiglu=True)
+    _close(y, y_ref, 0.03, 0.02, f"swiglu scaled={scaled} M{M}")
+
+
+@pytest.mark.parametrize("M,bn", [(300, 192), (1111, 256), (4352, 192), (2560, 256)])
+@pytest.mark.parametrize("scaled", [False, True])
+def test_gemm_qkv_epilogue(hip, M, bn, scaled):
+    """QKV epilogue: row scale, interleaved-pair RoPE on q / k, K / V into the paged cache at
+    slots[row] (-1 skipped), the qkv row written back -- vs GEMM -> rope_kv_ in fp32; 4352 rows
+    at bn 192 engage stream-K."""
+    x, w, pos, cs, slots, kc, vc = _qkv_setup(M, seed=M + bn)
+    ss = ref.ss_partials(x) if scaled else None
+    kc2, vc2 = kc.clone(), vc.clone()
+    out = hip.gemm_fused(x, w, 7, bn, None, 2, 1, ss_in=ss, eps=1e-5, positions=pos, cos_sin=cs, slots=slots,
+                         k_cache=kc, v_cache=vc, hq=32, hkv=8, hd=128)
+    want = ref.qkv_fused(x, w, ss, 4096, 1e-5, pos, cs, 32, 8, 128, kc2, vc2, slots)
+    torch.cuda.synchronize()
+    _close(out, want, 0.03, 0.02, f"qkv M{M} bn{bn}")
+    _close(kc, kc2, 0.03, 0.02, "k cache")
+    _close(vc, vc2, 0.03, 0.02, "v cache")
+    assert hip.gemm_streamk(-1) == 0
+
+
+def test_gemm_qkv_epilogue_layout(hip):
+    """Asymmetric exact data through the QKV epilogue: x = I-rows, W rows = distinct ramps, RoPE at
+    position 0 (identity): every output column / cache element lands where the reference puts it."""
+    M, Hq, Hkv, D, H = 512, 4, 2, 128, 1024
+    x = torch.zeros(M, H, device=DEV, dtype=torch.bfloat16)
+    x[torch.arange(M), torch.arange(M) % H] = 1
+    N = (Hq + 2 * Hkv) * D
+    w = ((torch.arange(N, device=DEV)[:, None] * 7 + torch.arange(H, device=DEV)[None, :]) % 251 - 125).to(torch.bfloat16)
+    pos = torch.zeros(M, device=DEV, dtype=torch.int32)
+    cs = ref.rope_cos_sin(16, D, 10000.0, device=DEV)
+    slots = torch.arange(M, device=DEV, dtype=torch.int32)
+    kc = torch.zeros(M // 16, Hkv, 16, D, device=DEV, dtype=torch.bfloat16)
+    vc, kc2, vc2 = kc.clone(), kc.clone(), kc.clone()
+    out = hip.gemm_fused(x, w, 7, 256, None, 2, 1, positions=pos, cos_sin=cs, slots=slots, k_cache=kc, v_cache=vc,
+                         hq=Hq, hkv=Hkv, hd=D)
+    want = ref.qkv_fused(x, w, None, H, 1e-5, pos, cs, Hq, Hkv, D, kc2, vc2, slots)
+    assert torch.equal(out.cpu(), want.cpu()) and torch.equal(kc.cpu(), kc2.cpu()) and torch.equal(vc.cpu(), vc2.cpu())

@@ -293,3 +293,82 @@ def test_lib_path_ab_knob_loads_the_named_build():
     out = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True,
                          timeout=300).stdout.strip().splitlines()[-1]
     assert out == so[0], out
+
+
+def _first_step_logits(m, prompts):
+    eng = _engine(m)
+    for p in prompts:
+        eng.add_request(p, SamplingParams.greedy(1))
+    eng._drain_inbox()
+    rows, lg = eng.runner.forward_logits(eng.scheduler.schedule().items)
+    return lg
+
+
+def test_folded_norms_and_fused_chain_match_hf(monkeypatch):
+    """fold_norms (norm weights into qkv / gate_up, q / k rows to adjacent RoPE pairs) is the same
+    model, and the fused prefill chain (_forward_chain: scale-in-epilogue GEMMs, RESID partial
+    sums of squares, RoPE + KV write in the QKV epilogue) computes the same logits and greedy
+    tokens as HF -- fp32 reference ops on the CPU (the GPU test runs the HIP epilogues)."""
+    from llm_kubernetes_minikube_sharp4dev_amd import ops
+
+    hcfg = transformers.LlamaConfig(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                                    num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=1024,
+                                    rope_theta=10000.0, rms_norm_eps=1e-5, tie_word_embeddings=False)
+    torch.manual_seed(0)
+    hf = transformers.LlamaForCausalLM(hcfg).eval()
+    cfg = DecoderConfig("t", "llama", 2, 256, 4, 2, 64, 512, 512, max_position=1024, rope_theta=10000.0)
+    sd = hf.state_dict()
+    for k in list(sd):  # non-trivial norm weights, so the fold is exercised
+        if k.endswith("norm.weight"):
+            sd[k] = 1 + 0.1 * torch.randn_like(sd[k])
+    hf.load_state_dict(sd)
+    prompts = [[5, 17, 99, 3, 250, 7, 7, 1, 400, 33, 21, 8, 2, 9, 11, 60, 61, 62, 63], list(range(30, 70))]
+    m = build_decoder(cfg, dtype=torch.float32)
+    m.load_hf_state_dict(sd)
+    assert not m.folded  # CPU: checkpoint layout
+    with torch.no_grad():
+        want = torch.stack([hf(torch.tensor([p])).logits[0, -1] for p in prompts])
+    plain = _first_step_logits(m, prompts)
+    m.fold_norms()
+    assert m.folded and not m.rope_neox and torch.all(m.layers[0].input_norm == 1)
+    folded = _first_step_logits(m, prompts)
+    calls = []
+    real = m._forward_chain
+
+    def spy(*a, **k):
+        calls.append(1)
+        return real(*a, **k)
+
+    monkeypatch.setattr(ops, "prefill_chain_ok", lambda *a: True)
+    monkeypatch.setattr(m, "_forward_chain", spy)
+    chained = _first_step_logits(m, prompts)
+    assert calls, "the fused chain did not run"
+    for got in (plain, folded, chained):
+        assert torch.allclose(got, want, atol=2e-4, rtol=2e-4), (got - want).abs().max()
+    seqs = _engine(m).generate(prompts, SamplingParams.greedy(8))
+    with torch.no_grad():
+        for p, s in zip(prompts, seqs):
+            ref = hf.generate(torch.tensor([p]), max_new_tokens=8, do_sample=False)[0, len(p):].tolist()
+            assert s.output_ids == ref
+
+
+def test_fused_chain_reference_ops():
+    """The CPU oracles of the fused epilogues: RESID partial sums of squares per 256 columns and
+    the consumer's row scale reproduce RMSNorm; the QKV oracle is GEMM -> interleaved rope_kv_."""
+    from llm_kubernetes_minikube_sharp4dev_amd.ops import reference as R
+
+    torch.manual_seed(1)
+    M, H = 37, 512
+    r = torch.randn(M, H)
+    x = torch.randn(M, 256)
+    w = torch.randn(H, 256) * 0.05
+    ss = torch.zeros(H // 256, 64)
+    r2 = r.clone()
+    R.linear_resid(x, w, r2, ss)
+    assert torch.allclose(r2, r + x @ w.t(), atol=1e-5)
+    s = R.row_scale(ss, H, 1e-5)[:M]
+    assert torch.allclose(s, torch.rsqrt(r2.pow(2).mean(-1) + 1e-5), rtol=1e-5)
+    wg = torch.randn(64, H) * 0.05
+    y = R.gemm_scaled(r2, wg, ss, H, 1e-5)
+    normed = r2 * torch.rsqrt(r2.pow(2).mean(-1, keepdim=True) + 1e-5)
+    assert torch.allclose(y, normed @ wg.t(), atol=1e-4)
