@@ -123,6 +123,9 @@ def parse():
                     help="tokenizer.json to use instead of the built-in one (e.g. benchmarks/data/"
                          "bpe_runbooks_r1.json, the round-1 tokenizer trained on the synthetic corpus itself, "
                          "for like-for-like comparisons with round-1 numbers)")
+    ap.add_argument("--collective-floor", default=None,
+                    help="with --tp-sim: JSON of the measured per-call TP tail collective floor "
+                         "(benchmarks/xgmi_floor.py; default profiles/r4_tp_collectives/floor_tp<N>_h<H>.json)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -178,6 +181,7 @@ def main():
     from llm_kubernetes_minikube_sharp4dev_amd.k8s.fake import FakeCluster
     from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder, build_encoder
     from llm_kubernetes_minikube_sharp4dev_amd.models.tokenizer import builtin_tokenizer
+    from llm_kubernetes_minikube_sharp4dev_amd import ops
     from llm_kubernetes_minikube_sharp4dev_amd.ops import _ext
     from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp import SINGLE, SimulatedTPGroup, new_tp_groups
     from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp_engine import (make_tp_engine, run_tp_worker,
@@ -299,9 +303,17 @@ def main():
     results, trace, elapsed, tim_setup = [], [], 0.0, 0.0
     load, load_host, tp_ctrl, prompt_len = None, {}, {}, {}
 
+    # --tp T: the corpus is sharded over the TP group (each rank scans 1/T of it; SURVEY 2.4
+    # "sharded kNN index"), the leader merges the per-rank top-k
+    knn_shard = None
+    if args.tp > 1:
+        from llm_kubernetes_minikube_sharp4dev_amd.parallel.sharded_index import ShardedKnnIndex
+
+        knn_shard = ShardedKnnIndex.for_tp(corpus, tpg)
     if not leader:
-        # TP follower: execute the driver's steps (and its barriers) until it says stop
-        run_tp_worker(llm, tpg, **runner_kw)
+        # TP follower: execute the driver's steps (and its barriers, sharded searches) until it says stop
+        del corpus, index
+        run_tp_worker(llm, tpg, knn=knn_shard, **runner_kw)
     else:
         # decode-graph buckets: one row per running request, plus the rows of jump-forward
         # extend chunks under the tool-call grammar
@@ -314,6 +326,19 @@ def main():
             engine = LLMEngine(llm, tok, **runner_kw, **engine_kw)
             if runner_kw["use_graphs"]:
                 engine.runner.capture_all(max_batch=graph_rows, variants=(args.sampling == "greedy" and not args.constrained,))
+        knn_info = {"mode": "single"}
+        if knn_shard is not None:
+            from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp_engine import tp_knn_search
+
+            # the sharded search must return exactly the single-scan top-k (ties by id)
+            qv = corpus[torch.arange(0, min(64, n)) * max(1, n // 64)].clone()
+            qv[1:8] += 0.01 * torch.randn_like(qv[1:8])
+            cs, ci = ops.knn_topk(corpus, index.gpu_tensors()[1], qv, ops.row_norms(qv), 6)
+            ss, si = tp_knn_search(engine, knn_shard, qv, 6)
+            knn_info = {"mode": f"sharded over tp{args.tp} ({knn_shard.corpus.shape[0]} rows per rank)",
+                        "matches_single_scan": bool(torch.equal(si.cpu().long(), ci.cpu().long()))}
+            index.set_sharded(lambda q, k: tp_knn_search(engine, knn_shard, q, k))
+            log(rank, f"kNN: {knn_info}")
         k8s = FakeCluster.default()
         rag = RagAgentPipeline(index, engine, tok, k8s, cfg)
         agent = AgentPipeline(engine, tok, k8s, cfg)
@@ -466,6 +491,11 @@ def main():
                       if any(r.timings and r.timings.get(k) is not None for r in results)}
         par = f"dp{n_replicas}" if args.tp == 1 else f"tp{args.tp}" + (f"xdp{n_replicas}" if n_replicas > 1 else "")
         sim = {}
+        if args.tp > 1 and getattr(tpg, "xgmi", None) is not None:
+            # the measured collective table the TP group routes by (parallel/xgmi_ar.py tune)
+            sim["tp_collectives"] = {"routes": {str(k): v for k, v in tpg.xgmi.table.items()},
+                                     "us_by_rows": {str(k): v for k, v in tpg.xgmi.timings.items()},
+                                     "mode": "ipc-only" if tpg.ipc_only else "auto (ipc1 / ipc2 / rccl measured)"}
         if args.tp_sim > 1:
             par = f"tp{args.tp_sim}-sim (rank-0 shard on one GPU, collectives elided)"
             # what the real group moves per rank: every step's rows through 2 all-reduces per layer
@@ -479,6 +509,18 @@ def main():
                    "allreduce_calls": ar_calls,
                    "rows_per_step": round(rows / max(1, len(trace)), 1),
                    "decode_only_steps": len(dec_only), "mixed_steps": len(mixed)}
+            floor = _collective_floor(args.collective_floor, args.tp_sim, lc.hidden)
+            if floor is not None:
+                # per-step collective time the real group would add, from the measured per-call
+                # floor (kernel + handshake of the routed algorithm at that row count, W ranks on one
+                # device: no link-bandwidth term): 2 tails per layer + the embedding all-reduce
+                per_call = [_floor_us(floor, t[0] + t[1]) for t in trace]
+                tot_s = sum(per_call) * (2 * lc.num_layers + 1) / 1e6
+                sim["collective_floor"] = {
+                    "source": floor["_path"], "ms_per_step": round(1e3 * tot_s / max(1, len(trace)), 3),
+                    "timed_window_s": round(tot_s, 3), "vs_elapsed": round(tot_s / elapsed, 3) if elapsed else None,
+                    "decode_only_ms_per_step": round(1e3 * (2 * lc.num_layers + 1) * sum(
+                        _floor_us(floor, t[0] + t[1]) for t in dec_only) / 1e6 / max(1, len(dec_only)), 3)}
         out = {
             "metric": METRICS[args.workload].format(model=MODEL_NAMES.get(args.model, args.model)),
             "value": round(qps, 3),
@@ -530,6 +572,7 @@ def main():
                 "engine_steps_per_request": steps_acct,
                 "step_mix_rank0": step_mix,
                 "index_build_s": round(t_index, 2),
+                "knn": knn_info,
                 "setup_s": round(tim_setup, 1),
                 "http_status_counts_rank0": statuses,
                 **sim,
@@ -542,6 +585,28 @@ def main():
                 f.write(line + "\n")
     if world > 1:
         dist.destroy_process_group()
+
+
+def _collective_floor(path, world: int, hidden: int):
+    path = path or os.path.join(ROOT, "profiles", "r4_tp_collectives", f"floor_tp{world}_h{hidden}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    d["_path"] = os.path.relpath(path, ROOT)
+    return d
+
+
+def _floor_us(floor: dict, rows: int) -> float:
+    """Per-call floor (us) of the routed algorithm at ``rows`` rows: the smallest measured bucket
+    >= rows, linear in rows past the largest."""
+    tab = {int(k): v for k, v in floor["us_by_rows"].items()}
+    route = {int(k): a for k, a in floor["route"].items()}
+    for b in sorted(tab):
+        if rows <= b:
+            return tab[b][route[b]]
+    b = max(tab)
+    return tab[b][route[b]] * rows / b
 
 
 def _jump_forward_on() -> bool:

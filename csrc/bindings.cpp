@@ -752,6 +752,21 @@ struct XgmiAr {
                                 cur_stream());
     CHECK_RC(rc, "xgmi_allreduce2");
   }
+  // raw-byte all-gather (root < 0: out = world x in) or broadcast from root (out = root's in)
+  void gather(const at::Tensor& in, at::Tensor& out, int64_t root) {
+    CHECK_CUDA(in); CHECK_CUDA(out); CHECK_CONTIG(in); CHECK_CONTIG(out);
+    const long nb = in.numel() * in.element_size();
+    TORCH_CHECK(nb % 16 == 0 && (size_t)nb <= bytes, "xgmi_gather: bytes must be a multiple of 16 and fit the staging buffer");
+    TORCH_CHECK(out.numel() * out.element_size() == (root < 0 ? world * nb : nb), "xgmi_gather: out size");
+    TORCH_CHECK(root < world, "xgmi_gather: root");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(in.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+                "xgmi_gather: 16-B alignment");
+    for (int r = 0; r < world; ++r) TORCH_CHECK(pdata[r] && psig[r], "xgmi_ar: open() not called");
+    int rc = lk_xgmi_gather(reinterpret_cast<bf16_t* const*>(pdata.data()), reinterpret_cast<unsigned* const*>(psig.data()),
+                            rank, world, (int)root, in.data_ptr(), out.data_ptr(), nb, err, cur_stream());
+    CHECK_RC(rc, "xgmi_gather");
+  }
+  int64_t max_bytes() const { return (int64_t)bytes; }
   int error() const {
     int h = 0;
     TORCH_CHECK(hipMemcpy(&h, err, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess, "xgmi_ar: read error word");
@@ -775,6 +790,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("all_reduce_rmsnorm", &XgmiAr::all_reduce_rmsnorm)
       .def("all_reduce2", &XgmiAr::all_reduce2, "", py::arg("x"), py::arg("out"), py::arg("residual") = py::none(),
            py::arg("w") = py::none(), py::arg("eps") = 1e-5)
+      .def("gather", &XgmiAr::gather, "", py::arg("in"), py::arg("out"), py::arg("root") = -1)
+      .def("max_bytes", &XgmiAr::max_bytes)
       .def("error", &XgmiAr::error)
       .def_readonly("bytes", &XgmiAr::bytes);
   m.doc() = "gfx950 (MI355X) HIP kernel library";

@@ -45,6 +45,8 @@ int lk_ws_scores_f32(const bf16_t* x, long ldx, const bf16_t* w, int M, long N, 
 
 // xgmi_allreduce.hip (one-shot / two-shot all-reduce over IPC-mapped peer buffers, K14)
 int lk_xgmi_ar_sig_words();
+int lk_xgmi_gather(bf16_t* const* data, unsigned* const* sig, int rank, int world, int root, const void* in,
+                   void* out, long nbytes, int* err, hipStream_t st);
 int lk_xgmi_allreduce2(bf16_t* const* data, unsigned* const* sig, long red_off, int rank, int world,
                        const bf16_t* in, bf16_t* residual, const bf16_t* w, bf16_t* out, int T, int H, float eps,
                        int norm, int* err, hipStream_t st);

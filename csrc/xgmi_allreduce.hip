@@ -35,6 +35,7 @@
 // with no host-side state.  Every spin is bounded: a peer that never arrives sets the
 // error word and the kernel exits instead of hanging the device.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "kernels.h"
@@ -343,6 +344,55 @@ __global__ __launch_bounds__(NW * 64) void xgmi_ar2_kernel(ArPeers p, long red_o
   handshake(p, rank, world, 2, epoch, err);
 }
 
+// All-gather / broadcast of raw bytes through the same peer mappings (a TP group that runs every
+// collective on the IPC path -- e.g. several ranks on one device, where RCCL refuses a
+// communicator): root < 0: every rank stages its nv 16-B vectors, handshake, each workgroup copies
+// its slice of EVERY rank's part into out[r * nv ..], barrier-out; root >= 0: broadcast -- only
+// root stages, every rank copies root's part into out (root's own out may alias in).
+__global__ __launch_bounds__(kArThreads) void xgmi_gather_kernel(ArPeers p, int rank, int world, int root,
+                                                                 const uint4_t* __restrict__ in, uint4_t* out, long nv,
+                                                                 int* err) {
+  const long per = (nv + gridDim.x - 1) / gridDim.x;
+  const long v0 = (long)blockIdx.x * per, v1 = min(nv, v0 + per);
+  unsigned* ctr = p.sig[rank] + kPhases * kArBlocks * kMaxRanks + blockIdx.x;
+  __shared__ unsigned s_epoch;
+  if (threadIdx.x == 0) {
+    s_epoch = *ctr + 1;
+    *ctr = s_epoch;
+  }
+  __syncthreads();
+  const unsigned epoch = s_epoch;
+  uint4_t* mine = reinterpret_cast<uint4_t*>(p.data[rank]);
+  if (root < 0 || rank == root)
+    for (long v = v0 + threadIdx.x; v < v1; v += kArThreads) mine[v] = in[v];
+  publish();
+  if (!handshake(p, rank, world, 0, epoch, err)) return;
+  acquire();
+  if (root < 0) {
+    for (int r = 0; r < world; ++r) {
+      const uint4_t* src = reinterpret_cast<const uint4_t*>(p.data[r]);
+      for (long v = v0 + threadIdx.x; v < v1; v += kArThreads) out[r * nv + v] = src[v];
+    }
+  } else if (rank != root || out != in) {
+    const uint4_t* src = reinterpret_cast<const uint4_t*>(p.data[root]);
+    for (long v = v0 + threadIdx.x; v < v1; v += kArThreads) out[v] = src[v];
+  }
+  __syncthreads();
+  handshake(p, rank, world, 1, epoch, err);  // every peer finished reading our staged part
+}
+
+// workgroups per call cap (LK_XGMI_AR_BLOCKS, default kArBlocks): several ranks sharing ONE
+// device (the single-GPU multi-rank tests) need every rank's spinning workgroups co-resident;
+// every rank must use the same value (the per-workgroup epochs are indexed by block)
+int block_cap() {
+  static const int cap = [] {
+    const char* e = getenv("LK_XGMI_AR_BLOCKS");
+    const int v = e ? atoi(e) : kArBlocks;
+    return v < 1 ? 1 : (v > kArBlocks ? kArBlocks : v);
+  }();
+  return cap;
+}
+
 }  // namespace
 
 // out = RMSNorm(allreduce(in) + residual) * w, residual updated in place; in / residual / out
@@ -359,7 +409,7 @@ int lk_xgmi_allreduce_rmsnorm(bf16_t* const* data, unsigned* const* sig, int ran
     p.data[r] = data[r];
     p.sig[r] = sig[r];
   }
-  const int blocks = std::min(kArBlocks, T);
+  const int blocks = std::min(block_cap(), T);
 #define CALL(MV, NW) \
   xgmi_ar_rmsnorm_kernel<MV, NW><<<blocks, NW * 64, 0, st>>>(p, rank, world, in, residual, w, out, T, H, eps, err)
   ROW_DISPATCH(H, CALL);
@@ -384,7 +434,7 @@ int lk_xgmi_allreduce2(bf16_t* const* data, unsigned* const* sig, long red_off, 
     p.sig[r] = sig[r];
   }
   const int n = (T + world - 1) / world;
-  const int blocks = std::min(kArBlocks, n);
+  const int blocks = std::min(block_cap(), n);
 #define CALL(MV, NW)                                                                                              \
   if (norm)                                                                                                       \
     xgmi_ar2_kernel<MV, NW, true><<<blocks, NW * 64, 0, st>>>(p, red_off, rank, world, in, residual, w, out, T, H, \
@@ -413,8 +463,27 @@ int lk_xgmi_allreduce(bf16_t* const* data, unsigned* const* sig, int rank, int w
     p.sig[r] = sig[r];
   }
   const long nv = n / 8;
-  const int blocks = (int)std::min<long>(kArSlices, std::max<long>(1, (nv + kArThreads - 1) / kArThreads));
+  const int blocks = (int)std::min<long>(std::min(kArSlices, block_cap()), std::max<long>(1, (nv + kArThreads - 1) / kArThreads));
   xgmi_allreduce_kernel<<<blocks, kArThreads, 0, st>>>(p, rank, world, in, out, n, err);
+  LK_CHECK_LAUNCH();
+  return 0;
+}
+
+// nbytes % 16 == 0, nbytes <= staging bytes (checked by the caller); out holds world * nbytes
+// (all-gather, root < 0) or nbytes (broadcast from root).  Same launch on every rank.
+int lk_xgmi_gather(bf16_t* const* data, unsigned* const* sig, int rank, int world, int root, const void* in,
+                   void* out, long nbytes, int* err, hipStream_t st) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || root >= world || nbytes % 16) return -1;
+  if (nbytes == 0) return 0;
+  ArPeers p{};
+  for (int r = 0; r < world; ++r) {
+    p.data[r] = data[r];
+    p.sig[r] = sig[r];
+  }
+  const long nv = nbytes / 16;
+  const int blocks = (int)std::min<long>(std::min(kArSlices, block_cap()), std::max<long>(1, (nv + kArThreads - 1) / kArThreads));
+  xgmi_gather_kernel<<<blocks, kArThreads, 0, st>>>(p, rank, world, root, reinterpret_cast<const uint4_t*>(in),
+                                                     reinterpret_cast<uint4_t*>(out), nv, err);
   LK_CHECK_LAUNCH();
   return 0;
 }

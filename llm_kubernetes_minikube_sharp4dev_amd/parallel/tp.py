@@ -31,30 +31,42 @@ class TPGroup:
     # ranks by new_tp_groups (torch requires every rank to join every new_group call)
     ctrl: Optional[object] = None
     ranks: Optional[list] = None
-    # optional one-shot xGMI all-reduce (parallel.xgmi_ar, K14) for messages that fit it
+    # xGMI collectives over IPC-mapped peer memory (parallel.xgmi_ar, K14): the fused
+    # all-reduce + norm tails by the start-up-measured table, all-gathers / broadcasts
     xgmi: Optional[object] = None
+    # every device collective on the IPC path, never RCCL (several ranks on one device, where
+    # RCCL refuses the communicator; LK_TP_COLLECTIVES=ipc)
+    ipc_only: bool = False
 
     @property
     def enabled(self) -> bool:
         return self.size > 1
 
+    def _ipc(self, t: torch.Tensor) -> bool:
+        return self.xgmi is not None and t.is_cuda
+
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
-            if self.xgmi is not None and self.xgmi.eligible(t):
-                return self.xgmi.all_reduce_(t)
+            if self._ipc(t):
+                if self.ipc_only:
+                    return self.xgmi.all_reduce_(t)
+                rows = t.shape[0] if t.dim() >= 2 else 1
+                if self.xgmi.eligible(t) and self.xgmi.algo(rows, t.numel() * 2) != "rccl":
+                    return self.xgmi.all_reduce_(t)
             dist.all_reduce(t, group=self.group)
         return t
 
     def all_reduce_rmsnorm(self, x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
                            eps: float) -> torch.Tensor:
         """RMSNorm(allreduce(x) + residual) * w, residual updated in place: the tail of every
-        row-parallel projection.  With the one-shot xGMI path attached this is ONE kernel
-        (csrc/xgmi_allreduce.hip xgmi_ar_rmsnorm_kernel); otherwise RCCL all-reduce + the
-        fused add+norm kernel."""
+        row-parallel projection.  On the IPC path ONE kernel (csrc/xgmi_allreduce.hip, one- or
+        two-shot by the measured table); otherwise RCCL all-reduce + the fused add+norm kernel."""
         from .. import ops
 
-        if self.size > 1 and self.xgmi is not None and self.xgmi.eligible_rows(x, residual):
-            return self.xgmi.all_reduce_rmsnorm_(x, residual, w, eps)
+        if self.size > 1 and self._ipc(x) and self.xgmi.eligible_rows(x, residual):
+            algo = self.xgmi.algo(x.shape[0], x.numel() * 2)
+            if algo != "rccl":
+                return self.xgmi.all_reduce_rmsnorm_(x, residual, w, eps, algo=algo)
         self.all_reduce_(x)
         return ops.rmsnorm(x, w, eps, residual=residual)
 
@@ -63,6 +75,9 @@ class TPGroup:
         if self.size == 1:
             return t
         n = t.shape[0] // self.size
+        if self.ipc_only and self._ipc(t):
+            self.all_reduce_(t)
+            return t[self.rank * n:(self.rank + 1) * n].contiguous()
         if dist.get_backend(self.group) == "gloo":  # gloo has no reduce_scatter
             dist.all_reduce(t, group=self.group)
             return t[self.rank * n:(self.rank + 1) * n].contiguous()
@@ -74,6 +89,8 @@ class TPGroup:
         """Concatenation over ranks of t [n, ...] -> [size*n, ...]."""
         if self.size == 1:
             return t
+        if self._ipc(t) and t.numel() * t.element_size() <= self.xgmi.max_bytes:
+            return self.xgmi.all_gather(t).reshape((t.shape[0] * self.size,) + tuple(t.shape[1:]))
         if dist.get_backend(self.group) == "gloo":
             return self.all_gather_cat(t, dim=0)
         out = torch.empty((t.shape[0] * self.size,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
@@ -83,6 +100,8 @@ class TPGroup:
     def all_gather_cat(self, t: torch.Tensor, dim: int = -1) -> torch.Tensor:
         if self.size == 1:
             return t
+        if self._ipc(t) and t.numel() * t.element_size() <= self.xgmi.max_bytes:
+            return torch.cat(list(self.xgmi.all_gather(t)), dim=dim)
         parts = [torch.empty_like(t) for _ in range(self.size)]
         dist.all_gather(parts, t.contiguous(), group=self.group)
         return torch.cat(parts, dim=dim)
@@ -106,6 +125,8 @@ class TPGroup:
     def broadcast_(self, t: torch.Tensor) -> torch.Tensor:
         """In place: the group leader's ``t`` on every rank."""
         if self.size > 1:
+            if self._ipc(t) and t.numel() * t.element_size() <= self.xgmi.max_bytes:
+                return self.xgmi.broadcast_(t, root=0)
             dist.broadcast(t, src=self.ranks[0] if self.ranks else 0, group=self.group)
         return t
 
@@ -194,8 +215,24 @@ def new_tp_groups(tp_size: int, with_ctrl: bool = True) -> TPGroup:
         ctrl = dist.new_group(ranks, backend="gloo") if with_ctrl and tp_size > 1 else None
         if rank in ranks:
             mine = TPGroup(ranks.index(rank), tp_size, grp, ctrl, ranks)
-    if mine is not None and tp_size > 1 and os.environ.get("LK_XGMI_AR") == "1" and torch.cuda.is_available():
-        from .xgmi_ar import attach  # one-shot xGMI all-reduce for decode-sized messages (K14)
+    if mine is not None and tp_size > 1:
+        mode = collectives_mode()
+        if mode == "ipc":
+            mine.ipc_only = True
+        if mode in ("ipc", "auto") and torch.cuda.is_available():
+            from .xgmi_ar import attach  # xGMI IPC collectives (K14); the table is tuned with the model
 
-        attach(mine)
+            attach(mine, rccl=mode == "auto" and dist.get_backend(mine.group) == "nccl")
     return mine
+
+
+def collectives_mode() -> str:
+    """LK_TP_COLLECTIVES: ``auto`` (default: IPC kernels attached, each all-reduce size routed by
+    the start-up measurement, RCCL one of the candidates), ``rccl`` (RCCL only, round-3
+    behaviour), ``ipc`` (IPC kernels only -- the mode for several ranks on one device)."""
+    m = os.environ.get("LK_TP_COLLECTIVES", "auto")
+    if os.environ.get("LK_XGMI_AR") == "0":
+        m = "rccl"
+    if m not in ("auto", "rccl", "ipc"):
+        raise ValueError(f"LK_TP_COLLECTIVES must be auto / rccl / ipc, not {m!r}")
+    return m

@@ -33,7 +33,7 @@ from .tp import TPGroup
 log = get_logger("tp")
 
 
-_CMDS = ("stop", "step", "capture", "barrier")
+_CMDS = ("stop", "step", "capture", "barrier", "knn")
 # StepInputs array fields in wire order (lists travel as int32 arrays; gather = (dst, src))
 _FIELDS = ("ids", "positions", "slots", "q_lens", "ctx_lens", "tables_p", "ctx_d", "tables_d", "logits_rows",
            "gather_dst", "gather_src")
@@ -58,6 +58,13 @@ def encode_msg(cmd: str, arg=None) -> tuple[np.ndarray, np.ndarray]:
     parts = []
     if cmd == "capture":
         h[7], h[8] = int(arg[0]), int(bool(arg[1]))
+    elif cmd == "knn":  # (queries [nq, D] bf16 / f32 host tensor, k): raw bytes travel as int32 words
+        q, k = arg
+        if q.dtype not in (torch.bfloat16, torch.float32):
+            raise TypeError("sharded kNN queries must be bf16 or f32")
+        raw = q.contiguous().view(-1).view(torch.uint8).numpy()
+        h[2], h[7], h[8], h[9] = int(q.dtype == torch.float32), q.shape[0], q.shape[1], int(k)
+        parts.append(np.frombuffer(np.ascontiguousarray(np.pad(raw, (0, (-raw.size) % 4))).tobytes(), dtype=np.int32))
     elif cmd == "step":
         si = arg
         h[2], h[3], h[4], h[5], h[6] = si.num_decode, si.decode_graph, int(si.greedy), si.shared_len, si.prev_bcast
@@ -87,6 +94,11 @@ def decode_msg(h: np.ndarray, payload: np.ndarray):
     cmd = _CMDS[int(h[0])]
     if cmd == "capture":
         return cmd, (int(h[7]), bool(h[8]))
+    if cmd == "knn":
+        nq, d, k = int(h[7]), int(h[8]), int(h[9])
+        dt, esz = (torch.float32, 4) if h[2] else (torch.bfloat16, 2)
+        raw = torch.from_numpy(payload.copy().view(np.uint8)[: nq * d * esz].copy())
+        return cmd, (raw.view(dt).view(nq, d), k)
     if cmd != "step":
         return cmd, None
     out, off = {}, 0
@@ -298,17 +310,37 @@ class _Ctrl:
 
 def _agree_num_blocks(model, tp: TPGroup, **kw) -> int:
     """Size the KV pool from this rank's free memory, then take the group minimum
-    (rank 0's allocator hands out block ids that every rank must hold)."""
+    (rank 0's allocator hands out block ids that every rank must hold) -- a host-side
+    agreement over the CPU control group."""
     keys = ("block_size", "max_model_len", "max_num_seqs", "kv_cache_gb", "gpu_memory_fraction")
     n = torch.tensor([ModelRunner.plan_num_blocks(model, **{k: kw[k] for k in keys if k in kw})], dtype=torch.int64)
     if tp.size > 1:
-        if torch.cuda.is_available() and model.device.type == "cuda":
-            n = n.to(model.device)
-        dist.all_reduce(n, op=dist.ReduceOp.MIN, group=tp.group)
+        if tp.ctrl is not None:
+            dist.all_reduce(n, op=dist.ReduceOp.MIN, group=tp.ctrl)
+        else:
+            if torch.cuda.is_available() and model.device.type == "cuda":
+                n = n.to(model.device)
+            dist.all_reduce(n, op=dist.ReduceOp.MIN, group=tp.group)
     return int(n.item())
 
 
+def tune_collectives(model, tp: TPGroup):
+    """Measure the group's all-reduce algorithms at the model's hidden size (every rank in
+    lockstep; the leader's table is used by all): xgmi_ar.XgmiAllReduce.tune."""
+    x = getattr(tp, "xgmi", None)
+    if x is None or x.table or tp.size == 1 or os.environ.get("LK_XGMI_TUNE", "1") == "0":
+        return
+    if not (torch.cuda.is_available() and model.device.type == "cuda"):
+        return
+    t0 = time.perf_counter()
+    x.tune(model.cfg.hidden)
+    x.tune_s = time.perf_counter() - t0
+    if tp.rank == 0:
+        log.info("TP collectives (measured in %.1f s): %s", x.tune_s, x.describe())
+
+
 def make_tp_runner(model, tp: TPGroup, **runner_kw) -> tuple[ModelRunner, _Ctrl]:
+    tune_collectives(model, tp)
     ctrl = _Ctrl(tp)
     nb = runner_kw.pop("num_blocks", None)
     if nb is None:
@@ -346,6 +378,19 @@ def shutdown_tp(engine):
     engine.tp_ctrl.send("stop")
 
 
+def tp_knn_search(engine, shard, queries: torch.Tensor, k: int):
+    """Leader side of the sharded kNN (every TP rank scans 1/T of the corpus): broadcast the
+    queries over the control channel, search this rank's shard, gather every rank's top-k over
+    the CPU control group and merge with the HIP merge (stable (score desc, id asc) order:
+    identical to one full scan).  The workers answer in order with their steps, so the exchange
+    never interleaves with the step collectives on the device."""
+    q = queries.to(shard.corpus.dtype)
+    ctrl = getattr(engine, "tp_ctrl", None)
+    if ctrl is not None and ctrl.tp.size > 1:
+        ctrl.send("knn", (q.cpu(), k))
+    return shard.search(q.to(shard.corpus.device), k)
+
+
 def tp_barrier(engine):
     """World barrier (after a device sync) from the TP driver while its workers sit in
     run_tp_worker: they receive a "barrier" command and join the same barrier."""
@@ -358,8 +403,9 @@ def tp_barrier(engine):
 
 
 @torch.inference_mode()
-def run_tp_worker(model, tp: TPGroup, **runner_kw):
-    """Ranks > 0: execute whatever rank 0 schedules until it says stop."""
+def run_tp_worker(model, tp: TPGroup, knn=None, **runner_kw):
+    """Ranks > 0: execute whatever rank 0 schedules until it says stop (``knn``: this rank's
+    ShardedKnnIndex, answering the leader's sharded searches)."""
     from ..utils.watchdog import StepWatchdog
 
     stall_s = float(runner_kw.pop("stall_s", 600.0)) if "stall_s" in runner_kw else 600.0
@@ -380,6 +426,11 @@ def run_tp_worker(model, tp: TPGroup, **runner_kw):
             if torch.cuda.is_available() and model.device.type == "cuda":
                 torch.cuda.synchronize()
             dist.barrier()
+        elif cmd == "knn":
+            if knn is None:
+                raise RuntimeError("TP worker got a sharded kNN search but holds no corpus shard")
+            q, k = arg
+            knn.search(q.to(knn.corpus.device), k)
         elif cmd == "step":
             with wd.busy():  # a step that never returns (dead peer in an all-reduce) is a stall
                 runner.execute(arg)

@@ -161,6 +161,12 @@ class RagIndex:
         """Attach a corpus matrix produced directly on the GPU (bulk index builds)."""
         self._gpu = (corpus_bf16.contiguous(), norms if norms is not None else ops.row_norms(corpus_bf16))
 
+    def set_sharded(self, search_fn):
+        """Route searches through a corpus-sharded kNN: ``search_fn(queries [nq, D] bf16, k) ->
+        (scores f32 [nq, k], ids int32 [nq, k])`` (parallel.tp_engine.tp_knn_search: every TP
+        rank scans its shard, merged in the single-scan order).  None restores the local scan."""
+        self._sharded = search_fn
+
     def search_vectors_async(self, q: np.ndarray | torch.Tensor, top_k: int) -> "PendingSearch":
         """Launch a batched search without blocking the host: on the GPU the kNN kernel and
         one non-blocking copy of its (scores, ids) into pinned memory are enqueued on the
@@ -173,8 +179,11 @@ class RagIndex:
             return PendingSearch(done=self.search_vectors(q, top_k) if n else [[] for _ in range(len(q))])
         corpus, norms = self.gpu_tensors()
         qt = torch.as_tensor(q).to(self.device, torch.bfloat16).reshape(-1, corpus.shape[1]).contiguous()
-        qn = ops.row_norms(qt) if qt.is_cuda else qt.float().norm(dim=-1)
-        s, i = ops.knn_topk(corpus, norms, qt, qn, min(k, 64))
+        if getattr(self, "_sharded", None) is not None:
+            s, i = self._sharded(qt, min(k, 64))
+        else:
+            qn = ops.row_norms(qt) if qt.is_cuda else qt.float().norm(dim=-1)
+            s, i = ops.knn_topk(corpus, norms, qt, qn, min(k, 64))
         if not s.is_cuda:
             return PendingSearch(done=_rows(s.tolist(), i.tolist(), min(k, n)))
         hs = torch.empty(s.shape, dtype=s.dtype, pin_memory=True)

@@ -62,8 +62,12 @@ def test_bench_four_rank_dp():
 
 
 def test_bench_two_rank_tp():
+    """--tp 2: the corpus is sharded over the TP group (each rank scans half, the leader merges) and
+    the sharded top-k equals the single full scan."""
     d = _run(["--tp", "2"], nproc=2)
     assert d["config"]["parallelism"] == "tp2" and d["config"]["global_batch"] == 2 and d["value"] > 0
+    knn = d["config"]["knn"]
+    assert knn["mode"].startswith("sharded over tp2") and knn["matches_single_scan"] is True, knn
 
 
 def test_bench_refuses_forced_reference_on_gpu_device():

@@ -1,0 +1,132 @@
+"""The tensor-parallel engine executing on HIP with several ranks: TP = 2 / 4 / 8 processes share
+the box's single MI355X (weights, KV heads and vocab sharded as on an 8-GPU node) and run every
+collective on the IPC path (``LK_TP_COLLECTIVES=ipc``: fused all-reduce + norm tails, all-gathers
+of the vocab-parallel argmax, broadcasts; RCCL refuses several ranks on one device), with the
+decode steps replayed from hipGraphs that capture those collectives, synchronous and pipelined
+stepping, and the start-up collective measurement.  Greedy tokens == the TP = 1 engine on the
+same checkpoint, up to near-ties (bf16 partial sums in a different order)."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+transformers = pytest.importorskip("transformers")
+
+pytestmark = pytest.mark.gpu
+# every rank's spinning IPC workgroups must be co-resident on the ONE device (8 ranks x 16
+# workgroups), and the decode routing tuner is not what this test is about
+os.environ.setdefault("LK_XGMI_AR_BLOCKS", "16")
+os.environ.setdefault("LK_DECODE_TUNE", "0")
+PROMPTS = [list(range(5, 45)), [7, 8, 9, 10], list(range(100, 180)), [300, 301, 302], list(range(200, 260))]
+NEW = 10
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _hf():
+    cfg = transformers.LlamaConfig(vocab_size=1024, hidden_size=1024, intermediate_size=2048, num_hidden_layers=2,
+                                   num_attention_heads=16, num_key_value_heads=8, max_position_embeddings=1024,
+                                   rope_theta=10000.0, rms_norm_eps=1e-5, tie_word_embeddings=False)
+    torch.manual_seed(11)
+    return transformers.LlamaForCausalLM(cfg).eval()
+
+
+def _cfg():
+    from llm_kubernetes_minikube_sharp4dev_amd.models.configs import DecoderConfig
+
+    return DecoderConfig("tp-ipc", "llama", 2, 1024, 16, 8, 64, 2048, 1024, max_position=1024, rope_theta=10000.0)
+
+
+def _run(eng, pipelined: bool):
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import SamplingParams
+
+    seqs = [eng.add_request(p, SamplingParams.greedy(NEW)) for p in PROMPTS]
+    while eng.has_work():
+        eng.step_pipelined() if pipelined else eng.step()
+    eng.flush()
+    return [s.output_ids for s in seqs]
+
+
+KW = dict(block_size=16, max_model_len=512, max_num_seqs=8, num_blocks=128, use_graphs=True)
+
+
+def _worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LK_TP_COLLECTIVES="ipc")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp import new_tp_groups
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp_engine import (make_tp_engine, run_tp_worker, shutdown_tp,
+                                                                          tp_capture_all)
+
+    tp = new_tp_groups(world)
+    assert tp.ipc_only and tp.xgmi is not None
+    m = build_decoder(_cfg(), device="cuda", tp=tp)
+    m.load_hf_state_dict(_hf().state_dict())
+    if rank == 0:
+        eng = make_tp_engine(m, tp, None, engine_kw={"eos_ids": set()}, **KW)
+        tp_capture_all(eng, max_batch=16, variants=(True,))
+        out = {"sync": _run(eng, False), "pipelined": _run(eng, True), "table": tp.xgmi.timings,
+               "routes": dict(tp.xgmi.table)}
+        shutdown_tp(eng)
+        torch.cuda.synchronize()
+        out["err"] = tp.xgmi.error()
+        torch.save(out, out_path)
+    else:
+        run_tp_worker(m, tp, **KW)
+        torch.cuda.synchronize()
+        assert tp.xgmi.error() == 0
+    dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def reference():
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.llm_engine import LLMEngine
+    from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder
+
+    hf = _hf()
+    m = build_decoder(_cfg(), device="cuda")
+    m.load_hf_state_dict(hf.state_dict())
+    eng = LLMEngine(m, None, eos_ids=set(), **KW)
+    eng.runner.capture_all(max_batch=16, variants=(True,))
+    toks = _run(eng, False)
+    del eng, m
+    torch.cuda.empty_cache()
+    return hf, toks
+
+
+def _same_or_near_tie(hf, got, ref):
+    for p, g, r in zip(PROMPTS, got, ref):
+        assert len(g) == NEW
+        if g == r:
+            continue
+        k = next(i for i, (a, b) in enumerate(zip(g, r)) if a != b)
+        with torch.no_grad():
+            want = hf(torch.tensor([p + r[:k]])).logits[0, -1]
+        gap = abs(want[g[k]] - want[r[k]]).item()
+        assert gap < 0.05 * want.abs().max().item() + 0.05, (p[:3], k, g[k], r[k], gap)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_tp_engine_ipc_matches_tp1(reference, world):
+    hf, ref = reference
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "out.pt")
+        mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        got = torch.load(out, weights_only=True)
+    assert got["err"] == 0
+    assert got["table"] and set(got["routes"].values()) <= {"ipc1", "ipc2"}, got["routes"]
+    print(f"TP={world} measured collective routes: {got['routes']}")
+    _same_or_near_tie(hf, got["sync"], ref)
+    _same_or_near_tie(hf, got["pipelined"], ref)

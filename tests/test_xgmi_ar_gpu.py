@@ -12,6 +12,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
+# up to 8 ranks share the ONE device here: keep every rank's spinning workgroups co-resident
+os.environ.setdefault("LK_XGMI_AR_BLOCKS", "32")
 
 
 def _free_port():
@@ -22,8 +24,9 @@ def _free_port():
     return p
 
 
-def _vals(n, r, it=0):
-    return ((torch.arange(n) * (r + 1) + it) % 64).to(torch.bfloat16)
+def _vals(n, r, it=0, mod=32):
+    # sums over up to 8 ranks stay below 256: exact in bf16
+    return ((torch.arange(n) * (r + 1) + it) % mod).to(torch.bfloat16)
 
 
 def _worker(rank, world, port, out_dir):
@@ -67,10 +70,12 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_xgmi_allreduce_two_processes():
+@pytest.mark.parametrize("world", [2, 8])
+def test_xgmi_allreduce_two_processes(world):
+    """World 8 = the production TP=8 group's signal layout (kMaxRanks slots per workgroup)."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _free_port(), d), nprocs=2, join=True)
-        for r in range(2):
+        mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        for r in range(world):
             ok = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)
             assert all(ok), f"rank {r}: {ok}"
 
@@ -175,10 +180,11 @@ def _fused_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_xgmi_allreduce_rmsnorm_fused_bit_identical():
+@pytest.mark.parametrize("world", [2, 8])
+def test_xgmi_allreduce_rmsnorm_fused_bit_identical(world):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_fused_worker, args=(2, _free_port(), d), nprocs=2, join=True)
-        for r in range(2):
+        mp.spawn(_fused_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        for r in range(world):
             ok = torch.load(os.path.join(d, f"f{r}.pt"), weights_only=True)
             assert all(o[-1] and o[-2] for o in ok), f"rank {r}: {ok}"
 
@@ -257,9 +263,76 @@ def _two_shot_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_xgmi_two_shot_allreduce_and_fused_norm():
+@pytest.mark.parametrize("world", [3, 8])
+def test_xgmi_two_shot_allreduce_and_fused_norm(world):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_two_shot_worker, args=(3, _free_port(), d), nprocs=3, join=True)
-        for r in range(3):
+        mp.spawn(_two_shot_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        for r in range(world):
             ok = torch.load(os.path.join(d, f"s{r}.pt"), weights_only=True)
+            assert all(o[-1] for o in ok), f"rank {r}: {ok}"
+
+
+def _gather_worker(rank, world, port, out_dir):
+    """IPC all-gather / broadcast of raw bytes (any dtype, sizes not a multiple of 16 B), the
+    TPGroup routes that use them (all_gather_cat / all_gather_rows / broadcast_ / greedy_ids) in
+    IPC-only mode, eager and replayed from a hipGraph."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp import TPGroup
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.xgmi_ar import XgmiAllReduce
+
+    tp = TPGroup(rank, world, dist.group.WORLD, ctrl=dist.group.WORLD, ranks=list(range(world)), ipc_only=True)
+    tp.xgmi = XgmiAllReduce(tp, 4 << 20, rccl=False)
+    ok = []
+    for shape, dt in (((5,), torch.float32), ((3, 7), torch.int64), ((64, 1000), torch.bfloat16), ((1,), torch.int32)):
+        x = (torch.arange(int(torch.tensor(shape).prod())).view(shape) * (rank + 1)).to(dt).cuda()
+        g = tp.xgmi.all_gather(x)
+        want = torch.stack([(torch.arange(x.numel()).view(shape) * (r + 1)).to(dt) for r in range(world)])
+        ok.append(("gather", str(dt), bool(torch.equal(g.cpu(), want))))
+        cat = tp.all_gather_cat(x, dim=-1)
+        ok.append(("cat", str(dt), bool(torch.equal(cat.cpu(), torch.cat(list(want), dim=-1)))))
+        b = x.clone()
+        tp.broadcast_(b)
+        ok.append(("bcast", str(dt), bool(torch.equal(b.cpu(), want[0]))))
+    rows = tp.all_gather_rows(torch.full((3, 16), float(rank), device="cuda", dtype=torch.bfloat16))
+    ok.append(("rows", "", bool(torch.equal(rows.float().cpu(), torch.arange(world).repeat_interleave(3)[:, None].float().expand(-1, 16)))))
+    # vocab-parallel greedy: rank r holds vocab slice [r*V, (r+1)*V), the max planted on rank world-1
+    V = 96
+    lg = torch.randn(4, V, generator=torch.Generator().manual_seed(rank)).to(torch.bfloat16).cuda()
+    if rank == world - 1:
+        lg[:, 17] = 50.0
+    ids = tp.greedy_ids(lg, vocab_lo=rank * V)
+    ok.append(("greedy", "", bool(torch.equal(ids.cpu(), torch.full((4,), (world - 1) * V + 17, dtype=torch.int32)))))
+    # hipGraph: broadcast + all-gather captured and replayed with new inputs
+    src = torch.zeros(40, dtype=torch.float32, device="cuda")
+    dst = torch.zeros(40, dtype=torch.float32, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        tp.xgmi.broadcast_(src)
+        tp.xgmi.state.gather(src.view(torch.uint8)[:144].clone(), torch.empty(144 * world, dtype=torch.uint8, device="cuda"), -1)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        tp.xgmi.broadcast_(src)
+        dst.copy_(src * 2)
+    for it in range(3):
+        src.copy_(torch.arange(40, dtype=torch.float32, device="cuda") + 100 * rank + it)
+        gr.replay()
+        torch.cuda.synchronize()
+        ok.append(("graph", it, bool(torch.equal(dst.cpu(), 2 * (torch.arange(40, dtype=torch.float32) + it)))))
+    ok.append(("err", "", tp.xgmi.error() == 0))
+    torch.save(ok, os.path.join(out_dir, f"g{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_xgmi_gather_broadcast(world):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_gather_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        for r in range(world):
+            ok = torch.load(os.path.join(d, f"g{r}.pt"), weights_only=True)
             assert all(o[-1] for o in ok), f"rank {r}: {ok}"
