@@ -812,6 +812,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("resid") = py::none(), py::arg("ss_out") = py::none(), py::arg("positions") = py::none(),
         py::arg("cos_sin") = py::none(), py::arg("slots") = py::none(), py::arg("k_cache") = py::none(),
         py::arg("v_cache") = py::none(), py::arg("hq") = 0, py::arg("hkv") = 0, py::arg("hd") = 0);
+  m.def("gemm_epi_lds", [](int64_t mode) { return (int64_t)lk_gemm_epi_lds((int)mode); }, "", py::arg("mode") = -1);
   m.def("gemm_streamk", &gemm_streamk,
         "stream-K policy of the prefill GEMM (mode 0 off / 1 on / -1 keep); returns the waits that gave up since the last call",
         py::arg("mode") = -1);

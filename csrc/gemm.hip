@@ -475,14 +475,49 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
   // ---- epilogue: lane holds row (.. + r); fragment pair (2p, 2p+1) gives it the 8 consecutive
   // columns 32p + 8g .. +7 of its wave's 16NF (the pair_col layout); NF = 3's third fragment
   // the 4 columns 32 + 4g .. +3
-  auto put8 = [](bf16_t* dst, const float (&y)[8]) {
+  // LDS-staged stores (ea.stage): the bf16 output tile [256][OW] goes to the dead staging LDS
+  // (16-B chunks XOR-swizzled by row & 7), then each wave writes whole rows: one 16-B store
+  // per lane covers 2 x 512 B (or 4 x 256 B) of CONSECUTIVE output bytes, where a fragment
+  // store covers 16 rows x 64 B spread over the output's row stride
+  constexpr int OW = EPI == EPI_SWIGLU ? 128 : BN;  // output columns of the tile
+  constexpr int OCH = OW / 8;                       // 16-B chunks per tile row
+  const bool staged = (EPI <= EPI_BIAS_RELU) && ea.stage > 0 && mode != SK_PARTIAL;
+  unsigned char* stile = smem;
+  auto schunk = [](int lrow, int ch) { return lrow * (OW * 2) + ((ch ^ (lrow & 7)) << 4); };
+  auto emit8 = [&](int lrow, int lcol, const float (&y)[8]) {  // lcol: multiple of 8
     uint4_t pk;
     pk.x = pack_bf2(y[0], y[1]);
     pk.y = pack_bf2(y[2], y[3]);
     pk.z = pack_bf2(y[4], y[5]);
     pk.w = pack_bf2(y[6], y[7]);
-    *reinterpret_cast<uint4_t*>(dst) = pk;
+    if (staged) *reinterpret_cast<uint4_t*>(stile + schunk(lrow, lcol >> 3)) = pk;
+    else *reinterpret_cast<uint4_t*>(out + (long)(tm * kBM + lrow) * ldo + (long)tn * OW + lcol) = pk;
   };
+  auto emit4 = [&](int lrow, int lcol, const float (&y)[4]) {  // lcol: multiple of 4
+    uint2 pk;
+    pk.x = pack_bf2(y[0], y[1]);
+    pk.y = pack_bf2(y[2], y[3]);
+    if (staged) *reinterpret_cast<uint2*>(stile + schunk(lrow, lcol >> 3) + ((lcol & 4) << 1)) = pk;
+    else *reinterpret_cast<uint2*>(out + (long)(tm * kBM + lrow) * ldo + (long)tn * OW + lcol) = pk;
+  };
+  auto flush = [&]() {
+    __syncthreads();
+    constexpr int PER = 256 * OCH / 512;  // chunks per thread
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = i * 512 + tid, lrow = c / OCH, ch = c % OCH;
+      const int row = tm * kBM + lrow;
+      const uint4_t v = *reinterpret_cast<const uint4_t*>(stile + schunk(lrow, ch));
+      if (row < M) *reinterpret_cast<uint4_t*>(out + (long)row * ldo + (long)tn * OW + ch * 8) = v;
+    }
+  };
+  // this lane's 8 row scales into registers BEFORE any staged write (the scale array lives in
+  // the same LDS the staged tile overwrites)
+  float scm[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) scm[m] = row_scale(wr * 128 + m * 16 + r);
+  if (staged) __syncthreads();  // every wave is past its last staging / scale read
+
   if constexpr (EPI == EPI_PARTIAL) {  // fp32 partial sums of split kz: out is float [splits, M, ldo]
     float* part = reinterpret_cast<float*>(out) + (long)kz * M * ldo;
 #pragma unroll
@@ -501,15 +536,16 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
     for (int m = 0; m < 8; ++m) {
       const int row = tm * kBM + wr * 128 + m * 16 + r;
       if (row >= M || mode == SK_PARTIAL) continue;
-      const float sc = row_scale(wr * 128 + m * 16 + r);
+      const float sc = scm[m];
       float y[8];
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int v = 0; v < 4; ++v)
           y[4 * h + v] = rbf(lk_silu(rbf(acc[m][h][v] * sc))) * rbf(acc[m][h + 2][v] * sc);
-      put8(out + (long)row * ldo + tn * 128 + wc * 32 + 8 * g, y);
+      emit8(wr * 128 + m * 16 + r, wc * 32 + 8 * g, y);
     }
+    if (staged) flush();
   } else if constexpr (EPI == EPI_RESID) {
     // producer side of the folded norm: r = bf16(r + bf16(acc)) in place, then the partial sum
     // of squares of the new r over this tile's BN columns (lanes r + 16 g, then the 4 wc waves)
@@ -586,7 +622,7 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
     for (int m = 0; m < 8; ++m) {
       const int row = tm * kBM + wr * 128 + m * 16 + r;
       if (row >= M || mode == SK_PARTIAL) continue;
-      const float sc = row_scale(wr * 128 + m * 16 + r);
+      const float sc = scm[m];
       const int pos = ea.pos[row];
       const int slot = ea.slots ? ea.slots[row] : -1;
       const float* cs = ea.cos_sin + (long)pos * ea.hd;
@@ -683,11 +719,10 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
     for (int m = 0; m < 8; ++m) {
       const int row = tm * kBM + wr * 128 + m * 16 + r;
       if (row >= M || mode == SK_PARTIAL) continue;
-      bf16_t* orow = out + (long)row * ldo + tn * BN + wc * 16 * NF;
+      const int lrow = wr * 128 + m * 16 + r, lc = wc * 16 * NF;
       if constexpr (EPI == EPI_NONE) {
-        const float sc = row_scale(wr * 128 + m * 16 + r);
 #pragma unroll
-        for (int n = 0; n < NF; ++n) acc[m][n] *= sc;
+        for (int n = 0; n < NF; ++n) acc[m][n] *= scm[m];
       }
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
@@ -696,18 +731,16 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
         for (int h = 0; h < 2; ++h)
 #pragma unroll
           for (int v = 0; v < 4; ++v) y[4 * h + v] = act(acc[m][2 * p + h][v], bv[2 * p + h][v]);
-        put8(orow + 32 * p + 8 * g, y);
+        emit8(lrow, lc + 32 * p + 8 * g, y);
       }
       if constexpr (NF == 3) {
         float y[4];
 #pragma unroll
         for (int v = 0; v < 4; ++v) y[v] = act(acc[m][2][v], bv[2][v]);
-        uint2 pk;
-        pk.x = pack_bf2(y[0], y[1]);
-        pk.y = pack_bf2(y[2], y[3]);
-        *reinterpret_cast<uint2*>(orow + 32 + 4 * g) = pk;
+        emit4(lrow, lc + 32 + 4 * g, y);
       }
     }
+    if (staged) flush();
   }
 }
 
@@ -844,6 +877,16 @@ int group_rows() {
     return v >= 1 ? v : 4;
   }();
   return g;
+}
+
+// LDS-staged epilogue stores by default?  LK_GEMM_EPI_LDS (0 / 1); lk_gemm_set_epi_lds overrides
+int g_epi_lds = -1;
+int epi_lds_default() {
+  if (g_epi_lds < 0) {
+    const char* e = getenv("LK_GEMM_EPI_LDS");
+    g_epi_lds = e ? (atoi(e) != 0) : 0;
+  }
+  return g_epi_lds;
 }
 
 int cu_count() {
@@ -1024,6 +1067,12 @@ int lk_gemm_streamk(int mode) {
   return errs;
 }
 
+// policy knob for in-process A/Bs: mode 0 / 1 sets the staged-epilogue default, -1 reads it
+int lk_gemm_epi_lds(int mode) {
+  if (mode >= 0) g_epi_lds = mode != 0;
+  return epi_lds_default();
+}
+
 int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks) {
   if (M < 1 || K < kBK || K % kBK || (bn != 192 && bn != 256)) return 0;
   if (ks < 1 || ks > 8 || K / kBK < 2 * ks || (ks > 1 && (epi == EPI_SWIGLU || epi == EPI_QKV || N % 4))) return 0;
@@ -1039,7 +1088,8 @@ int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks) {
 // 8-B aligned output rows; any M >= 1.
 int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
             int variant, bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, const LkEpi* ea_) {
-  const LkEpi ea = ea_ ? *ea_ : LkEpi{};
+  LkEpi ea = ea_ ? *ea_ : LkEpi{};
+  if (ea.stage < 0) ea.stage = epi_lds_default();
   // fused-chain epilogue arguments (checked here: a bad pointer / shape would fault the device)
   if (ea.ss_in && (ea.ss_nt < 1 || ea.ss_nt > 32 || ea.ss_ld < M || ea.inv_h <= 0.f)) return -1;
   if (epi == EPI_RESID && (!ea.resid || !ea.ss_out || ea.ldr % 8 || ea.ss_out_ld < M)) return -1;
