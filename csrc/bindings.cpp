@@ -336,6 +336,37 @@ at::Tensor gemm_fused(const at::Tensor& x, const at::Tensor& w, int64_t epi, int
   return out;
 }
 
+// embedding rows from int32 ids (vocab shard [lo, lo + n_local) of a vocab-parallel table: others 0)
+at::Tensor embed_rows(const at::Tensor& table, const at::Tensor& ids, int64_t lo, int64_t n_local) {
+  CHECK_CUDA(table); CHECK_BF16(table); CHECK_CONTIG(table); CHECK_CUDA(ids); CHECK_I32(ids); CHECK_CONTIG(ids);
+  if (n_local < 0) n_local = table.size(0);
+  TORCH_CHECK(table.dim() == 2 && table.size(1) % 8 == 0 && n_local <= table.size(0), "table [V, H], H % 8");
+  check_rows16(table, "table");
+  at::Tensor out = at::empty({ids.numel(), table.size(1)}, table.options());
+  CHECK_RC(lk_embed_rows(bp(out), bp(table), ip(ids), ids.numel(), table.size(1), lo, n_local, cur_stream()), "embed_rows");
+  return out;
+}
+
+// ids[dst] = prev[src] (in-flight decode inputs of a pipelined step)
+void scatter_ids(at::Tensor& ids, const at::Tensor& dst, const at::Tensor& prev, const at::Tensor& src) {
+  CHECK_CUDA(ids); CHECK_I32(ids); CHECK_CONTIG(ids); CHECK_I32(prev); CHECK_CONTIG(prev);
+  TORCH_CHECK(dst.scalar_type() == at::kLong && src.scalar_type() == at::kLong && dst.is_contiguous() && src.is_contiguous() &&
+              dst.numel() == src.numel(), "dst / src int64 of equal length");
+  CHECK_RC(lk_scatter_ids(ids.data_ptr<int>(), dst.data_ptr<int64_t>(), prev.data_ptr<int>(), src.data_ptr<int64_t>(),
+                          (int)dst.numel(), cur_stream()), "scatter_ids");
+}
+
+// out[r] = x[idx[r]] (bf16 rows)
+at::Tensor gather_rows(const at::Tensor& x, const at::Tensor& idx) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_LASTDIM(x); check_rows16(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % 8 == 0, "x [T, H], H % 8");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.is_contiguous(), "idx int64");
+  at::Tensor out = at::empty({idx.numel(), x.size(1)}, x.options());
+  CHECK_RC(lk_gather_rows(bp(out), bp(x), x.stride(0), idx.data_ptr<int64_t>(), idx.numel(), x.size(1), cur_stream()),
+           "gather_rows");
+  return out;
+}
+
 int64_t gemm_streamk(int64_t mode) { return lk_gemm_streamk((int)mode); }
 
 bool gemm_supported(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bn, int64_t splits) {
@@ -813,6 +844,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("cos_sin") = py::none(), py::arg("slots") = py::none(), py::arg("k_cache") = py::none(),
         py::arg("v_cache") = py::none(), py::arg("hq") = 0, py::arg("hkv") = 0, py::arg("hd") = 0);
   m.def("gemm_epi_lds", [](int64_t mode) { return (int64_t)lk_gemm_epi_lds((int)mode); }, "", py::arg("mode") = -1);
+  m.def("embed_rows", &embed_rows, "", py::arg("table"), py::arg("ids"), py::arg("lo") = 0, py::arg("n_local") = -1);
+  m.def("scatter_ids", &scatter_ids);
+  m.def("gather_rows", &gather_rows);
   m.def("gemm_streamk", &gemm_streamk,
         "stream-K policy of the prefill GEMM (mode 0 off / 1 on / -1 keep); returns the waits that gave up since the last call",
         py::arg("mode") = -1);

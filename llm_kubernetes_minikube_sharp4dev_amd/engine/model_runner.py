@@ -391,7 +391,7 @@ class ModelRunner:
         (rows ``src``): no host sync."""
         if self.prev_ids is None:
             raise RuntimeError("step has in-flight input tokens but no previous step ids")
-        ids.index_copy_(0, dst, self.prev_ids.index_select(0, src).to(ids.dtype))
+        ops.scatter_ids(ids, dst, self.prev_ids, src)
 
     def _cascade_meta(self, meta, B: int, shared_len: torch.Tensor):
         """Cascade fields of ``meta`` for B decode rows (static shapes per B: graph-safe)."""

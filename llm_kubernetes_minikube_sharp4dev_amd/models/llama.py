@@ -134,12 +134,8 @@ class LlamaModel(nn.Module):
     # ------------------------------------------------------------------ forward
     def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
         if not self.tp.enabled:
-            return self.embed[ids.long()]
-        local = ids.long() - self.vocab_lo
-        mask = (local < 0) | (local >= self.vocab_local)
-        h = self.embed[local.clamp(0, self.vocab_local - 1)]
-        h = h.masked_fill(mask[:, None], 0)
-        return self.tp.all_reduce_(h)
+            return ops.embed_rows(self.embed, ids)
+        return self.tp.all_reduce_(ops.embed_rows(self.embed, ids, self.vocab_lo, self.vocab_local))
 
     def forward(self, ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
         """ids [T] -> final hidden states of rows ``meta.logits_idx`` (or all rows)."""
@@ -172,7 +168,7 @@ class LlamaModel(nn.Module):
             a = ops.linear_swiglu(x, L.gate_up)
             x = self.tp.all_reduce_rmsnorm(ops.linear(a, L.down), res, nxt, cfg.norm_eps)
         if meta.logits_idx is not None:
-            x = x.index_select(0, meta.logits_idx)
+            x = ops.gather_rows(x, meta.logits_idx)
         return x
 
     def _forward_chain(self, res: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
@@ -198,7 +194,7 @@ class LlamaModel(nn.Module):
             a = ops.linear_swiglu_scaled(res, L.gate_up, ss_post, eps)
             ops.linear_resid(a, L.down, res, ss_in)
             x, scale = res, ss_in
-        h = res if meta.logits_idx is None else res.index_select(0, meta.logits_idx)
+        h = res if meta.logits_idx is None else ops.gather_rows(res, meta.logits_idx)
         return ops.rmsnorm(h, self.final_norm, eps)
 
     def _forward_sp(self, ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:

@@ -20,7 +20,8 @@ __all__ = [
     "kv_write", "paged_decode", "flash_prefill", "prefill_tiles", "knn_topk", "knn_merge",
     "pool_normalize", "row_norms", "select_tokens", "repeat_penalty_", "sample", "linear", "linear_swiglu",
     "decode_splits", "rope_cos_sin", "tune_gemm", "tune_decode", "gemm", "linear_add_rmsnorm", "linear_rope_kv",
-    "prefill_chain_ok", "linear_resid", "linear_qkv_fused", "linear_swiglu_scaled",
+    "prefill_chain_ok", "linear_resid", "linear_qkv_fused", "linear_swiglu_scaled", "embed_rows", "scatter_ids",
+    "gather_rows",
 ]
 
 rope_cos_sin = ref.rope_cos_sin
@@ -708,6 +709,34 @@ def linear_qkv_fused(x, w, ss, eps: float, positions, cos_sin, Hq: int, Hkv: int
     sched, bn, _ = _cfg_of(M, N, K, 0)
     return lib().gemm_fused(x, w, EPI_QKV, bn, None, sched, 1, ss_in=ss, eps=eps, positions=positions,
                             cos_sin=cos_sin, slots=slots, k_cache=k_cache, v_cache=v_cache, hq=Hq, hkv=Hkv, hd=D)
+
+
+# ---------------------------------------------------------------- per-step gathers (csrc/step_ops.hip)
+def embed_rows(table, ids, lo: int = 0, n_local: Optional[int] = None):
+    """Rows of ``table`` for int32 ``ids``; with ``lo`` / ``n_local`` a vocab-parallel shard:
+    ids outside [lo, lo + n_local) give zero rows (summed over the TP group afterwards)."""
+    n_local = table.shape[0] if n_local is None else n_local
+    if use_hip(table) and ids.dtype == torch.int32:
+        return lib().embed_rows(table, ids.contiguous(), lo, n_local)
+    local = ids.long() - lo
+    mask = (local < 0) | (local >= n_local)
+    return table[local.clamp(0, max(0, n_local - 1))].masked_fill(mask[:, None], 0)
+
+
+def scatter_ids(ids, dst, prev, src):
+    """ids[dst] = prev[src] (the in-flight decode inputs of a pipelined step), one launch."""
+    if use_hip(ids) and ids.dtype == torch.int32 and prev.dtype == torch.int32:
+        lib().scatter_ids(ids, dst.contiguous(), prev.contiguous(), src.contiguous())
+        return ids
+    ids.index_copy_(0, dst, prev.index_select(0, src).to(ids.dtype))
+    return ids
+
+
+def gather_rows(x, idx):
+    """x[idx] (rows), one launch on the GPU."""
+    if use_hip(x) and x.dtype == torch.bfloat16 and idx.dtype == torch.int64 and x.stride(-1) == 1:
+        return lib().gather_rows(x, idx.contiguous())
+    return x.index_select(0, idx)
 
 
 def softmax_scale(D: int) -> float:

@@ -112,9 +112,10 @@ class TPGroup:
         max (first rank on ties = lowest id, the single-GPU argmax order)."""
         from .. import ops
 
-        idx = ops.select_tokens(local_logits).long()  # HIP argmax on the bf16 logits (first max)
+        ids = ops.select_tokens(local_logits)  # HIP argmax on the bf16 logits (first max), int32
         if self.size == 1:
-            return (idx + vocab_lo).int()
+            return ids if vocab_lo == 0 else ids + vocab_lo
+        idx = ids.long()
         vals = local_logits.gather(1, idx[:, None]).squeeze(1).float()
         idx = idx + vocab_lo
         v = self.all_gather_cat(vals[None], dim=0)

@@ -873,3 +873,30 @@ def test_gemm_lds_staged_epilogue_bit_identical(hip, M, N, K, epi, bn):
         hip.gemm_epi_lds(old)
     assert torch.equal(outs[0], outs[1]), (outs[0].float() - outs[1].float()).abs().max()
     assert hip.gemm_streamk(-1) == 0
+
+
+@pytest.mark.parametrize("lo,n_local", [(0, None), (0, 300), (300, 300), (600, 424)])
+def test_embed_rows(hip, lo, n_local):
+    """Token-embedding gather (full table, and a vocab-parallel shard: out-of-shard ids -> 0)."""
+    V, H = 1024, 4096
+    table = torch.randn(V if n_local is None else n_local, H, device=DEV, dtype=torch.bfloat16)
+    ids = torch.randint(0, V, (777,), device=DEV, dtype=torch.int32)
+    got = ops.embed_rows(table, ids, lo, n_local)
+    local = ids.long() - lo
+    n = table.shape[0]
+    want = table[local.clamp(0, n - 1)].masked_fill(((local < 0) | (local >= n))[:, None], 0)
+    assert torch.equal(got.cpu(), want.cpu())
+
+
+def test_scatter_ids_and_gather_rows(hip):
+    ids = torch.arange(64, device=DEV, dtype=torch.int32)
+    prev = torch.randint(0, 1000, (16,), device=DEV, dtype=torch.int32)
+    dst = torch.tensor([3, 9, 40], device=DEV)
+    src = torch.tensor([15, 0, 7], device=DEV)
+    want = ids.clone()
+    want[dst] = prev[src]
+    ops.scatter_ids(ids, dst, prev, src)
+    assert torch.equal(ids.cpu(), want.cpu())
+    x = torch.randn(1000, 4096, device=DEV, dtype=torch.bfloat16)
+    idx = torch.tensor([999, 0, 17, 17, 500], device=DEV)
+    assert torch.equal(ops.gather_rows(x, idx).cpu(), x[idx].cpu())
