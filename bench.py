@@ -456,6 +456,7 @@ def main():
         p50 = statistics.median(lat_all) * 1000 if lat_all else None
         lat_sorted = sorted(lat_all)
         p90 = lat_sorted[int(0.9 * (len(lat_sorted) - 1))] * 1000 if lat_sorted else None
+        p99 = lat_sorted[int(0.99 * (len(lat_sorted) - 1))] * 1000 if lat_sorted else None
         avg_prompt = float(allst[:, 2].sum() / max(1.0, float(allst[:, 3].sum())))
         statuses = {}
         for r in results:
@@ -489,6 +490,17 @@ def main():
         steps_acct = {k: round(statistics.mean(r.timings[k] for r in results if r.timings and r.timings.get(k) is not None), 2)
                       for k in ("steps_queued", "steps_in_system", "steps_run", "jumped_tokens")
                       if any(r.timings and r.timings.get(k) is not None for r in results)}
+        # what the slowest decile of requests did differently from the median one (engine steps
+        # waited / lived / ran, grammar-jumped tokens, prompt length, time to first token)
+        tail = {}
+        tim_res = [r for r in results if r.timings and r.timings.get("e2e_s") is not None]
+        if len(tim_res) >= 20:
+            cut = sorted(r.timings["e2e_s"] for r in tim_res)[int(0.9 * (len(tim_res) - 1))]
+            for name, grp in (("p90_plus", [r for r in tim_res if r.timings["e2e_s"] >= cut]), ("all", tim_res)):
+                tail[name] = {k: round(statistics.mean(r.timings[k] for r in grp if r.timings.get(k) is not None), 3)
+                              for k in ("e2e_s", "ttft_s", "steps_queued", "steps_in_system", "steps_run",
+                                        "jumped_tokens", "prompt_tokens", "preemptions")
+                              if any(r.timings.get(k) is not None for r in grp)}
         par = f"dp{n_replicas}" if args.tp == 1 else f"tp{args.tp}" + (f"xdp{n_replicas}" if n_replicas > 1 else "")
         sim = {}
         if args.tp > 1 and getattr(tpg, "xgmi", None) is not None:
@@ -537,6 +549,7 @@ def main():
                     f"-> {n} chunks; random-init weights)",
             "p50_latency_ms": round(p50, 1) if p50 is not None else None,
             "p90_latency_ms": round(p90, 1) if p90 is not None else None,
+            "p99_latency_ms": round(p99, 1) if p99 is not None else None,
             # completions whose tool call executed (HTTP 200) per second: with random weights the
             # rest end in the reference's own 400 / 500 branches after the same generation work
             "success_qps": round(statuses.get("200", 0) * (total_req / max(1, len(results))) / t_max, 3),
@@ -570,6 +583,7 @@ def main():
                 "avg_cached_prefix_tokens": round(statistics.mean(pre), 1) if pre else 0,
                 "stage_means_s": {k: round(v, 4) for k, v in tim.items()},
                 "engine_steps_per_request": steps_acct,
+                "latency_tail": tail,
                 "step_mix_rank0": step_mix,
                 "index_build_s": round(t_index, 2),
                 "knn": knn_info,

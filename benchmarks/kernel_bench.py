@@ -101,7 +101,9 @@ def case_encoder_attn(B=1600, L=80, H=12, D=64):
     t = timeit(lambda: ops.flash_prefill(qkv[:, : H * D], qkv[:, H * D: 2 * H * D], qkv[:, 2 * H * D:], cu, H, H, D,
                                          1 / math.sqrt(D), False, tiles=tiles))
     flops = B * 4 * L * L * D * H
-    return {"case": f"encoder_attn B{B} L{L} H{H} D{D}", "us": t * 1e6, "TFLOP/s": flops / t / 1e12}
+    # q, k, v read + o written once each: at L <= 128 the kernel is bounded by these bytes
+    return {"case": f"encoder_attn B{B} L{L} H{H} D{D}", "us": t * 1e6, "TFLOP/s": flops / t / 1e12,
+            "GB/s": T * H * D * 2 * 4 / t / 1e9}
 
 
 def case_rmsnorm(T=8192, H=4096):

@@ -266,7 +266,12 @@ def test_fused_prefill_chain_matches_hf(monkeypatch):
 
     hf, m = _gpu_llama()
     assert m.folded and not m.rope_neox
-    prompts = [list(range(3 + i, 3 + i + 90)) for i in range(4)]  # 360 prefill rows in one step
+    # the toy QKV GEMM has 4 tiles, which the default dispatch would split over K (and a split
+    # QKV GEMM has no in-kernel epilogue, so the chain would not be taken)
+    monkeypatch.setattr(ops, "GEMM_SPLITK", False)
+    # 512 prefill rows in one step (a multiple of the scheduler's 256-row alignment, so no chunk
+    # is trimmed and every prompt's last row is in this step)
+    prompts = [list(range(3 + i, 3 + i + 128)) for i in range(4)]
     calls = []
     real = m._forward_chain
     monkeypatch.setattr(m, "_forward_chain", lambda *a, **k: calls.append(1) or real(*a, **k))
