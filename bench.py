@@ -480,6 +480,9 @@ def main():
             "gpu_step_busy_frac": round(sum(t[7] for t in trace) / elapsed, 3) if trace and elapsed else None,
             "avg_prefill_tokens_mixed": round(statistics.mean(t[0] for t in mixed), 1) if mixed else 0,
             "avg_decode_rows": round(statistics.mean(t[1] for t in trace), 1) if trace else 0,
+            # device idle between a step's ids copy and the next step's start marker, i.e. the
+            # host reached the launch after the device ran dry; by what the host did just before
+            "idle_before_launch": _idle_summary(trace),
             # mixed steps by total rows (256-row buckets): where the prefill GEMMs run
             "mixed_rows_hist": {str(k * 256): v for k, v in sorted(collections.Counter(
                 (t[0] + t[1] + 255) // 256 for t in mixed).items())},
@@ -599,6 +602,25 @@ def main():
                 f.write(line + "\n")
     if world > 1:
         dist.destroy_process_group()
+
+
+def _idle_summary(trace) -> dict:
+    """Device idle before each traced launch (engine step_trace element 8), in total and for
+    gaps > 1 ms / > 0.1 ms, split by the host work tag of the launch (element 9: "plan" = a
+    retrieval batch was launched, "admit" = planned requests were added, "" = neither)."""
+    if not trace or len(trace[0]) < 10:
+        return {}
+    out = {"total_ms": round(1e3 * sum(t[8] for t in trace), 1)}
+    for lim, key in ((1e-3, "gt_1ms"), (1e-4, "gt_0.1ms")):
+        big = [t for t in trace if t[8] > lim]
+        by = collections.Counter(t[9] or "-" for t in big)
+        ms = collections.defaultdict(float)
+        for t in big:
+            ms[t[9] or "-"] += 1e3 * t[8]
+        out[key] = {"count": len(big), "ms": round(1e3 * sum(t[8] for t in big), 1),
+                    "by_tag": {k: [by[k], round(ms[k], 1)] for k in by},
+                    "decode_only": sum(1 for t in big if t[0] == 0)}
+    return out
 
 
 def _collective_floor(path, world: int, hidden: int):

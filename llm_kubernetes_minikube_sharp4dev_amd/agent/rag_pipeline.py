@@ -324,10 +324,17 @@ class ContinuousLoad:
         try:
             while len(done) < n_complete:
                 free = self.concurrency - len(self.inflight) - self._planning
+                note = ""
                 if free >= min(self.admit_chunk, self.concurrency) or (not self.inflight and not self._planning):
                     self._submit(self.next_queries(free))
+                    note = "plan"
                 # nothing to run: wait for the planner instead of spinning
+                n_in = len(self.inflight)
                 self._admit_ready(done, block=not llm.has_work() and not self.inflight)
+                if len(self.inflight) != n_in:
+                    note += "+admit"
+                if note:  # step traces tag the launch that follows this host work (bench.py)
+                    llm.trace_note = note
                 t_st = time.perf_counter()
                 if llm.has_work():
                     llm.step_pipelined()

@@ -82,6 +82,8 @@ class LLMEngine:
         self._pending = None   # the launched step not yet sampled (step_pipelined, LK_PIPELINE=csl)
         # optional per-step trace: (prefill tokens, decode rows, wall seconds) -- bench.py
         self.step_trace: Optional[list] = None
+        self._trace_end_ev = None  # the last traced step's ids-copy event (device idle before the next)
+        self.trace_note = ""       # caller's tag for the host work before the next launch (bench)
 
     # ------------------------------------------------------------------ API
     def add_request(self, prompt_ids: list, params: Optional[SamplingParams] = None,
@@ -195,16 +197,18 @@ class LLMEngine:
                 ev0 = torch.cuda.Event(enable_timing=True)  # GPU-side step start (after earlier work)
                 ev0.record()
             rows, out = self.runner.forward_logits(batch.items, greedy)
+            note, self.trace_note = self.trace_note, ""
             for seq, start, n in batch.items:
                 seq.num_computed = start + n
                 seq.steps_run += 1
                 if seq.step_first is None:
                     seq.step_first = self.launches
             self.launches += 1
-            return [batch, rows, out, greedy, ts, t0, time.perf_counter(), ev0]
+            return [batch, rows, out, greedy, ts, t0, time.perf_counter(), (ev0, note)]
 
     def _sample(self, launched):
-        batch, rows, out, greedy, ts, t0, t1, ev0 = launched
+        batch, rows, out, greedy, ts, t0, t1, ev0n = launched
+        ev0 = ev0n[0]
         host = ev = ids = None
         if rows:
             seqs = [s for s, _ in rows]
@@ -222,10 +226,10 @@ class LLMEngine:
                     s.num_inflight, s.inflight_row = 1, i
             self.runner.prev_ids = ids
             self.runner.prev_sampled_rows = 0 if greedy else len(rows)
-        return (batch, rows, host, ev, ts, t0, t1, time.perf_counter(), ev0)
+        return (batch, rows, host, ev, ts, t0, t1, time.perf_counter(), ev0n)
 
     def _collect(self, pending) -> list:
-        batch, rows, host, ev, ts, t0, t1, t1s, ev0 = pending
+        batch, rows, host, ev, ts, t0, t1, t1s, (ev0, launched_note) = pending
         t2 = time.perf_counter()
         if rows and ev is not None:
             ev.synchronize()  # outside the lock: aborts and admissions never wait on the device
@@ -258,10 +262,18 @@ class LLMEngine:
                 ndec = len(batch.items) - sum(1 for sq, st, n in batch.items if st < len(sq.prompt_ids))
                 npre = sum(n for sq, st, n in batch.items if st < len(sq.prompt_ids))
                 gpu = ev0.elapsed_time(ev) / 1e3 if (ev0 is not None and ev is not None) else 0.0
+                # device idle between the previous traced step's ids copy and this step's start
+                # marker: > 0 when the host reached this launch after the device ran dry
+                idle = 0.0
+                if ev0 is not None and self._trace_end_ev is not None:
+                    idle = max(0.0, self._trace_end_ev.elapsed_time(ev0) / 1e3)
+                if ev is not None:
+                    self._trace_end_ev = ev
                 # (prefill tokens, decode rows, step s, schedule s, prepare+launch s, sample+sync s, post s,
-                #  GPU s from the step's first kernel to its ids copy)
+                #  GPU s from the step's first kernel to its ids copy, device idle before it, caller tag)
                 self.step_trace.append((npre, ndec, t3 - t0, t0 - ts, t1 - t0,
-                                        (t2 - t1) if rows else 0.0, (t3 - t2) if rows else 0.0, gpu))
+                                        (t2 - t1) if rows else 0.0, (t3 - t2) if rows else 0.0, gpu, idle,
+                                        launched_note))
             M.STEP_TOKENS.observe(batch.num_tokens)
             M.STEP_TIME.observe(time.perf_counter() - t0)
             M.KV_USAGE.set(self.allocator.usage())
