@@ -125,7 +125,7 @@ def parse():
                          "for like-for-like comparisons with round-1 numbers)")
     ap.add_argument("--collective-floor", default=None,
                     help="with --tp-sim: JSON of the measured per-call TP tail collective floor "
-                         "(benchmarks/xgmi_floor.py; default profiles/r4_tp_collectives/floor_tp<N>_h<H>.json)")
+                         "(benchmarks/xgmi_floor.py --world 2; default profiles/r4_tp_collectives/floor_tp2_h<H>.json)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -524,18 +524,23 @@ def main():
                    "allreduce_calls": ar_calls,
                    "rows_per_step": round(rows / max(1, len(trace)), 1),
                    "decode_only_steps": len(dec_only), "mixed_steps": len(mixed)}
-            floor = _collective_floor(args.collective_floor, args.tp_sim, lc.hidden)
+            floor = _collective_floor(args.collective_floor, lc.hidden)
             if floor is not None:
-                # per-step collective time the real group would add, from the measured per-call
-                # floor (kernel + handshake of the routed algorithm at that row count, W ranks on one
-                # device: no link-bandwidth term): 2 tails per layer + the embedding all-reduce
-                per_call = [_floor_us(floor, t[0] + t[1]) for t in trace]
-                tot_s = sum(per_call) * (2 * lc.num_layers + 1) / 1e6
-                sim["collective_floor"] = {
-                    "source": floor["_path"], "ms_per_step": round(1e3 * tot_s / max(1, len(trace)), 3),
+                # per-step collective time the real group would add: per call the faster of
+                # one-shot / two-shot = the measured kernel + handshake floor at that row count
+                # (2 ranks sharing one device, benchmarks/xgmi_floor.py) + the xGMI link time of its
+                # bytes at XGMI_LINK_GBPS per link (a model figure); 2 tails per layer + the
+                # vocab-parallel embedding all-reduce
+                W, Hd, n_ar = args.tp_sim, lc.hidden, 2 * lc.num_layers + 1
+                per_step = [n_ar * _per_call_us(floor, t[0] + t[1], Hd, W) for t in trace]
+                tot_s = sum(per_step) / 1e6
+                sim["collective_estimate"] = {
+                    "floor_source": floor["_path"], "link_GBps_model": XGMI_LINK_GBPS,
+                    "ms_per_step": round(1e3 * tot_s / max(1, len(trace)), 3),
                     "timed_window_s": round(tot_s, 3), "vs_elapsed": round(tot_s / elapsed, 3) if elapsed else None,
-                    "decode_only_ms_per_step": round(1e3 * (2 * lc.num_layers + 1) * sum(
-                        _floor_us(floor, t[0] + t[1]) for t in dec_only) / 1e6 / max(1, len(dec_only)), 3)}
+                    "decode_only_ms_per_step": round(sum(p for p, t in zip(per_step, trace) if t[0] == 0) / 1e3
+                                                     / max(1, len(dec_only)), 3),
+                    "per_call_us": {str(r): round(_per_call_us(floor, r, Hd, W), 1) for r in (1, 64, 128, 256, 4096)}}
         out = {
             "metric": METRICS[args.workload].format(model=MODEL_NAMES.get(args.model, args.model)),
             "value": round(qps, 3),
@@ -611,6 +616,13 @@ def _idle_summary(trace) -> dict:
     if not trace or len(trace[0]) < 10:
         return {}
     out = {"total_ms": round(1e3 * sum(t[8] for t in trace), 1)}
+    if len(trace[0]) > 10:
+        # launches that began with the device already idle: their schedule + input preparation
+        # (host seconds 3 and 4) is device idle too, by step kind
+        st = [t for t in trace if t[10]]
+        out["starved_launches"] = {"count": len(st), "decode_only": sum(1 for t in st if t[0] == 0),
+                                   "host_prep_ms": round(1e3 * sum(t[3] + t[4] for t in st), 1),
+                                   "by_tag": dict(collections.Counter(t[9] or "-" for t in st))}
     for lim, key in ((1e-3, "gt_1ms"), (1e-4, "gt_0.1ms")):
         big = [t for t in trace if t[8] > lim]
         by = collections.Counter(t[9] or "-" for t in big)
@@ -623,8 +635,11 @@ def _idle_summary(trace) -> dict:
     return out
 
 
-def _collective_floor(path, world: int, hidden: int):
-    path = path or os.path.join(ROOT, "profiles", "r4_tp_collectives", f"floor_tp{world}_h{hidden}.json")
+XGMI_LINK_GBPS = 153.0  # per xGMI link, per direction (MI355X: 7 links per GPU)
+
+
+def _collective_floor(path, hidden: int):
+    path = path or os.path.join(ROOT, "profiles", "r4_tp_collectives", f"floor_tp2_h{hidden}.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -633,16 +648,24 @@ def _collective_floor(path, world: int, hidden: int):
     return d
 
 
-def _floor_us(floor: dict, rows: int) -> float:
-    """Per-call floor (us) of the routed algorithm at ``rows`` rows: the smallest measured bucket
+def _floor_us(floor: dict, rows: int, algo: str) -> float:
+    """Measured per-call floor (us) of ``algo`` at ``rows`` rows: the smallest measured bucket
     >= rows, linear in rows past the largest."""
     tab = {int(k): v for k, v in floor["us_by_rows"].items()}
-    route = {int(k): a for k, a in floor["route"].items()}
     for b in sorted(tab):
         if rows <= b:
-            return tab[b][route[b]]
+            return tab[b][algo]
     b = max(tab)
-    return tab[b][route[b]] * rows / b
+    return tab[b][algo] * rows / b
+
+
+def _per_call_us(floor: dict, rows: int, hidden: int, world: int) -> float:
+    """One fused all-reduce + norm tail of ``rows`` x ``hidden`` bf16 on ``world`` ranks: the
+    faster of one-shot (every peer's S bytes over its own link, in parallel) and two-shot
+    (2 S / world bytes per link), each = measured floor + link time."""
+    S = rows * hidden * 2
+    link = {"ipc1": S / (XGMI_LINK_GBPS * 1e3), "ipc2": 2 * S / world / (XGMI_LINK_GBPS * 1e3)}
+    return min(_floor_us(floor, rows, a) + link[a] for a in ("ipc1", "ipc2"))
 
 
 def _jump_forward_on() -> bool:

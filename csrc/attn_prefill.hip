@@ -77,11 +77,8 @@ struct PrefillParams {
 // NW waves per workgroup (4 or 8): WH of them share a row group (one head each), and
 // NW / WH row groups of 32 queries sit on top of each other, all fed by the same staged
 // K/V tile -- with NW = 8 each K/V byte brought into LDS serves 2x the MFMA work.
-// OCC4 (dense encoder attention, D <= 64): 4 waves per SIMD (<= 128 VGPRs) instead of 3, so
-// short sequences' workgroups (one or two K/V tiles each) overlap more of each other's load
-// latency (LK_ENC_OCC4)
-template <int D, bool CAUSAL, bool PAGED, int WH, int NW, bool PIPE, bool OCC4 = false>
-__global__ __launch_bounds__(64 * NW, OCC4 ? 4 : 8 / NW) void flash_prefill_kernel(PrefillParams p) {
+template <int D, bool CAUSAL, bool PAGED, int WH, int NW, bool PIPE>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillParams p) {
   constexpr int NT = 64 * NW;      // threads
   constexpr int KK = D / 16;       // QK k-steps
   constexpr int ND = D / 32;       // O^T d tiles
@@ -472,14 +469,6 @@ static float prefill_defer() {
   return env;
 }
 
-static bool enc_occ4() {
-  static const bool env = [] {
-    const char* e = getenv("LK_ENC_OCC4");
-    return e ? atoi(e) != 0 : false;
-  }();
-  return env;
-}
-
 // the query rows one workgroup covers: must use the launch's prefill_waves(G, D)
 int lk_prefill_rows_per_tile(int G, int D) { return G >= 4 ? 32 * (prefill_waves(G, D) / 4) : 32 * (4 / G); }
 
@@ -513,9 +502,7 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
   if (WH == 4 && NW == 8) { L(DD, C, PG, 4, (DD >= 64 ? 8 : 4)); } \
   else if (WH == 4) { L(DD, C, PG, 4, 4); }                   \
   else if (WH == 2) { L(DD, C, PG, 2, 4); }                   \
-  else if (!C && !PG && DD == 64 && enc_occ4()) {              \
-    flash_prefill_kernel<64, false, false, 1, 4, false, true><<<grid, 256, 0, st>>>(pr); \
-  } else { L(DD, C, PG, 1, 4); }
+  else { L(DD, C, PG, 1, 4); }
 #define BY_MODE(DD)                                    \
   if (causal && paged) { BY_W(DD, true, true) }        \
   else if (causal && !paged) { BY_W(DD, true, false) } \

@@ -83,6 +83,7 @@ class LLMEngine:
         # optional per-step trace: (prefill tokens, decode rows, wall seconds) -- bench.py
         self.step_trace: Optional[list] = None
         self._trace_end_ev = None  # the last traced step's ids-copy event (device idle before the next)
+        self._last_ids_ev = None   # the most recently recorded ids-copy event (starvation check)
         self.trace_note = ""       # caller's tag for the host work before the next launch (bench)
 
     # ------------------------------------------------------------------ API
@@ -193,6 +194,10 @@ class LLMEngine:
             # under TP an all-gather of (max, argmax) pairs instead of the vocab)
             greedy = all(_plain_greedy(sq.params) for sq, _, _ in batch.items)
             ev0 = None
+            # traced runs: did the device already finish everything queued before this launch
+            # (then all of this launch's host preparation is device idle)?
+            starved = (self.step_trace is not None and self._last_ids_ev is not None
+                       and self._last_ids_ev.query())
             if self.step_trace is not None and self.model.device.type == "cuda":
                 ev0 = torch.cuda.Event(enable_timing=True)  # GPU-side step start (after earlier work)
                 ev0.record()
@@ -204,7 +209,7 @@ class LLMEngine:
                 if seq.step_first is None:
                     seq.step_first = self.launches
             self.launches += 1
-            return [batch, rows, out, greedy, ts, t0, time.perf_counter(), (ev0, note)]
+            return [batch, rows, out, greedy, ts, t0, time.perf_counter(), (ev0, note, starved)]
 
     def _sample(self, launched):
         batch, rows, out, greedy, ts, t0, t1, ev0n = launched
@@ -219,6 +224,7 @@ class LLMEngine:
                 host.copy_(ids, non_blocking=True)
                 ev = torch.cuda.Event(enable_timing=ev0 is not None)
                 ev.record()
+                self._last_ids_ev = ev
             else:
                 host = ids
             for i, s in enumerate(seqs):
@@ -229,7 +235,7 @@ class LLMEngine:
         return (batch, rows, host, ev, ts, t0, t1, time.perf_counter(), ev0n)
 
     def _collect(self, pending) -> list:
-        batch, rows, host, ev, ts, t0, t1, t1s, (ev0, launched_note) = pending
+        batch, rows, host, ev, ts, t0, t1, t1s, (ev0, launched_note, starved) = pending
         t2 = time.perf_counter()
         if rows and ev is not None:
             ev.synchronize()  # outside the lock: aborts and admissions never wait on the device
@@ -270,10 +276,11 @@ class LLMEngine:
                 if ev is not None:
                     self._trace_end_ev = ev
                 # (prefill tokens, decode rows, step s, schedule s, prepare+launch s, sample+sync s, post s,
-                #  GPU s from the step's first kernel to its ids copy, device idle before it, caller tag)
+                #  GPU s from the step's first kernel to its ids copy, device idle before it, caller tag,
+                #  device already idle when the launch began)
                 self.step_trace.append((npre, ndec, t3 - t0, t0 - ts, t1 - t0,
                                         (t2 - t1) if rows else 0.0, (t3 - t2) if rows else 0.0, gpu, idle,
-                                        launched_note))
+                                        launched_note, starved))
             M.STEP_TOKENS.observe(batch.num_tokens)
             M.STEP_TIME.observe(time.perf_counter() - t0)
             M.KV_USAGE.set(self.allocator.usage())
