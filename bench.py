@@ -123,6 +123,11 @@ def parse():
                     help="tokenizer.json to use instead of the built-in one (e.g. benchmarks/data/"
                          "bpe_runbooks_r1.json, the round-1 tokenizer trained on the synthetic corpus itself, "
                          "for like-for-like comparisons with round-1 numbers)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="every rank on cuda:0 (several ranks share ONE GPU): gloo process group, the TP "
+                         "collectives on the IPC kernels only (LK_TP_COLLECTIVES=ipc) -- runs the multi-rank "
+                         "TP engine (e.g. --tp 8, 70B shards of 17.6 GB each) on a one-GPU box; a correctness "
+                         "and collective-table run, not a throughput figure")
     ap.add_argument("--collective-floor", default=None,
                     help="with --tp-sim: JSON of the measured per-call TP tail collective floor "
                          "(benchmarks/xgmi_floor.py --world 2; default profiles/r4_tp_collectives/floor_tp2_h<H>.json)")
@@ -193,11 +198,21 @@ def main():
     on_gpu = args.device == "cuda"
     if on_gpu:
         assert torch.cuda.is_available(), "bench.py needs an MI355X (or --device cpu)"
+        if args.one_device:
+            # RCCL refuses several ranks on one device: gloo for the host-side collectives, the
+            # IPC kernels for every TP collective, a capped grid so all ranks' spinning
+            # workgroups stay co-resident on the one GPU
+            local = 0
+            os.environ["LK_TP_COLLECTIVES"] = "ipc"
+            os.environ.setdefault("LK_XGMI_AR_BLOCKS", "16")
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         _ext.lib()  # fail loudly if the HIP library is not built
         if world > 1:
-            dist.init_process_group("nccl", device_id=dev)
+            if args.one_device:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=dev)
     else:
         dev = torch.device("cpu")
         if world > 1:
@@ -234,7 +249,9 @@ def main():
     full = torch.zeros((per * world, enc.cfg.hidden), dtype=wdtype, device=dev)
     shard = torch.zeros((per, enc.cfg.hidden), dtype=wdtype, device=dev)
     shard[: hi - lo] = mine.to(wdtype)
-    if world > 1:
+    if world > 1 and args.one_device:  # gloo: through the host
+        full = torch.cat([t.to(dev) for t in _gather_cpu(shard.cpu(), world)])
+    elif world > 1:
         dist.all_gather_into_tensor(full, shard)
     else:
         full = shard
@@ -440,9 +457,12 @@ def main():
     stats = torch.tensor([elapsed, float(len(results)), float(sum(ptok)), float(len(ptok))],
                          dtype=torch.float64, device=dev)
     if world > 1:
-        allst = [torch.zeros_like(stats) for _ in range(world)]
-        dist.all_gather(allst, stats)
-        allst = torch.stack(allst).cpu()
+        if args.one_device:
+            allst = torch.stack(_gather_cpu(stats.cpu(), world))
+        else:
+            allst = [torch.zeros_like(stats) for _ in range(world)]
+            dist.all_gather(allst, stats)
+            allst = torch.stack(allst).cpu()
         objs = [None] * world
         dist.all_gather_object(objs, lat)
         lat_all = [x for o in objs for x in o]
@@ -633,6 +653,14 @@ def _idle_summary(trace) -> dict:
                     "by_tag": {k: [by[k], round(ms[k], 1)] for k in by},
                     "decode_only": sum(1 for t in big if t[0] == 0)}
     return out
+
+
+def _gather_cpu(t, world: int) -> list:
+    """all_gather of a host tensor over the (gloo) default group; bf16 travels as int16."""
+    src = t.view(torch.int16) if t.dtype == torch.bfloat16 else t
+    out = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(out, src.contiguous())
+    return [o.view(t.dtype) for o in out]
 
 
 XGMI_LINK_GBPS = 153.0  # per xGMI link, per direction (MI355X: 7 links per GPU)
