@@ -552,15 +552,18 @@ def main():
                 # bytes at XGMI_LINK_GBPS per link (a model figure); 2 tails per layer + the
                 # vocab-parallel embedding all-reduce
                 W, Hd, n_ar = args.tp_sim, lc.hidden, 2 * lc.num_layers + 1
-                per_step = [n_ar * _per_call_us(floor, t[0] + t[1], Hd, W) for t in trace]
-                tot_s = sum(per_step) / 1e6
-                sim["collective_estimate"] = {
-                    "floor_source": floor["_path"], "link_GBps_model": XGMI_LINK_GBPS,
-                    "ms_per_step": round(1e3 * tot_s / max(1, len(trace)), 3),
-                    "timed_window_s": round(tot_s, 3), "vs_elapsed": round(tot_s / elapsed, 3) if elapsed else None,
-                    "decode_only_ms_per_step": round(sum(p for p, t in zip(per_step, trace) if t[0] == 0) / 1e3
-                                                     / max(1, len(dec_only)), 3),
-                    "per_call_us": {str(r): round(_per_call_us(floor, r, Hd, W), 1) for r in (1, 64, 128, 256, 4096)}}
+                est = {"floor_source": floor["_path"], "link_GBps_model": XGMI_LINK_GBPS, "hbm_GBps_model": HBM_GBPS}
+                for name, up in (("upper", True), ("latency_floor_plus_bytes", False)):
+                    per_step = [n_ar * _per_call_us(floor, t[0] + t[1], Hd, W, up) for t in trace]
+                    tot_s = sum(per_step) / 1e6
+                    est[name] = {
+                        "ms_per_step": round(1e3 * tot_s / max(1, len(trace)), 3),
+                        "timed_window_s": round(tot_s, 3), "vs_elapsed": round(tot_s / elapsed, 3) if elapsed else None,
+                        "decode_only_ms_per_step": round(sum(p for p, t in zip(per_step, trace) if t[0] == 0) / 1e3
+                                                         / max(1, len(dec_only)), 3),
+                        "per_call_us": {str(r): round(_per_call_us(floor, r, Hd, W, up), 1)
+                                        for r in (1, 64, 128, 256, 4096)}}
+                sim["collective_estimate"] = est
         out = {
             "metric": METRICS[args.workload].format(model=MODEL_NAMES.get(args.model, args.model)),
             "value": round(qps, 3),
@@ -687,13 +690,23 @@ def _floor_us(floor: dict, rows: int, algo: str) -> float:
     return tab[b][algo] * rows / b
 
 
-def _per_call_us(floor: dict, rows: int, hidden: int, world: int) -> float:
+HBM_GBPS = 5000.0  # streaming rate of one MI355X's HBM3E under these kernels (model figure)
+
+
+def _per_call_us(floor: dict, rows: int, hidden: int, world: int, upper: bool = True) -> float:
     """One fused all-reduce + norm tail of ``rows`` x ``hidden`` bf16 on ``world`` ranks: the
     faster of one-shot (every peer's S bytes over its own link, in parallel) and two-shot
-    (2 S / world bytes per link), each = measured floor + link time."""
+    (2 S / world bytes per link).  ``upper``: measured floor at ``rows`` + link time -- the floor
+    was measured with 2 ranks sharing one device, so past a few hundred rows it also carries
+    both ranks' HBM passes through one HBM (an upper bound).  Otherwise: the measured floor at
+    <= 64 rows (kernel + handshake latency) + link time + this rank's own HBM passes (one-shot:
+    read W copies, write 2 (out + residual); two-shot: ~5 S / W + 2 S)."""
     S = rows * hidden * 2
     link = {"ipc1": S / (XGMI_LINK_GBPS * 1e3), "ipc2": 2 * S / world / (XGMI_LINK_GBPS * 1e3)}
-    return min(_floor_us(floor, rows, a) + link[a] for a in ("ipc1", "ipc2"))
+    if upper:
+        return min(_floor_us(floor, rows, a) + link[a] for a in ("ipc1", "ipc2"))
+    hbm = {"ipc1": (world + 2) * S / (HBM_GBPS * 1e3), "ipc2": (5 * S / world + 2 * S) / (HBM_GBPS * 1e3)}
+    return min(_floor_us(floor, min(rows, 64), a) + link[a] + hbm[a] for a in ("ipc1", "ipc2"))
 
 
 def _jump_forward_on() -> bool:
