@@ -660,6 +660,9 @@ def _idle_summary(trace) -> dict:
 
 def _gather_cpu(t, world: int) -> list:
     """all_gather of a host tensor over the (gloo) default group; bf16 travels as int16."""
+    import torch
+    import torch.distributed as dist
+
     src = t.view(torch.int16) if t.dtype == torch.bfloat16 else t
     out = [torch.empty_like(src) for _ in range(world)]
     dist.all_gather(out, src.contiguous())

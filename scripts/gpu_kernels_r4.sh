@@ -10,3 +10,5 @@ for occ in 0 1; do
   LK_ENC_OCC4=$occ timeout -k 10 120 python -u benchmarks/kernel_bench.py encoder prefill > gpurun_out/r4k/attn_occ$occ.log 2>&1 || { tail -20 gpurun_out/r4k/attn_occ$occ.log; exit 5; }
   echo "LK_ENC_OCC4=$occ"; grep -E "encoder|flash" gpurun_out/r4k/attn_occ$occ.log
 done
+timeout -k 10 500 python bench.py --steps 8 --warmup 2 > gpurun_out/r4k/bench_idle.log 2>&1 || { tail -20 gpurun_out/r4k/bench_idle.log; exit 6; }
+grep '"metric"' gpurun_out/r4k/bench_idle.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['p50_latency_ms'], d['p90_latency_ms'], json.dumps(d['config']['step_mix_rank0'].get('idle_before_launch')))"
