@@ -659,11 +659,12 @@ def _idle_summary(trace) -> dict:
 
 
 def _gather_cpu(t, world: int) -> list:
-    """all_gather of a host tensor over the (gloo) default group; bf16 travels as int16."""
+    """all_gather of a host tensor over the (gloo) default group; bf16 travels as raw bytes
+    (gloo has no 16-bit integer or bf16 all-gather)."""
     import torch
     import torch.distributed as dist
 
-    src = t.view(torch.int16) if t.dtype == torch.bfloat16 else t
+    src = t.contiguous().view(torch.uint8) if t.dtype == torch.bfloat16 else t
     out = [torch.empty_like(src) for _ in range(world)]
     dist.all_gather(out, src.contiguous())
     return [o.view(t.dtype) for o in out]
