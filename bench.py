@@ -386,6 +386,21 @@ def main():
                 out.append(r)
             return out
 
+        # progress on stderr every LK_BENCH_HEARTBEAT seconds (default 30; 0 = off): long
+        # runs (70B, several ranks sharing one GPU) show where they are
+        hb_s = float(os.environ.get("LK_BENCH_HEARTBEAT", "30"))
+        if hb_s > 0:
+            import threading
+
+            def _beat():
+                t_hb = time.perf_counter()
+                while True:
+                    time.sleep(hb_s)
+                    # host-side counters only: no HIP call from this thread (a graph capture may be open)
+                    log(rank, f"alive {time.perf_counter() - t_hb:.0f}s: engine steps {engine.steps}, launches "
+                              f"{engine.launches}, timed completions {len(results)}")
+
+            threading.Thread(target=_beat, name="bench-heartbeat", daemon=True).start()
         load = None
         if args.mode == "continuous":
             # warm-up fills the pipeline and reaches the steady prefill/decode mix; the timed
