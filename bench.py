@@ -545,7 +545,9 @@ def main():
             # the measured collective table the TP group routes by (parallel/xgmi_ar.py tune)
             sim["tp_collectives"] = {"routes": {str(k): v for k, v in tpg.xgmi.table.items()},
                                      "us_by_rows": {str(k): v for k, v in tpg.xgmi.timings.items()},
-                                     "mode": "ipc-only" if tpg.ipc_only else "auto (ipc1 / ipc2 / rccl measured)"}
+                                     "mode": "ipc-only" if tpg.ipc_only else "auto (ipc1 / ipc2 / rccl measured)",
+                                     # handshakes that hit the bounded spin (a peer late by > ~4 s)
+                                     "handshake_timeouts": int(tpg.xgmi.error())}
         if args.tp_sim > 1:
             par = f"tp{args.tp_sim}-sim (rank-0 shard on one GPU, collectives elided)"
             # what the real group moves per rank: every step's rows through 2 all-reduces per layer
