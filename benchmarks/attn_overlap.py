@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Do a mixed step's two attention kernels overlap?  Flash prefill over the step's prompt
+chunks (compute-bound) and paged decode over its decode rows (HBM-bound) at the serving shapes
+(Llama-3-8B heads, 6 prompts x 643 new tokens over 930 keys; 128 decode rows x 1000 keys), timed
+back to back on one stream vs on two streams (both launch orders), cold KV (rotated copies),
+HIP events, medians of interleaved rounds.
+
+    python benchmarks/attn_overlap.py [--md out.md]
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from llm_kubernetes_minikube_sharp4dev_amd import ops  # noqa: E402
+
+DEV = "cuda"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--md", default=None)
+    ap.add_argument("--rounds", type=int, default=15)
+    a = ap.parse_args()
+    Hq, Hkv, D, BS = 32, 8, 128, 16
+    # decode rows: 128 x 1000 keys, its own blocks
+    Bd, ctx_d = 128, 1000
+    nb_d = (ctx_d + BS - 1) // BS
+    # prefill: 6 prompts, 643 new of 930 keys
+    Bp, q, ctx_p = 6, 643, 930
+    nb_p = (ctx_p + BS - 1) // BS
+    NB = Bd * nb_d + Bp * nb_p + 1
+    copies = []
+    for _ in range(2):  # two KV caches so consecutive rounds do not hit the same bytes in MALL
+        kc = torch.randn(NB, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
+        copies.append((kc, torch.randn_like(kc)))
+    perm = torch.randperm(NB - 1, device=DEV).int()
+    bt_d = torch.zeros(Bd, 8192 // BS, dtype=torch.int32, device=DEV)
+    bt_d[:, :nb_d] = perm[: Bd * nb_d].view(Bd, nb_d)
+    bt_p = perm[Bd * nb_d: Bd * nb_d + Bp * nb_p].view(Bp, nb_p).contiguous()
+    qd = torch.randn(Bd, Hq, D, device=DEV, dtype=torch.bfloat16)
+    cl_d = torch.full((Bd,), ctx_d, dtype=torch.int32, device=DEV)
+    qp = torch.randn(Bp * q, Hq * D, device=DEV, dtype=torch.bfloat16)
+    cu = torch.arange(0, Bp * q + 1, q, dtype=torch.int32, device=DEV)
+    cl_p = torch.full((Bp,), ctx_p, dtype=torch.int32, device=DEV)
+    ts, tq = ops.prefill_tiles([q] * Bp, [ctx_p] * Bp, Hq // Hkv, True)
+    tiles = (torch.from_numpy(ts).to(DEV), torch.from_numpy(tq).to(DEV))
+    out_p = torch.empty_like(qp)
+    out_d = torch.empty_like(qd)
+    side = torch.cuda.Stream()
+    sc = 1 / math.sqrt(D)
+    it = [0]
+
+    def flash(kv):
+        ops.flash_prefill(qp, kv[0], kv[1], cu, Hq, Hkv, D, sc, True, block_tables=bt_p, ctx_lens=cl_p,
+                          tiles=tiles, out=out_p)
+
+    def decode(kv):
+        ops.paged_decode(qd, kv[0], kv[1], bt_d, cl_d, sc, out=out_d)
+
+    def arm(name):
+        kv = copies[it[0] % 2]
+        it[0] += 1
+        if name == "flash":
+            flash(kv)
+        elif name == "decode":
+            decode(kv)
+        elif name == "serial":
+            flash(kv)
+            decode(kv)
+        else:  # two streams: the first named kernel on the current stream, the other on the side
+            first, second = (flash, decode) if name == "2s_flash_first" else (decode, flash)
+            ev = torch.cuda.Event()
+            ev.record()
+            side.wait_event(ev)
+            first(kv)
+            with torch.cuda.stream(side):
+                second(kv)
+            ev2 = torch.cuda.Event()
+            ev2.record(side)
+            torch.cuda.current_stream().wait_event(ev2)
+
+    arms = ["flash", "decode", "serial", "2s_flash_first", "2s_decode_first"]
+    for n in arms:
+        arm(n)
+    torch.cuda.synchronize()
+    ts_ = {n: [] for n in arms}
+    for _ in range(a.rounds):
+        for n in arms:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            arm(n)
+            e1.record()
+            e1.synchronize()
+            ts_[n].append(e0.elapsed_time(e1) * 1e3)
+    med = {n: statistics.median(v) for n, v in ts_.items()}
+    lines = ["| arm | us |", "|---|---|"] + [f"| {n} | {med[n]:.1f} |" for n in arms]
+    lines.append(f"\nsum of the two alone {med['flash'] + med['decode']:.1f} us, max {max(med['flash'], med['decode']):.1f} us")
+    print("\n".join(lines), flush=True)
+    if a.md:
+        with open(a.md, "w") as f:
+            f.write("\n".join(lines) + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,5 @@
+# Round-4 probes: do a mixed step's flash prefill and paged decode kernels overlap on two streams?
+set -o pipefail
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/r4p
+timeout -k 10 180 python -u benchmarks/attn_overlap.py --md gpurun_out/r4p/attn_overlap.md > gpurun_out/r4p/attn_overlap.log 2>&1 || { tail -20 gpurun_out/r4p/attn_overlap.log; exit 2; }
+cat gpurun_out/r4p/attn_overlap.md
