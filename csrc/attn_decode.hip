@@ -70,9 +70,10 @@ __global__ __launch_bounds__(256, LK_DECODE_WG_PER_CU) void paged_decode_kernel(
   __shared__ float mrg_o[4][G][D];
 
   const int nblk = (nkeys + BS - 1) / BS;
-  for (int i = threadIdx.x; i < nblk; i += 256)
+  for (int i = threadIdx.x; i < nblk; i += 256) {
     blk[i] = block_tables[(long)b * bt_stride + k_begin / BS + i];
     LK_DASSERT(blk[i] >= 0);
+  }
   __syncthreads();
 
   // A wave's 16 K rows (16t + r16) and the 4 V rows of one load (i * RPL + lane / CPR) lie in

@@ -214,3 +214,23 @@ def test_runtime_under_asan_ubsan(native):
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "passed" in r.stdout
+
+
+def test_device_assert_build_compiles(tmp_path):
+    """The LK_DEBUG build (device asserts on, `csrc/build.py --debug`) must compile: every
+    kernel source that uses LK_DASSERT, device code only, for gfx950."""
+    import glob
+    import shutil
+    import subprocess
+
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("no hipcc")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    srcs = [s for s in sorted(glob.glob(os.path.join(root, "csrc", "*.hip"))) if "LK_DASSERT" in open(s).read()]
+    assert srcs
+    for s in srcs:
+        r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O1", "-std=c++17", "-DLK_DEBUG", "--offload-device-only",
+                            "-c", s, "-o", str(tmp_path / (os.path.basename(s) + ".o"))],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, (s, r.stderr[-2000:])
