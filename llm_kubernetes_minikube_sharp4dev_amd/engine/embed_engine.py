@@ -19,8 +19,18 @@ import torch
 
 from ..utils import metrics as M
 
+
+def _nullctx():
+    import contextlib
+
+    return contextlib.nullcontext()
+
 # high-priority HIP streams for concurrent serving embeddings (one per in-flight micro-batch)
 EMBED_STREAMS = int(os.environ.get("LK_EMBED_STREAMS", "2"))
+# bulk embedding (index build): consecutive micro-batches alternate over this many HIP streams,
+# so one batch's memory-bound kernels (attention, LayerNorm, pooling) and its GEMMs' partial last
+# waves overlap the next batch's work instead of draining the device between kernels
+BUILD_STREAMS = int(os.environ.get("LK_EMBED_BUILD_STREAMS", "2"))
 
 
 class EmbeddingEngine:
@@ -53,13 +63,14 @@ class EmbeddingEngine:
         return flat.astype(np.int32), lens
 
     @torch.inference_mode()
-    def _run(self, flat: np.ndarray, lens: np.ndarray, out: torch.Tensor, row0: int):
+    def _run(self, flat: np.ndarray, lens: np.ndarray, out: torch.Tensor, row0: int, streams=None):
         """Embed packed sequences into out[row0:]: token-budgeted varlen micro-batches,
-        launched asynchronously (the caller tokenises the next texts meanwhile)."""
+        launched asynchronously (the caller tokenises the next texts meanwhile).  With
+        ``streams`` the micro-batches alternate over them (the caller joins them afterwards)."""
         d = self.device
         starts = np.zeros(len(lens) + 1, dtype=np.int64)
         starts[1:] = np.cumsum(lens)
-        i = 0
+        i, k = 0, 0
         while i < len(lens):
             j = i + 1
             while j < len(lens) and starts[j + 1] - starts[i] <= self.budget:
@@ -68,11 +79,13 @@ class EmbeddingEngine:
             ln = lens[i:j]
             pos = (np.arange(b - a, dtype=np.int64) - np.repeat(starts[i:j] - a, ln)).astype(np.int32)
             cu = (starts[i:j + 1] - a).astype(np.int32)
-            emb = self.model(torch.from_numpy(flat[a:b]).to(d, non_blocking=True),
-                             torch.from_numpy(cu).to(d, non_blocking=True),
-                             torch.from_numpy(pos).to(d, non_blocking=True), ln.tolist())
-            out[row0 + i:row0 + j] = emb
-            i = j
+            st = streams[k % len(streams)] if streams else None
+            with torch.cuda.stream(st) if st is not None else _nullctx():
+                emb = self.model(torch.from_numpy(flat[a:b]).to(d, non_blocking=True),
+                                 torch.from_numpy(cu).to(d, non_blocking=True),
+                                 torch.from_numpy(pos).to(d, non_blocking=True), ln.tolist())
+                out[row0 + i:row0 + j] = emb
+            i, k = j, k + 1
 
     @torch.inference_mode()
     def embed_ids(self, seqs: list[list[int]]) -> torch.Tensor:
@@ -83,14 +96,28 @@ class EmbeddingEngine:
         return out
 
     @torch.inference_mode()
-    def _embed_texts(self, texts: list[str], group: int = 4096) -> torch.Tensor:
+    def _embed_texts(self, texts: list[str], group: int = 4096, bulk: bool = False) -> torch.Tensor:
         """Tokenise group by group: group g+1 is tokenised on the CPU (native encoder,
-        GIL released) while the device runs group g's encoder batches."""
+        GIL released) while the device runs group g's encoder batches.  ``bulk`` (index
+        builds): the micro-batches alternate over BUILD_STREAMS streams, joined at the end."""
         out = torch.empty((len(texts), self.dim), dtype=torch.float32, device=self.device)
+        streams = None
+        if bulk and self.device.type == "cuda" and BUILD_STREAMS > 1 and len(texts) > group:
+            if getattr(self, "_build_streams", None) is None:
+                self._build_streams = [torch.cuda.Stream(self.device) for _ in range(BUILD_STREAMS)]
+            streams = self._build_streams
+            cur = torch.cuda.current_stream(self.device)
+            for st in streams:  # out (and anything before it) exists before the side streams write
+                st.wait_stream(cur)
+                out.record_stream(st)
         for g0 in range(0, len(texts), group):
             ids = self.tok.encode_for_embedding(texts[g0:g0 + group], self.max_len)
             flat, lens = self._flat(ids)
-            self._run(flat, lens, out, g0)
+            self._run(flat, lens, out, g0, streams)
+        if streams:
+            cur = torch.cuda.current_stream(self.device)
+            for st in streams:
+                cur.wait_stream(st)
         return out
 
     def embed_cpu(self, texts: list[str]) -> torch.Tensor:
@@ -123,6 +150,6 @@ class EmbeddingEngine:
     def embed(self, texts: list[str]) -> torch.Tensor:
         t0 = time.perf_counter()
         with self.lock:
-            r = self._embed_texts(list(texts)) if texts else torch.zeros((0, self.dim))
+            r = self._embed_texts(list(texts), bulk=True) if texts else torch.zeros((0, self.dim))
         M.EMBED_LAT.observe(time.perf_counter() - t0)
         return r

@@ -291,3 +291,24 @@ def test_fused_prefill_chain_matches_hf(monkeypatch):
     monkeypatch.setattr(ops, "PREFILL_CHAIN", False)
     plain = [s.output_ids for s in _engine(m, use_graphs=True).generate(prompts, SamplingParams.greedy(10))]
     _assert_same_or_near_tie(hf, prompts, fused, plain)
+
+
+def test_bulk_embedding_two_streams_bit_identical(monkeypatch):
+    """Index-build embedding with micro-batches alternating over two HIP streams writes exactly
+    the vectors of the one-stream build (same kernels, same inputs; every stream-K / split-K
+    workspace is per stream or per call)."""
+    from llm_kubernetes_minikube_sharp4dev_amd.engine import embed_engine
+    from llm_kubernetes_minikube_sharp4dev_amd.models.tokenizer import builtin_tokenizer
+    from llm_kubernetes_minikube_sharp4dev_amd.rag.corpus import build_chunks
+
+    tok = builtin_tokenizer()
+    enc = build_encoder("bge-base", device=DEV, seed=0)
+    chunks = [c[2] for c in build_chunks(1500, 0, workers=1)][:9000]
+    assert len(chunks) > 4096  # more than one tokenisation group: the bulk path engages
+    outs = []
+    for n in (1, 2):
+        monkeypatch.setattr(embed_engine, "BUILD_STREAMS", n)
+        eng = embed_engine.EmbeddingEngine(enc, tok, name="bge", max_tokens_per_batch=65536)
+        outs.append(eng.embed(chunks))
+        torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
