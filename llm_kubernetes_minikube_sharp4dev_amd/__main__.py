@@ -1,10 +1,10 @@
 """Command line.
 
-  serve           Ollama-compatible server on :11434.  One GPU: one process.  ``--gpus N``:
-                  the split server by default -- one engine-core process per GPU + 2 HTTP
-                  front-end processes sharing the port (SO_REUSEPORT), each routing over
-                  every core; ``--frontends F`` sets F (also on one GPU); ``--frontends 0``
-                  with ``--gpus N`` keeps the round-2 layout (N replica servers + one proxy)
+  serve           Ollama-compatible server on :11434.  On GPUs the split server by default --
+                  one engine-core process per GPU + 2 HTTP front-end processes sharing the
+                  port (SO_REUSEPORT), each routing over every core; ``--frontends F`` sets F;
+                  ``--frontends 0``: one process on one GPU / the CPU, and with ``--gpus N``
+                  the round-2 layout (N replica servers + one proxy)
   serve-core      one engine core (GPU process of the split server)
   serve-frontend  one HTTP front-end of the split server
   rag-app         Minimal_RAG port (:5103): /health, /rag/search, /agent_rag
@@ -64,10 +64,15 @@ def _uvicorn(app, host, port, name="http"):
 
 def cmd_serve(args):
     if args.frontends is None:
-        # several GPUs: the split server (engine core per GPU + 2 SO_REUSEPORT front-ends) by
-        # default, so no single Python loop relays every replica's NDJSON chunks; one GPU: the
-        # one-process server unless asked
-        args.frontends = 2 if args.gpus > 1 else 0
+        # on GPUs the split server (engine core per GPU + 2 SO_REUSEPORT front-ends) by default:
+        # no single Python loop relays every replica's NDJSON chunks, and HTTP framing and
+        # (de)tokenisation leave the GPU process (one MI355X at 128 sessions: 93.95 vs 87.31 q/s,
+        # profiles/r3_http_split/); on the CPU the one-process server.  device_count() does not
+        # initialise the GPU, so the cores can still be started as fresh processes.
+        import torch
+
+        on_gpu = args.device != "cpu" and torch.cuda.device_count() > 0
+        args.frontends = 2 if (args.gpus > 1 or on_gpu) else 0
     if args.frontends > 0:
         return _serve_split(args)
     if args.gpus > 1:  # --frontends 0: the round-2 single-proxy router over replica servers
@@ -371,7 +376,7 @@ def main(argv=None):
     p.add_argument("--preload", action="append")
     p.add_argument("--frontends", type=int, default=None,
                    help="split server: HTTP front-end processes (SO_REUSEPORT) in front of the engine core(s); "
-                        "default 2 with --gpus > 1, else 0 (one process); 0 with --gpus > 1 = single-proxy router")
+                        "default 2 on GPUs, 0 (one process) on the CPU; 0 with --gpus > 1 = single-proxy router")
     p.set_defaults(fn=cmd_serve)
     p = common(sub.add_parser("serve-core"), 0)
     p.add_argument("--socket", required=True)
