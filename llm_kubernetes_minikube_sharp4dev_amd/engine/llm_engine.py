@@ -48,6 +48,17 @@ def _jump_ok(p: SamplingParams) -> bool:
     return p.logits_processor is not None and (p.repeat_penalty == 1.0 or p.repeat_last_n == 0)
 
 
+def _small_buckets() -> tuple:
+    """LK_SMALL_STEP_ALIGN: "1" = the decode GEMMs' row buckets (64, 128, 192, 256), or an
+    explicit comma list; unset / "0" = off (Scheduler.small_buckets)."""
+    v = os.environ.get("LK_SMALL_STEP_ALIGN", "0")
+    if v in ("", "0"):
+        return ()
+    if v == "1":
+        return (64, 128, 192, 256)
+    return tuple(int(x) for x in v.split(","))
+
+
 class LLMEngine:
     def __init__(self, model, tokenizer=None, block_size: int = 16, max_model_len: int = 8192,
                  max_num_seqs: int = 256, max_num_batched_tokens: int = 65536,
@@ -65,7 +76,8 @@ class LLMEngine:
         self.scheduler = Scheduler(self.allocator, block_size, max_num_seqs, max_num_batched_tokens, max_model_len,
                                    token_align, token_align_wave, prefill_hold,
                                    int(os.environ.get("LK_HOLD_MIN_DECODE", "64")),
-                                   float(os.environ.get("LK_HOLD_FILL", "1.0")))
+                                   float(os.environ.get("LK_HOLD_FILL", "1.0")),
+                                   _small_buckets())
         self.sampler = Sampler(model.cfg.vocab_size, seed, history_len=max_model_len)
         self.max_model_len = max_model_len
         if eos_ids is None:

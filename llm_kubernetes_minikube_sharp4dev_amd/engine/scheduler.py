@@ -35,8 +35,13 @@ class Scheduler:
     def __init__(self, allocator, block_size: int, max_num_seqs: int = 256,
                  max_num_batched_tokens: int = 65536, max_model_len: int = 8192, token_align: int = 256,
                  token_align_wave: int = 0, prefill_hold: int = 0, hold_min_decode: int = 64,
-                 hold_fill: float = 1.0):
+                 hold_fill: float = 1.0, small_buckets: tuple = ()):
         self.alloc = allocator
+        # weight-streaming steps (<= small_buckets[-1] rows): prompt prefill is trimmed so the
+        # step stays in the row bucket its decode / extend rows already need (the decode GEMMs'
+        # cost steps up with the padded row count, 64 / 128 / 192 / 256); the trimmed prompt
+        # tokens lead the next step.  () = off
+        self.small_buckets = tuple(sorted(small_buckets))
         # prefill hold-back: while at least hold_min_decode decode rows keep the GPU busy, new
         # prefill waits (up to prefill_hold consecutive steps) until it fills the step's token
         # budget (hold_fill x max_num_batched_tokens): the prefill GEMMs then run on whole waves
@@ -180,7 +185,34 @@ class Scheduler:
             batch.items.append((seq, seq.num_computed, n))
             budget -= n
         self._align(batch)
+        self._align_small(batch)
         return batch
+
+    def _align_small(self, batch: ScheduledBatch):
+        if not self.small_buckets:
+            return
+        total = batch.num_tokens
+        if total > self.small_buckets[-1]:
+            return
+        fixed = sum(n for seq, _, n in batch.items if self._generating(seq))
+        if fixed == 0 or fixed == total:  # a pure prefill step, or nothing to trim
+            return
+        cap = next(b for b in self.small_buckets if b >= fixed)
+        ex = total - cap
+        if ex <= 0:
+            return
+        for k in range(len(batch.items) - 1, -1, -1):
+            seq, st, n = batch.items[k]
+            if self._generating(seq):
+                continue
+            cut = min(ex, n)
+            if cut == n:
+                del batch.items[k]  # the whole chunk waits for the next step (its blocks stay reserved)
+            else:
+                batch.items[k] = (seq, st, n - cut)
+            ex -= cut
+            if not ex:
+                return
 
     def _align(self, batch: ScheduledBatch):
         a = self.token_align

@@ -229,6 +229,39 @@ def test_prefill_hold_back_same_tokens_fuller_steps(monkeypatch):
     assert part1 < part0, (part0, part1)
 
 
+def test_small_step_bucket_alignment_same_tokens(monkeypatch):
+    """LK_SMALL_STEP_ALIGN: a weight-streaming step (<= the largest bucket in rows) with decode
+    rows trims prompt prefill to the row bucket its decode rows need (the trimmed tokens lead the
+    next step): same greedy tokens as without it, and no step mixes decode rows with prefill
+    past that bucket."""
+    m = build_decoder("llama-tiny", dtype=torch.float32)
+    prompts = [list(range(3, 3 + n)) for n in (40, 33, 25, 30, 17, 22, 35, 28)]
+
+    def run(buckets):
+        monkeypatch.setenv("LK_SMALL_STEP_ALIGN", buckets)
+        eng = _engine(m, max_num_batched_tokens=64, token_align=0)
+        eng.step_trace = []
+        seqs = [eng.add_request(p, SamplingParams.greedy(12)) for p in prompts[:3]]
+        it = 0
+        while eng.has_work() or len(seqs) < len(prompts):
+            if it % 3 == 2 and len(seqs) < len(prompts):
+                seqs.append(eng.add_request(prompts[len(seqs)], SamplingParams.greedy(12)))
+            eng.step()
+            it += 1
+        return [s.output_ids for s in seqs], eng.step_trace
+
+    ref, _ = run("0")
+    got, tr = run("4,8,16")
+    assert got == ref
+    trimmed = 0
+    for npre, ndec, *_ in tr:  # (prefill tokens, decode rows, ...)
+        if npre and ndec and npre + ndec <= 16:  # a step the alignment applies to
+            cap = next(b for b in (4, 8, 16) if b >= ndec)
+            assert npre + ndec <= cap, (npre, ndec)
+            trimmed += npre + ndec == cap
+    assert trimmed  # the policy engaged
+
+
 def test_fused_decode_ops_cpu_fallback():
     """ops.linear_add_rmsnorm / ops.linear_rope_kv on CPU tensors are the unfused
     reference ops (the HIP fusions only exist for split-K decode shapes on the GPU)."""
