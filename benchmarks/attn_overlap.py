@@ -28,6 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--md", default=None)
     ap.add_argument("--rounds", type=int, default=15)
+    ap.add_argument("--splits", default="64,96,128,160", type=lambda v: [int(x) for x in v.split(",")])
     a = ap.parse_args()
     Hq, Hkv, D, BS = 32, 8, 128, 16
     # decode rows: 128 x 1000 keys, its own blocks
@@ -66,6 +67,8 @@ def main():
         ops.paged_decode(qd, kv[0], kv[1], bt_d, cl_d, sc, out=out_d)
 
     def arm(name):
+        if name in extra:
+            return masked_arm(*extra[name])
         kv = copies[it[0] % 2]
         it[0] += 1
         if name == "flash":
@@ -87,7 +90,63 @@ def main():
             ev2.record(side)
             torch.cuda.current_stream().wait_event(ev2)
 
+    # CU-partitioned arms: flash and decode on two streams restricted to disjoint CU sets
+    # (hipExtStreamCreateWithCUMask), K CUs for decode; "lo" = CUs [0, K), "il" = every
+    # (256 / K)-th CU
+    L = ops.lib()
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    nw = (ncu + 31) // 32
+
+    def words(cus):
+        w = [0] * nw
+        for c in cus:
+            w[c // 32] |= 1 << (c % 32)
+        return w
+
+    masked = {}
+    for K in a.splits:
+        for lay in ("lo", "il"):
+            if lay == "lo":
+                dec = list(range(K))
+            else:
+                step = ncu / K
+                dec = sorted({int(i * step) for i in range(K)})
+            fl = [c for c in range(ncu) if c not in set(dec)]
+            masked[(K, lay)] = (torch.cuda.ExternalStream(L.cu_mask_stream(words(dec))),
+                                torch.cuda.ExternalStream(L.cu_mask_stream(words(fl))))
+
+    def masked_arm(K, lay, which):
+        sd, sf = masked[(K, lay)]
+        kv = copies[it[0] % 2]
+        it[0] += 1
+        cur = torch.cuda.current_stream()
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        joins = []
+        if which in ("both", "decode"):
+            sd.wait_event(ev)
+            with torch.cuda.stream(sd):
+                decode(kv)
+            e = torch.cuda.Event()
+            e.record(sd)
+            joins.append(e)
+        if which in ("both", "flash"):
+            sf.wait_event(ev)
+            with torch.cuda.stream(sf):
+                flash(kv)
+            e = torch.cuda.Event()
+            e.record(sf)
+            joins.append(e)
+        for e in joins:
+            cur.wait_event(e)
+
     arms = ["flash", "decode", "serial", "2s_flash_first", "2s_decode_first"]
+    extra = {}
+    for (K, lay) in masked:
+        for which in ("both", "decode", "flash"):
+            name = f"mask{K}{lay}_{which}"
+            arms.append(name)
+            extra[name] = (K, lay, which)
     for n in arms:
         arm(n)
     torch.cuda.synchronize()
@@ -102,6 +161,9 @@ def main():
             ts_[n].append(e0.elapsed_time(e1) * 1e3)
     med = {n: statistics.median(v) for n, v in ts_.items()}
     lines = ["| arm | us |", "|---|---|"] + [f"| {n} | {med[n]:.1f} |" for n in arms]
+    if L is not None:
+        lines.append(f"\nCU masks of the decode streams: " + "; ".join(
+            f"{K}{lay}: {L.stream_cu_mask(masked[(K, lay)][0].cuda_stream, nw)}" for (K, lay) in list(masked)[:2]))
     lines.append(f"\nsum of the two alone {med['flash'] + med['decode']:.1f} us, max {max(med['flash'], med['decode']):.1f} us")
     print("\n".join(lines), flush=True)
     if a.md:

@@ -812,6 +812,24 @@ extern "C" const char lk_source_stamp[];
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("window_mark", [](int64_t id) { CHECK_RC(lk_window_mark((int)id, cur_stream()), "window_mark"); });
+  // a HIP stream restricted to the CUs of a bit mask (32 CUs per word): two kernels that
+  // would each fill the chip (a mixed step's flash prefill and paged decode) run side by side
+  // on disjoint CU sets.  Returned as an integer handle for torch.cuda.ExternalStream; the
+  // stream lives for the process.
+  m.def("cu_mask_stream", [](std::vector<int64_t> words) {
+    std::vector<uint32_t> w(words.size());
+    for (size_t i = 0; i < words.size(); ++i) w[i] = (uint32_t)(words[i] & 0xffffffffLL);
+    hipStream_t st = nullptr;
+    TORCH_CHECK(hipExtStreamCreateWithCUMask(&st, (uint32_t)w.size(), w.data()) == hipSuccess,
+                "hipExtStreamCreateWithCUMask failed");
+    return (int64_t)reinterpret_cast<uintptr_t>(st);
+  });
+  m.def("stream_cu_mask", [](int64_t handle, int64_t nwords) {
+    std::vector<uint32_t> w((size_t)nwords, 0u);
+    TORCH_CHECK(hipExtStreamGetCUMask(reinterpret_cast<hipStream_t>((uintptr_t)handle), (uint32_t)nwords, w.data()) ==
+                    hipSuccess, "hipExtStreamGetCUMask failed");
+    return std::vector<int64_t>(w.begin(), w.end());
+  });
   m.def("source_stamp", [] { return std::string(lk_source_stamp + 8); });
   py::class_<XgmiAr>(m, "XgmiAr")
       .def(py::init<int, int, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("bytes"))
