@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""In-process A/Bs of the prefill GEMM's epilogue work (csrc/gemm.hip), cold weights (rotated
-through > 600 MB of copies, as in serving), HIP events, interleaved rounds, medians:
+"""In-process A/B of the prefill GEMM's fused epilogue work (csrc/gemm.hip), cold weights (rotated
+through > 600 MB of copies, as in serving), HIP events, interleaved rounds, medians.  (Round 4's
+LDS-staged-store arm was removed with the variant: profiles/r4_kernels/gemm_epi_ab.md.)
 
-* ``staged``: fragment stores vs LDS-staged whole-row stores (LK_GEMM_EPI_LDS), per shape;
 * ``chain``: one decoder block's unfused prefill tail (QKV GEMM -> rope_kv_; O GEMM -> add+RMSNorm;
   gate_up+SwiGLU; down GEMM -> add+RMSNorm) vs the fused chain (QKV epilogue with RoPE + KV
   write and the input-norm scale; O / down RESID epilogues with partial sums of squares;
@@ -24,10 +24,6 @@ import torch  # noqa: E402
 from llm_kubernetes_minikube_sharp4dev_amd import ops  # noqa: E402
 from llm_kubernetes_minikube_sharp4dev_amd.ops import reference as ref  # noqa: E402
 
-SHAPES = [(6144, 4096, 0), (4096, 4096, 0), (28672, 4096, 1), (4096, 14336, 0), (3072, 768, 3), (768, 3072, 2),
-          (2304, 768, 2)]
-
-
 def _time(fns: dict, rounds: int = 7) -> dict:
     ts = {k: [] for k in fns}
     for f in fns.values():
@@ -47,38 +43,6 @@ def _time(fns: dict, rounds: int = 7) -> dict:
 def _copies(w, cold=600 << 20):
     n = max(1, -(-cold // (w.numel() * 2)))
     return [w] + [w.clone() for _ in range(n - 1)]
-
-
-def staged(ms, lines):
-    L = ops.lib()
-    lines.append("| M | N | K | epi | bn | fragment stores us | LDS-staged us | speedup |")
-    lines.append("|---|---|---|---|---|---|---|---|")
-    for M in ms:
-        for N, K, epi in SHAPES:
-            if K == 768 and M < 16384:
-                Mx = 32768
-            else:
-                Mx = M
-            x = torch.randn(Mx, K, device="cuda", dtype=torch.bfloat16)
-            w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
-            b = torch.zeros(N, device="cuda", dtype=torch.bfloat16) if epi >= 2 else None
-            cfg = ops._gemm_default(Mx, N, K, epi)
-            if cfg is None or cfg[2] != 1:
-                continue
-            cs = _copies(w)
-            rot = [0]
-
-            def run(mode, cs=cs, x=x, b=b, cfg=cfg, epi=epi):
-                L.gemm_epi_lds(mode)
-                rot[0] = (rot[0] + 1) % len(cs)
-                L.gemm(x, cs[rot[0]], b, epi, cfg[1], None, cfg[0])
-
-            t = _time({"frag": lambda: run(0), "lds": lambda: run(1)})
-            lines.append(f"| {Mx} | {N} | {K} | {epi} | {cfg[1]} | {t['frag']:.1f} | {t['lds']:.1f} | "
-                         f"{t['frag'] / t['lds']:.3f} |")
-            print(lines[-1], flush=True)
-            del cs
-    L.gemm_epi_lds(-1)
 
 
 def chain(ms, lines):
@@ -127,13 +91,11 @@ def chain(ms, lines):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ms", default="2048,3072,4096,8192")
-    ap.add_argument("--only", default="staged,chain")
+    ap.add_argument("--only", default="chain")
     ap.add_argument("--md", default=None)
     a = ap.parse_args()
     ms = [int(v) for v in a.ms.split(",")]
     lines = []
-    if "staged" in a.only:
-        staged(ms, lines)
     if "chain" in a.only:
         chain(ms, lines)
     if a.md:

@@ -861,7 +861,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("resid") = py::none(), py::arg("ss_out") = py::none(), py::arg("positions") = py::none(),
         py::arg("cos_sin") = py::none(), py::arg("slots") = py::none(), py::arg("k_cache") = py::none(),
         py::arg("v_cache") = py::none(), py::arg("hq") = 0, py::arg("hkv") = 0, py::arg("hd") = 0);
-  m.def("gemm_epi_lds", [](int64_t mode) { return (int64_t)lk_gemm_epi_lds((int)mode); }, "", py::arg("mode") = -1);
   m.def("embed_rows", &embed_rows, "", py::arg("table"), py::arg("ids"), py::arg("lo") = 0, py::arg("n_local") = -1);
   m.def("scatter_ids", &scatter_ids);
   m.def("gather_rows", &gather_rows);

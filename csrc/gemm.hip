@@ -118,7 +118,9 @@ struct SkArgs {
 enum { SK_FULL = 0, SK_PARTIAL = 1, SK_FINAL = 2 };
 constexpr int kSysCoherent = 1 | 16;  // buffer cache policy sc0 | sc1: past L1 and L2
 
-template <int NF, int EPI, int PH, int PRIO>
+// SC: this instantiation applies the folded-RMSNorm row scale (LkEpi::ss_in set): only those
+// carry the partial-sum prefetch registers through the K loop
+template <int NF, int EPI, int PH, int PRIO, bool SC>
 __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W,
                                            const bf16_t* __restrict__ bias, int M, int K, int I,
                                            bf16_t* __restrict__ out, long ldo, int TM, int TN, int group_m,
@@ -147,10 +149,10 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
   // row tid & 255 BEFORE the K loop (their latency hides under it; they are older than every
   // LDS-DMA, so the loop's counted vmcnt waits stay exact); the buffer range check returns 0
   // for t >= ss_nt -- no predicated loads
-  const bool has_scale = scalable(EPI) && ea.ss_in != nullptr;
+  constexpr bool has_scale = scalable(EPI) && SC;
   float ssp[16];
-  if constexpr (scalable(EPI)) {
-    if (has_scale) {
+  if constexpr (has_scale) {
+    {
       const __amdgpu_buffer_rsrc_t srs = rsrc_of(ea.ss_in, (long)ea.ss_nt * ea.ss_ld * 4);
       const unsigned base = (unsigned)(((tid >> 8) * ea.ss_ld + (long)tm * kBM + (tid & 255)) * 4);
 #pragma unroll
@@ -455,8 +457,8 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
 
   // ---- row scales of the folded RMSNorm: s[row] = rsqrt(sum of the partials / H + eps), into LDS
   float* scl = reinterpret_cast<float*>(smem + kLdsScale);
-  if constexpr (scalable(EPI)) {
-    if (has_scale && mode != SK_PARTIAL) {
+  if constexpr (has_scale) {
+    if (mode != SK_PARTIAL) {
       float part = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) part += ssp[i];
@@ -468,55 +470,32 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
     }
   }
   auto row_scale = [&](int lrow) -> float {
-    if constexpr (scalable(EPI)) return has_scale ? scl[512 + lrow] : 1.f;
+    if constexpr (has_scale) return scl[512 + lrow];
     else return 1.f;
   };
 
   // ---- epilogue: lane holds row (.. + r); fragment pair (2p, 2p+1) gives it the 8 consecutive
   // columns 32p + 8g .. +7 of its wave's 16NF (the pair_col layout); NF = 3's third fragment
-  // the 4 columns 32 + 4g .. +3
-  // LDS-staged stores (ea.stage): the bf16 output tile [256][OW] goes to the dead staging LDS
-  // (16-B chunks XOR-swizzled by row & 7), then each wave writes whole rows: one 16-B store
-  // per lane covers 2 x 512 B (or 4 x 256 B) of CONSECUTIVE output bytes, where a fragment
-  // store covers 16 rows x 64 B spread over the output's row stride
+  // the 4 columns 32 + 4g .. +3.  (An LDS-staged whole-row store variant measured 0.98-1.04x
+  // and raised every instantiation's VGPRs; removed: profiles/r4_kernels/README.md.)
   constexpr int OW = EPI == EPI_SWIGLU ? 128 : BN;  // output columns of the tile
-  constexpr int OCH = OW / 8;                       // 16-B chunks per tile row
-  const bool staged = (EPI <= EPI_BIAS_RELU) && ea.stage > 0 && mode != SK_PARTIAL;
-  unsigned char* stile = smem;
-  auto schunk = [](int lrow, int ch) { return lrow * (OW * 2) + ((ch ^ (lrow & 7)) << 4); };
   auto emit8 = [&](int lrow, int lcol, const float (&y)[8]) {  // lcol: multiple of 8
     uint4_t pk;
     pk.x = pack_bf2(y[0], y[1]);
     pk.y = pack_bf2(y[2], y[3]);
     pk.z = pack_bf2(y[4], y[5]);
     pk.w = pack_bf2(y[6], y[7]);
-    if (staged) *reinterpret_cast<uint4_t*>(stile + schunk(lrow, lcol >> 3)) = pk;
-    else *reinterpret_cast<uint4_t*>(out + (long)(tm * kBM + lrow) * ldo + (long)tn * OW + lcol) = pk;
+    *reinterpret_cast<uint4_t*>(out + (long)(tm * kBM + lrow) * ldo + (long)tn * OW + lcol) = pk;
   };
   auto emit4 = [&](int lrow, int lcol, const float (&y)[4]) {  // lcol: multiple of 4
     uint2 pk;
     pk.x = pack_bf2(y[0], y[1]);
     pk.y = pack_bf2(y[2], y[3]);
-    if (staged) *reinterpret_cast<uint2*>(stile + schunk(lrow, lcol >> 3) + ((lcol & 4) << 1)) = pk;
-    else *reinterpret_cast<uint2*>(out + (long)(tm * kBM + lrow) * ldo + (long)tn * OW + lcol) = pk;
+    *reinterpret_cast<uint2*>(out + (long)(tm * kBM + lrow) * ldo + (long)tn * OW + lcol) = pk;
   };
-  auto flush = [&]() {
-    __syncthreads();
-    constexpr int PER = 256 * OCH / 512;  // chunks per thread
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c = i * 512 + tid, lrow = c / OCH, ch = c % OCH;
-      const int row = tm * kBM + lrow;
-      const uint4_t v = *reinterpret_cast<const uint4_t*>(stile + schunk(lrow, ch));
-      if (row < M) *reinterpret_cast<uint4_t*>(out + (long)row * ldo + (long)tn * OW + ch * 8) = v;
-    }
-  };
-  // this lane's 8 row scales into registers BEFORE any staged write (the scale array lives in
-  // the same LDS the staged tile overwrites)
-  float scm[8];
+  float scm[8];  // this lane's 8 row scales (1 unless the folded-norm scale applies)
 #pragma unroll
   for (int m = 0; m < 8; ++m) scm[m] = row_scale(wr * 128 + m * 16 + r);
-  if (staged) __syncthreads();  // every wave is past its last staging / scale read
 
   if constexpr (EPI == EPI_PARTIAL) {  // fp32 partial sums of split kz: out is float [splits, M, ldo]
     float* part = reinterpret_cast<float*>(out) + (long)kz * M * ldo;
@@ -545,7 +524,6 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
           y[4 * h + v] = rbf(lk_silu(rbf(acc[m][h][v] * sc))) * rbf(acc[m][h + 2][v] * sc);
       emit8(wr * 128 + m * 16 + r, wc * 32 + 8 * g, y);
     }
-    if (staged) flush();
   } else if constexpr (EPI == EPI_RESID) {
     // producer side of the folded norm: r = bf16(r + bf16(acc)) in place, then the partial sum
     // of squares of the new r over this tile's BN columns (lanes r + 16 g, then the 4 wc waves)
@@ -720,7 +698,7 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
       const int row = tm * kBM + wr * 128 + m * 16 + r;
       if (row >= M || mode == SK_PARTIAL) continue;
       const int lrow = wr * 128 + m * 16 + r, lc = wc * 16 * NF;
-      if constexpr (EPI == EPI_NONE) {
+      if constexpr (EPI == EPI_NONE && has_scale) {
 #pragma unroll
         for (int n = 0; n < NF; ++n) acc[m][n] *= scm[m];
       }
@@ -740,7 +718,6 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
         emit4(lrow, lc + 32 + 4 * g, y);
       }
     }
-    if (staged) flush();
   }
 }
 
@@ -795,7 +772,7 @@ __global__ __launch_bounds__(64) void splitk_resid_kernel(const float* __restric
   if (threadIdx.x == 0) ea.ss_out[(long)tn * ea.ss_out_ld + row] = ss;
 }
 
-template <int NF, int EPI, int PH, int PRIO>
+template <int NF, int EPI, int PH, int PRIO, bool SC>
 __global__ __launch_bounds__(512, 1) void gemm_kernel(const bf16_t* __restrict__ X, long ldx,
                                                       const bf16_t* __restrict__ W,
                                                       const bf16_t* __restrict__ bias, int M, int K, int I,
@@ -850,8 +827,8 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const bf16_t* __restrict__
     } else {
       break;
     }
-    gemm8_body<NF, EPI, PH, PRIO>(X, ldx, W, bias, M, K, I, out, ldo, TM, TN, group_m, tile, a0, n, kz, mode, fin_end,
-                                  sk, ea);
+    gemm8_body<NF, EPI, PH, PRIO, SC>(X, ldx, W, bias, M, K, I, out, ldo, TM, TN, group_m, tile, a0, n, kz, mode,
+                                      fin_end, sk, ea);
     wait_vm<0>();
   }
 }
@@ -877,16 +854,6 @@ int group_rows() {
     return v >= 1 ? v : 4;
   }();
   return g;
-}
-
-// LDS-staged epilogue stores by default?  LK_GEMM_EPI_LDS (0 / 1); lk_gemm_set_epi_lds overrides
-int g_epi_lds = -1;
-int epi_lds_default() {
-  if (g_epi_lds < 0) {
-    const char* e = getenv("LK_GEMM_EPI_LDS");
-    g_epi_lds = e ? (atoi(e) != 0) : 0;
-  }
-  return g_epi_lds;
 }
 
 int cu_count() {
@@ -973,21 +940,32 @@ bool sk_plan(int M, int tiles, int nkt, int bn, hipStream_t st, SkArgs* sk, int*
   return true;
 }
 
-template <int NF, int EPI, int PH, int PRIO = 0>
-void launch_ph(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
+template <int NF, int EPI, int PH, int PRIO, bool SC>
+void launch_sc(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
                long ldo, int TM, int TN, int ks, hipStream_t st, const LkEpi& ea) {
   constexpr int lds = 2 * Geo<NF>::BUF;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_kernel<NF, EPI, PH, PRIO>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_kernel<NF, EPI, PH, PRIO, SC>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
   SkArgs sk{0, 0, nullptr, nullptr, nullptr, 0};
   int grid = gemm_grid(TM * TN);
   if (ks == 1 && EPI != EPI_PARTIAL) sk_plan(M, TM * TN, K / kBK, 64 * NF, st, &sk, &grid);
-  gemm_kernel<NF, EPI, PH, PRIO><<<dim3(grid, ks), 512, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN,
-                                                                   group_rows(), sk, ea);
+  gemm_kernel<NF, EPI, PH, PRIO, SC><<<dim3(grid, ks), 512, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN,
+                                                                       group_rows(), sk, ea);
+}
+template <int NF, int EPI, int PH, int PRIO = 0>
+void launch_ph(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
+               long ldo, int TM, int TN, int ks, hipStream_t st, const LkEpi& ea) {
+  if constexpr (scalable(EPI)) {
+    if (ea.ss_in != nullptr) {
+      launch_sc<NF, EPI, PH, PRIO, true>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st, ea);
+      return;
+    }
+  }
+  launch_sc<NF, EPI, PH, PRIO, false>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, st, ea);
 }
 // schedule: 0 = 4 phases per K-tile (per-cluster priority), 1 = 2 phases (static priority)
 template <int NF, int EPI>
@@ -1067,12 +1045,6 @@ int lk_gemm_streamk(int mode) {
   return errs;
 }
 
-// policy knob for in-process A/Bs: mode 0 / 1 sets the staged-epilogue default, -1 reads it
-int lk_gemm_epi_lds(int mode) {
-  if (mode >= 0) g_epi_lds = mode != 0;
-  return epi_lds_default();
-}
-
 int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks) {
   if (M < 1 || K < kBK || K % kBK || (bn != 192 && bn != 256)) return 0;
   if (ks < 1 || ks > 8 || K / kBK < 2 * ks || (ks > 1 && (epi == EPI_SWIGLU || epi == EPI_QKV || N % 4))) return 0;
@@ -1089,7 +1061,6 @@ int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks) {
 int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
             int variant, bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, const LkEpi* ea_) {
   LkEpi ea = ea_ ? *ea_ : LkEpi{};
-  if (ea.stage < 0) ea.stage = epi_lds_default();
   // fused-chain epilogue arguments (checked here: a bad pointer / shape would fault the device)
   if (ea.ss_in && (ea.ss_nt < 1 || ea.ss_nt > 32 || ea.ss_ld < M || ea.inv_h <= 0.f)) return -1;
   if (epi == EPI_RESID && (!ea.resid || !ea.ss_out || ea.ldr % 8 || ea.ss_out_ld < M)) return -1;

@@ -63,7 +63,6 @@ int lk_xgmi_allreduce(bf16_t* const* data, unsigned* const* sig, int rank, int w
 // epilogue (not SwiGLU) -- for shapes with fewer tiles than CUs
 int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks = 1);
 int lk_gemm_streamk(int mode);
-int lk_gemm_epi_lds(int mode);
 // Fused prefill-chain epilogues of lk_gemm (the RMSNorm of the pre-norm decoder block folded
 // into its neighbouring GEMMs, the norm weight g folded into the consumer's weight rows):
 //   row scale (any of epi NONE / SWIGLU / QKV, when ss_in is set): acc *= rsqrt(sum_t
@@ -90,9 +89,6 @@ struct LkEpi {
   bf16_t* kc = nullptr;          // QKV: paged caches [num_blocks, hkv, bs, hd]
   bf16_t* vc = nullptr;
   int bs = 0, hq = 0, hkv = 0, hd = 0;
-  // epilogue stores through LDS: the bf16 tile is written to the (dead) staging LDS, then
-  // leaves as whole contiguous row segments instead of 16-row x 64-B fragments
-  int stage = -1;                // -1: the library default (LK_GEMM_EPI_LDS), 0 / 1 forced
 };
 int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
             int variant, bf16_t* out, long ldo, hipStream_t st, int ks = 1, float* ws = nullptr,

@@ -2,7 +2,7 @@
 # one GPU), each step under its own timeout.
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/r4k
-timeout -k 10 400 python -u benchmarks/gemm_epi_ab.py --ms 2048,3072,4096,8192 --md gpurun_out/r4k/gemm_epi_ab.md > gpurun_out/r4k/gemm_epi_ab.log 2>&1 || { tail -20 gpurun_out/r4k/gemm_epi_ab.log; exit 3; }
+timeout -k 10 400 python -u benchmarks/gemm_epi_ab.py --ms 2048,3072,4096,8192 --only chain --md gpurun_out/r4k/gemm_epi_ab.md > gpurun_out/r4k/gemm_epi_ab.log 2>&1 || { tail -20 gpurun_out/r4k/gemm_epi_ab.log; exit 3; }
 cat gpurun_out/r4k/gemm_epi_ab.md
 timeout -k 10 300 python -u benchmarks/xgmi_floor.py --world 8 --hidden 8192 --out gpurun_out/r4k/floor_tp8_h8192.json > gpurun_out/r4k/floor.log 2>&1 || { tail -20 gpurun_out/r4k/floor.log; exit 4; }
 tail -c 1500 gpurun_out/r4k/floor_tp8_h8192.json

@@ -851,30 +851,6 @@ def test_gemm_qkv_epilogue_layout(hip):
     assert torch.equal(out.cpu(), want.cpu()) and torch.equal(kc.cpu(), kc2.cpu()) and torch.equal(vc.cpu(), vc2.cpu())
 
 
-@pytest.mark.parametrize("M,N,K,epi,bn", [(300, 1024, 512, 0, 256), (777, 3072, 768, 3, 256), (1000, 1536, 512, 2, 192),
-                                          (2049, 1792 * 2, 1024, 1, 256), (4352, 4096, 4096, 0, 256),
-                                          (513, 6144, 1024, 0, 192), (4352, 6144, 4096, 4, 192)])
-def test_gemm_lds_staged_epilogue_bit_identical(hip, M, N, K, epi, bn):
-    """LDS-staged epilogue stores (tile through the dead staging LDS, whole-row writes) write
-    exactly the bytes of the fragment stores: every epilogue, both column tiles, M tails,
-    stream-K grids (4352 rows)."""
-    torch.manual_seed(M + N + epi)
-    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
-    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
-    b = torch.randn(N, device=DEV, dtype=torch.bfloat16) if epi >= 2 else None
-    old = hip.gemm_epi_lds(-1)
-    try:
-        outs = []
-        for mode in (0, 1):
-            hip.gemm_epi_lds(mode)
-            outs.append(hip.gemm(x, w, b, epi, bn, None, 2))
-        torch.cuda.synchronize()
-    finally:
-        hip.gemm_epi_lds(old)
-    assert torch.equal(outs[0], outs[1]), (outs[0].float() - outs[1].float()).abs().max()
-    assert hip.gemm_streamk(-1) == 0
-
-
 @pytest.mark.parametrize("lo,n_local", [(0, None), (0, 300), (300, 300), (600, 424)])
 def test_embed_rows(hip, lo, n_local):
     """Token-embedding gather (full table, and a vocab-parallel shard: out-of-shard ids -> 0)."""
