@@ -28,7 +28,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--md", default=None)
     ap.add_argument("--rounds", type=int, default=15)
-    ap.add_argument("--splits", default="64,96,128,160", type=lambda v: [int(x) for x in v.split(",")])
+    ap.add_argument("--splits", default="", type=lambda v: [int(x) for x in v.split(",") if x])
+    ap.add_argument("--pads", default="56,64", type=lambda v: [int(x) for x in v.split(",") if x])
     a = ap.parse_args()
     Hq, Hkv, D, BS = 32, 8, 128, 16
     # decode rows: 128 x 1000 keys, its own blocks
@@ -69,6 +70,13 @@ def main():
     def arm(name):
         if name in extra:
             return masked_arm(*extra[name])
+        if name.startswith("pad"):
+            kb, base = name[3:].split("_", 1)
+            L.flash_lds_pad(int(kb) * 1024)
+            try:
+                return arm(base)
+            finally:
+                L.flash_lds_pad(0)
         kv = copies[it[0] % 2]
         it[0] += 1
         if name == "flash":
@@ -141,6 +149,11 @@ def main():
             cur.wait_event(e)
 
     arms = ["flash", "decode", "serial", "2s_flash_first", "2s_decode_first"]
+    # flash with an occupancy cap (unused dynamic LDS per workgroup) so a decode workgroup fits
+    # beside it on every CU, alone and on two streams with decode
+    for pad_kb in a.pads:
+        for nm in ("flash", "2s_flash_first", "2s_decode_first"):
+            arms.append(f"pad{pad_kb}_{nm}")
     extra = {}
     for (K, lay) in masked:
         for which in ("both", "decode", "flash"):
@@ -161,7 +174,7 @@ def main():
             ts_[n].append(e0.elapsed_time(e1) * 1e3)
     med = {n: statistics.median(v) for n, v in ts_.items()}
     lines = ["| arm | us |", "|---|---|"] + [f"| {n} | {med[n]:.1f} |" for n in arms]
-    if L is not None:
+    if masked:
         lines.append(f"\nCU masks of the decode streams: " + "; ".join(
             f"{K}{lay}: {L.stream_cu_mask(masked[(K, lay)][0].cuda_stream, nw)}" for (K, lay) in list(masked)[:2]))
     lines.append(f"\nsum of the two alone {med['flash'] + med['decode']:.1f} us, max {max(med['flash'], med['decode']):.1f} us")
