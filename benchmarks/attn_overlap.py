@@ -2,8 +2,10 @@
 """Do a mixed step's two attention kernels overlap?  Flash prefill over the step's prompt
 chunks (compute-bound) and paged decode over its decode rows (HBM-bound) at the serving shapes
 (Llama-3-8B heads, 6 prompts x 643 new tokens over 930 keys; 128 decode rows x 1000 keys), timed
-back to back on one stream vs on two streams (both launch orders), cold KV (rotated copies),
-HIP events, medians of interleaved rounds.
+back to back on one stream vs on two streams (both launch orders) and, with --splits, on two
+streams restricted to disjoint CU sets; cold KV (rotated copies), HIP events, medians of
+interleaved rounds.  (A flash-occupancy-cap arm -- unused LDS so a decode workgroup fits beside
+one flash workgroup per CU -- measured 190 us vs 178 serial and was removed.)
 
     python benchmarks/attn_overlap.py [--md out.md]
 """
@@ -29,7 +31,6 @@ def main():
     ap.add_argument("--md", default=None)
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--splits", default="", type=lambda v: [int(x) for x in v.split(",") if x])
-    ap.add_argument("--pads", default="56,64", type=lambda v: [int(x) for x in v.split(",") if x])
     a = ap.parse_args()
     Hq, Hkv, D, BS = 32, 8, 128, 16
     # decode rows: 128 x 1000 keys, its own blocks
@@ -70,13 +71,6 @@ def main():
     def arm(name):
         if name in extra:
             return masked_arm(*extra[name])
-        if name.startswith("pad"):
-            kb, base = name[3:].split("_", 1)
-            L.flash_lds_pad(int(kb) * 1024)
-            try:
-                return arm(base)
-            finally:
-                L.flash_lds_pad(0)
         kv = copies[it[0] % 2]
         it[0] += 1
         if name == "flash":
@@ -149,11 +143,6 @@ def main():
             cur.wait_event(e)
 
     arms = ["flash", "decode", "serial", "2s_flash_first", "2s_decode_first"]
-    # flash with an occupancy cap (unused dynamic LDS per workgroup) so a decode workgroup fits
-    # beside it on every CU, alone and on two streams with decode
-    for pad_kb in a.pads:
-        for nm in ("flash", "2s_flash_first", "2s_decode_first"):
-            arms.append(f"pad{pad_kb}_{nm}")
     extra = {}
     for (K, lay) in masked:
         for which in ("both", "decode", "flash"):

@@ -469,36 +469,8 @@ static float prefill_defer() {
   return env;
 }
 
-// occupancy cap for the flash kernel: reserve this much dynamic LDS per workgroup (unused) so
-// fewer flash workgroups fit on a CU, leaving room for a concurrent kernel's workgroups (a mixed
-// step's paged decode on a second stream); 0 = off.  lk_flash_set_lds_pad / LK_FLASH_LDS_PAD_KB
-int g_flash_pad = -1;
-static int flash_pad() {
-  if (g_flash_pad < 0) {
-    const char* e = getenv("LK_FLASH_LDS_PAD_KB");
-    g_flash_pad = e ? atoi(e) * 1024 : 0;
-  }
-  return g_flash_pad;
-}
-int lk_flash_set_lds_pad(int bytes) {
-  if (bytes >= 0) g_flash_pad = bytes;
-  return flash_pad();
-}
-
 // the query rows one workgroup covers: must use the launch's prefill_waves(G, D)
 int lk_prefill_rows_per_tile(int G, int D) { return G >= 4 ? 32 * (prefill_waves(G, D) / 4) : 32 * (4 / G); }
-
-template <typename Kern>
-static void launch_flash(Kern kern, dim3 grid, int threads, int pad, hipStream_t st, const PrefillParams& pr) {
-  if (pad > 0) {
-    static int set_for = 0;  // per instantiation: the largest pad its attribute allows
-    if (pad > set_for) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, pad);
-      set_for = pad;
-    }
-  }
-  kern<<<grid, threads, pad, st>>>(pr);
-}
 
 int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v, long ks, long vs,
                      const int* block_tables, int bt_stride, const int* cu_q, const int* ctx_lens,
@@ -523,10 +495,9 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
   const int NW = prefill_waves(G, D);
   dim3 grid(ntiles, Hq / WH);
   const bool pipe = causal && prefill_pipe();
-  const int pad = part_o ? 0 : flash_pad();
-#define L(DD, C, PG, W, N)                                                                          \
-  if (pipe) launch_flash(flash_prefill_kernel<DD, C, PG, W, N, true>, grid, 64 * N, pad, st, pr);   \
-  else launch_flash(flash_prefill_kernel<DD, C, PG, W, N, false>, grid, 64 * N, pad, st, pr)
+#define L(DD, C, PG, W, N)                                                        \
+  if (pipe) flash_prefill_kernel<DD, C, PG, W, N, true><<<grid, 64 * N, 0, st>>>(pr); \
+  else flash_prefill_kernel<DD, C, PG, W, N, false><<<grid, 64 * N, 0, st>>>(pr)
 #define BY_W(DD, C, PG)                                 \
   if (WH == 4 && NW == 8) { L(DD, C, PG, 4, (DD >= 64 ? 8 : 4)); } \
   else if (WH == 4) { L(DD, C, PG, 4, 4); }                   \

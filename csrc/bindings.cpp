@@ -884,8 +884,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_split_size", &decode_split_size);
   m.def("paged_decode", &paged_decode, "", py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("max_splits"), py::arg("split"), py::arg("scale"), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("out") = py::none(), py::arg("k_start") = py::none(), py::arg("pp_o") = py::none(), py::arg("pp_ml") = py::none());
   m.def("prefill_rows_per_tile", &prefill_rows_per_tile);
-  m.def("flash_lds_pad", [](int64_t bytes) { return (int64_t)lk_flash_set_lds_pad((int)bytes); }, "",
-        py::arg("bytes") = -1);
   m.def("flash_prefill", &flash_prefill, "", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("block_tables"), py::arg("cu_q"), py::arg("ctx_lens"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("out") = py::none(), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("q_past") = py::none());
   m.def("knn_topk", &knn_topk, "", py::arg("corpus"), py::arg("cnorm"), py::arg("queries"), py::arg("qnorm"),
         py::arg("K"), py::arg("force_fused") = false);

@@ -117,7 +117,6 @@ int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc
 
 // attn_prefill.hip
 int lk_prefill_rows_per_tile(int G, int D);
-int lk_flash_set_lds_pad(int bytes);  // -1: read; >= 0: set (bytes of unused dynamic LDS per flash workgroup)
 int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v, long ks, long vs,
                      const int* block_tables, int bt_stride, const int* cu_q, const int* ctx_lens,
                      const int* tile_seq, const int* tile_q0, int ntiles, bf16_t* out, long os,

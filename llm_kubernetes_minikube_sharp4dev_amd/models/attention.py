@@ -22,11 +22,6 @@ from .. import ops
 # paged decode ~84 us per layer) it read 103.38 / 103.18 vs 102.97 / 102.81 q/s with identical
 # schedules (mixed-step GPU time -0.45 %, profiles/r3_overlap/): on by default.
 OVERLAP_ATTN = os.environ.get("LK_OVERLAP_ATTN", "1") == "1"
-# ... with the flash kernel's occupancy capped by this much unused LDS per workgroup (KB) while
-# the decode kernel runs beside it, so a decode workgroup fits on every CU next to a flash one
-# (the flash kernel's 248-VGPR workgroups otherwise fill the CUs two at a time and the second
-# stream waits: profiles/r4_kernels/attn_overlap_*.md); 0 = no cap
-OVERLAP_PAD_KB = int(os.environ.get("LK_OVERLAP_PAD_KB", "0"))
 _side: dict = {}
 
 
@@ -127,17 +122,10 @@ def paged_attention(qkv: torch.Tensor, k_cache, v_cache, meta: AttnMeta, Hq: int
         out.record_stream(side)
     if Tp:
         meta.ensure_tiles(Hq, Hkv, qkv.device, D)
-        pad = side is not None and OVERLAP_PAD_KB > 0
-        if pad:
-            ops.lib().flash_lds_pad(OVERLAP_PAD_KB * 1024)
-        try:
-            ops.flash_prefill(qkv[:Tp, : Hq * D], k_cache, v_cache, meta.cu_q, Hq, Hkv, D, scale, True,
-                              block_tables=meta.block_tables_p, ctx_lens=meta.ctx_lens_p,
-                              q_lens_cpu=meta.q_lens_cpu, ctx_lens_cpu=meta.ctx_lens_cpu,
-                              tiles=meta.tiles, out=out[:Tp])
-        finally:
-            if pad:
-                ops.lib().flash_lds_pad(0)
+        ops.flash_prefill(qkv[:Tp, : Hq * D], k_cache, v_cache, meta.cu_q, Hq, Hkv, D, scale, True,
+                          block_tables=meta.block_tables_p, ctx_lens=meta.ctx_lens_p,
+                          q_lens_cpu=meta.q_lens_cpu, ctx_lens_cpu=meta.ctx_lens_cpu,
+                          tiles=meta.tiles, out=out[:Tp])
     if side is not None:
         torch.cuda.current_stream(qkv.device).wait_stream(side)
     elif Bd:

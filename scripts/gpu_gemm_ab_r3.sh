@@ -1,10 +1,10 @@
-# Prefill GEMM: this tree's gemm.hip vs round 3's (commit 457622b, built into build/ablib/_C_r3.so),
+# Prefill GEMM: this tree's gemm.hip vs round 3's (commit 457622b, built into ablib/_C_r3.so),
 # alternating processes, cold weights, each shape's dispatch-policy config
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/gab
 SETS=${SETS:-"llama:768,1024,4096,8192;bge:131072"}
 for r in 1 2; do
-  timeout -k 10 300 python benchmarks/gemm_ab_lib.py --lib build/ablib/_C_r3.so --tag r3 --sets "$SETS" > gpurun_out/gab/r3_$r.log 2>&1 || { tail -5 gpurun_out/gab/r3_$r.log; exit 2; }
+  timeout -k 10 300 python benchmarks/gemm_ab_lib.py --lib ablib/_C_r3.so --tag r3 --sets "$SETS" > gpurun_out/gab/r3_$r.log 2>&1 || { tail -5 gpurun_out/gab/r3_$r.log; exit 2; }
   timeout -k 10 300 python benchmarks/gemm_ab_lib.py --tag r4 --sets "$SETS" > gpurun_out/gab/r4_$r.log 2>&1 || { tail -5 gpurun_out/gab/r4_$r.log; exit 3; }
 done
 python - <<'PY'
