@@ -196,6 +196,12 @@ def main():
     from llm_kubernetes_minikube_sharp4dev_amd.rag.synthetic import make_queries
 
     on_gpu = args.device == "cuda"
+    if on_gpu and args.one_device:
+        # several processes' hardware queues share the device: at 4 per process the scheduler
+        # time-slices 8 ranks and every all-reduce waits for its peers' turn (0.08 vs 2.46 q/s at
+        # 2 per process, profiles/r4_tp8_onedev/); read when HIP initialises, so set it first
+        if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) > 2:
+            os.environ["GPU_MAX_HW_QUEUES"] = "2"
     if on_gpu:
         assert torch.cuda.is_available(), "bench.py needs an MI355X (or --device cpu)"
         if args.one_device:
