@@ -1,3 +1,4 @@
+# (ablib/ is gpurun-ignored: remove it from .gpurunignore to rerun.)
 # Prefill GEMM: this tree's gemm.hip vs round 3's (commit 457622b, built into ablib/_C_r3.so),
 # alternating processes, cold weights, each shape's dispatch-policy config
 set -o pipefail
