@@ -884,6 +884,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_split_size", &decode_split_size);
   m.def("paged_decode", &paged_decode, "", py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("max_splits"), py::arg("split"), py::arg("scale"), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("out") = py::none(), py::arg("k_start") = py::none(), py::arg("pp_o") = py::none(), py::arg("pp_ml") = py::none());
   m.def("prefill_rows_per_tile", &prefill_rows_per_tile);
+  m.def("ws_set_variant", [](int64_t M, int64_t N, int64_t K, bool swiglu, int64_t v) {
+    CHECK_RC(lk_wsgemm_set_variant((int)M, (int)N, (int)K, swiglu ? 1 : 0, (int)v), "ws_set_variant");
+  }, "weight-streaming GEMM kernel for this (M bucket, N, K, swiglu): 0 ring, 1 loader waves, -1 default",
+        py::arg("M"), py::arg("N"), py::arg("K"), py::arg("swiglu"), py::arg("variant"));
   m.def("flash_prefill", &flash_prefill, "", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("block_tables"), py::arg("cu_q"), py::arg("ctx_lens"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("out") = py::none(), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("q_past") = py::none());
   m.def("knn_topk", &knn_topk, "", py::arg("corpus"), py::arg("cnorm"), py::arg("queries"), py::arg("qnorm"),
         py::arg("K"), py::arg("force_fused") = false);

@@ -35,6 +35,7 @@ int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, i
 
 // GEMM part only (S >= 2): f32 partial slabs part[S][M][N], for a consumer that fuses the
 // split-K reduction (lk_splitk_rmsnorm, lk_splitk_rope_kv)
+int lk_wsgemm_set_variant(int M, int N, int K, int swiglu, int variant);  // -1 = back to the default
 int lk_wsgemm_part(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, float* part,
                    hipStream_t st);
 

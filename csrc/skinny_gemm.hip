@@ -26,6 +26,9 @@
 // up columns I + [...]; out[m][j] = bf16(silu(bf16(g)) ) * bf16(u), rounded like
 // the unfused linear -> silu_mul path (bit-identical to it).
 #include <algorithm>
+#include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "common.h"
 #include "kernels.h"
@@ -428,6 +431,201 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Loader-wave variant of the weight-streaming GEMM ("lw").  s_waitcnt vmcnt retires a wave's
+// vector-memory ops in issue order, so in wsgemm_kernel -- X and W of a stage issued together by
+// the same waves -- the W prefetch can run only as far ahead as the shared ring, and at M 192-256
+// (X stages twice the W stages) that is 1-2 stages: the W stream ran 3.0-3.9 TB/s, in proportion
+// to the W bytes in flight per CU.  Here the W stream has waves of its own (2 loader waves, their
+// own vmcnt): 4 compute waves stage X through a short ring (L2-resident, 2-3 stages) and compute;
+// the loader waves keep NSW - 1 W stages (all the remaining LDS) in flight; one s_barrier per
+// stage joins them.  Same tile, swizzles, K rotation and epilogue as wsgemm_kernel.
+constexpr int lw_nsx(int MT) { return MT <= 8 ? 3 : 2; }
+constexpr int lw_nsw(int MT, int BN) {
+  const int n = (163840 - lw_nsx(MT) * 16 * MT * 128) / (BN * 128);
+  return n > 12 ? 12 : n;
+}
+
+template <int MT, int BN, bool SWIGLU>
+__global__ __launch_bounds__(384, 1) void wsgemm_lw_kernel(const bf16_t* __restrict__ X, long ldx,
+                                                           const bf16_t* __restrict__ W, int M, int K, int ks,
+                                                           int n_tiles, int swiglu_I, bf16_t* __restrict__ out,
+                                                           long ldo, float* __restrict__ part, long part_ld,
+                                                           long n_rows, int rot_mul) {
+  constexpr int ROWS = 16 * MT;
+  constexpr int MTW = MT / 4;
+  constexpr int NT = BN / 16;
+  constexpr int XB = ROWS * 128;
+  constexpr int WB = BN * 128;
+  constexpr int NSX = lw_nsx(MT);
+  constexpr int NSW = lw_nsw(MT, BN);
+  constexpr int LX = ROWS / 32;  // X glds per compute wave per stage (4 waves x 8 rows)
+  constexpr int LW = BN / 16;    // W glds per loader wave per stage (2 waves x 8 rows)
+  static_assert(NSW >= 3, "W ring");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* xring = smem;
+  unsigned char* wring = smem + NSX * XB;
+
+  const int t = blockIdx.x % n_tiles, s = blockIdx.x / n_tiles;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool loader = w >= 4;
+  const int r = lane & 15, g = lane >> 4;
+  const long kbase = (long)s * ks;
+  const int nst = ks / 64;
+  const int rot = rot_mul ? (int)(((long)t * rot_mul) % nst) : 0;
+  auto kof = [&](int st) { return (st + rot < nst ? st + rot : st + rot - nst) * 64; };
+
+  auto wrow = [&](int row) -> long {
+    if constexpr (SWIGLU) {
+      return row < BN / 2 ? (long)t * (BN / 2) + row : (long)swiglu_I + (long)t * (BN / 2) + row - BN / 2;
+    } else {
+      return (long)t * BN + row;
+    }
+  };
+  const int lrow = lane >> 3, lch = lane & 7;
+
+  floatx4 acc[MTW][NT];
+#pragma unroll
+  for (int m = 0; m < MTW; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  if (loader) {
+    const int lw = w - 4;
+    const bf16_t* wsrc[LW];
+#pragma unroll
+    for (int i = 0; i < LW; ++i) {
+      const int row = (lw * LW + i) * 8 + lrow;
+      wsrc[i] = W + min(wrow(row), n_rows - 1) * K + kbase + ((lch ^ wsz(row)) * 8);
+    }
+    auto issue_w = [&](int st) {
+      unsigned char* base = wring + (st % NSW) * WB;
+#pragma unroll
+      for (int i = 0; i < LW; ++i)
+        __builtin_amdgcn_global_load_lds((gbl_void_ptr)(wsrc[i] + kof(st)),
+                                         (lds_void_ptr)(base + (lw * LW + i) * 8 * 128), 16, 0, 2);
+    };
+#pragma unroll
+    for (int p = 0; p < NSW - 1; ++p)
+      if (p < nst) issue_w(p);
+    for (int st = 0; st < nst; ++st) {
+      wait_ahead<LW, NSW>(min(NSW - 2, nst - 1 - st));  // W(st) landed, later stages in flight
+      __builtin_amdgcn_s_barrier();                      // ... and ring slot (st - 1) % NSW is free
+      __builtin_amdgcn_sched_barrier(0);
+      if (st + NSW - 1 < nst) issue_w(st + NSW - 1);
+    }
+    return;  // the epilogue is the compute waves' (no barrier after the loop)
+  }
+
+  const bf16_t* xsrc[LX];
+#pragma unroll
+  for (int i = 0; i < LX; ++i) {
+    const int row = (w * LX + i) * 8 + lrow;
+    xsrc[i] = X + (long)min(row, M - 1) * ldx + kbase + ((lch ^ wsz(row)) * 8);
+  }
+  auto issue_x = [&](int st) {
+    unsigned char* base = xring + (st % NSX) * XB;
+#pragma unroll
+    for (int i = 0; i < LX; ++i)
+      __builtin_amdgcn_global_load_lds((gbl_void_ptr)(xsrc[i] + kof(st)),
+                                       (lds_void_ptr)(base + (w * LX + i) * 8 * 128), 16, 0, 0);
+  };
+  auto compute = [&](int st) {
+    const unsigned char* xb = xring + (st % NSX) * XB;
+    const unsigned char* wb = wring + (st % NSW) * WB;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = 4 * h + g;
+      short8 a[MTW], b[NT];
+#pragma unroll
+      for (int m = 0; m < MTW; ++m) {
+        const int row = w * (4 * MT) + 16 * m + r;
+        a[m] = *reinterpret_cast<const short8*>(xb + row * 128 + ((c ^ wsz(row)) << 4));
+      }
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const int row = 16 * n + r;
+        b[n] = *reinterpret_cast<const short8*>(wb + row * 128 + ((c ^ wsz(row)) << 4));
+      }
+#pragma unroll
+      for (int m = 0; m < MTW; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[n], a[m], acc[m][n], 0, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int p = 0; p < NSX - 1; ++p)
+    if (p < nst) issue_x(p);
+  for (int st = 0; st < nst; ++st) {
+    wait_ahead<LX, NSX>(min(NSX - 2, nst - 1 - st));  // X(st) landed (the W side waits in the loaders)
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + NSX - 1 < nst) issue_x(st + NSX - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(st);
+  }
+
+  // ---- epilogue (as wsgemm_kernel): lane holds row 16m + r of its wave's rows, tile columns
+  // 16n + 4g .. +3
+  const bool split = part != nullptr;
+  const bool part_vec = split && part_ld % 4 == 0 && reinterpret_cast<uintptr_t>(part) % 16 == 0;
+  const bool out_vec = ldo % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 8 == 0;
+#pragma unroll
+  for (int m = 0; m < MTW; ++m) {
+    const int row = w * (4 * MT) + 16 * m + r;
+    if (row >= M) continue;
+    if (SWIGLU && !split) {
+#pragma unroll
+      for (int n = 0; n < NT / 2; ++n) {
+        float y[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = rbf(silu_f(rbf(acc[m][n][i]))) * rbf(acc[m][n + NT / 2][i]);
+        bf16_t* dst = out + (long)row * ldo + (long)t * (BN / 2) + 16 * n + 4 * g;
+        if (out_vec) {
+          uint2 pk;
+          pk.x = pack_bf2(y[0], y[1]);
+          pk.y = pack_bf2(y[2], y[3]);
+          *reinterpret_cast<uint2*>(dst) = pk;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dst[i] = f2bf(y[i]);
+        }
+      }
+    } else if (split) {
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const long col = wrow(16 * n + 4 * g);
+        float* dst = part + (long)s * M * part_ld + (long)row * part_ld + col;
+        if (part_vec && col + 3 < n_rows) {
+          *reinterpret_cast<floatx4*>(dst) = acc[m][n];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (col + i < n_rows) dst[i] = acc[m][n][i];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const long col = (long)t * BN + 16 * n + 4 * g;
+        bf16_t* dst = out + (long)row * ldo + col;
+        if (out_vec && col + 3 < n_rows) {
+          uint2 pk;
+          pk.x = pack_bf2(acc[m][n][0], acc[m][n][1]);
+          pk.y = pack_bf2(acc[m][n][2], acc[m][n][3]);
+          *reinterpret_cast<uint2*>(dst) = pk;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (col + i < n_rows) dst[i] = f2bf(acc[m][n][i]);
+        }
+      }
+    }
+  }
+}
+
 // K-step rotation multiplier: -1 = policy (5 for unsplit-K grids -- the long-K gate_up
 // + SwiGLU and LM-head shapes, 4-8 % faster on MI355X; off for split-K grids, where it
 // measured neutral to 30 % slower: benchmarks/ws_rot_probe.py), >= 0 forces it
@@ -448,14 +646,32 @@ void launch_ws(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks,
   kern<<<n_tiles * S, 256, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows, rot_mul);
 }
 
+template <int MT, int BN, bool SWIGLU>
+void launch_ws_lw(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks, int S, int n_tiles, int I,
+                  bf16_t* out, long ldo, float* part, long part_ld, long n_rows, hipStream_t st) {
+  constexpr size_t lds = (size_t)lw_nsx(MT) * 16 * MT * 128 + (size_t)lw_nsw(MT, BN) * BN * 128;
+  auto kern = wsgemm_lw_kernel<MT, BN, SWIGLU>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    attr = true;
+  }
+  const int rot_mul = g_ws_rot_mul >= 0 ? g_ws_rot_mul : (S == 1 ? 5 : 0);
+  kern<<<n_tiles * S, 384, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows, rot_mul);
+}
+
 template <bool SWIGLU>
 int dispatch_ws(int MT, int BN, const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks, int S,
                 int n_tiles, int I, bf16_t* out, long ldo, float* part, long part_ld, hipStream_t st,
-                long n_rows = 1L << 40) {
-#define LK_WS(mt, bn)                                                                                   \
-  if (MT == mt && BN == bn) {                                                                           \
-    launch_ws<mt, bn, SWIGLU>(x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, part, part_ld, n_rows, st); \
-    return 0;                                                                                           \
+                long n_rows = 1L << 40, int variant = 0) {
+#define LK_WS(mt, bn)                                                                                      \
+  if (MT == mt && BN == bn) {                                                                              \
+    if (variant == 1)                                                                                      \
+      launch_ws_lw<mt, bn, SWIGLU>(x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, part, part_ld, n_rows, st); \
+    else                                                                                                   \
+      launch_ws<mt, bn, SWIGLU>(x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, part, part_ld, n_rows, st);    \
+    return 0;                                                                                              \
   }
   LK_WS(4, 64) LK_WS(4, 128) LK_WS(8, 64) LK_WS(8, 128) LK_WS(12, 64) LK_WS(12, 128) LK_WS(16, 64) LK_WS(16, 128)
 #undef LK_WS
@@ -525,6 +741,32 @@ void lk_wsgemm_plan(int M, int N, int K, int swiglu, int* bn_out, int* s_out) {
   }
 }
 
+// per-shape kernel variant of the weight-streaming GEMM: 0 = one LDS ring (wsgemm_kernel),
+// 1 = loader waves (wsgemm_lw_kernel); keyed by (row tile MT, N, K, swiglu), set by the decode
+// tuner's measurement (ops.tune_decode), default LK_WS_LOADER (0)
+static std::mutex g_ws_var_mu;
+static std::map<long, int> g_ws_var;
+static long ws_var_key(int MT, int N, int K, int swiglu) {
+  return (((long)MT * 1000003L + N) * 1000003L + K) * 2 + (swiglu ? 1 : 0);
+}
+static int ws_variant(int M, int N, int K, int swiglu) {
+  static const int dflt = [] {
+    const char* e = getenv("LK_WS_LOADER");
+    return e ? (atoi(e) != 0) : 0;
+  }();
+  std::lock_guard<std::mutex> lock(g_ws_var_mu);
+  auto it = g_ws_var.find(ws_var_key(ws_mt(M), N, K, swiglu));
+  return it != g_ws_var.end() ? it->second : dflt;
+}
+int lk_wsgemm_set_variant(int M, int N, int K, int swiglu, int variant) {
+  if (variant < -1 || variant > 1) return -1;
+  std::lock_guard<std::mutex> lock(g_ws_var_mu);
+  const long key = ws_var_key(ws_mt(M), N, K, swiglu);
+  if (variant < 0) g_ws_var.erase(key);
+  else g_ws_var[key] = variant;
+  return 0;
+}
+
 int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, int swiglu,
               bf16_t* out, long ldo, float* part, hipStream_t st) {
   if (M < 1 || M > 256 || S < 1 || K % (S * 64) || (BN != 64 && BN != 128)) return -1;
@@ -536,8 +778,11 @@ int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, i
   const int MT = ws_mt(M);
   const int ks = K / S;
   float* p = S > 1 ? part : nullptr;
-  const int rc = swiglu ? dispatch_ws<true>(MT, BN, x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, p, N, st)
-                        : dispatch_ws<false>(MT, BN, x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, p, N, st);
+  const int var = ws_variant(M, N, K, swiglu);
+  const int rc = swiglu ? dispatch_ws<true>(MT, BN, x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, p, N, st,
+                                            1L << 40, var)
+                        : dispatch_ws<false>(MT, BN, x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, p, N, st,
+                                             1L << 40, var);
   if (rc) return rc;
   if (S > 1) {
     const int n_out = swiglu ? I : N;
@@ -559,7 +804,8 @@ int lk_wsgemm_part(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int
                    hipStream_t st) {
   if (M < 1 || M > 256 || S < 2 || K % (S * 64) || (BN != 64 && BN != 128) || N % BN || part == nullptr) return -1;
   const int MT = ws_mt(M);
-  const int rc = dispatch_ws<false>(MT, BN, x, ldx, w, M, K, K / S, S, N / BN, 0, nullptr, 0, part, N, st);
+  const int rc = dispatch_ws<false>(MT, BN, x, ldx, w, M, K, K / S, S, N / BN, 0, nullptr, 0, part, N, st,
+                                    1L << 40, ws_variant(M, N, K, 0));
   LK_CHECK_LAUNCH();
   return rc;
 }

@@ -147,14 +147,20 @@ class ModelRunner:
         if tp is not None and tp.enabled and not getattr(tp, "simulated", False):
             import torch.distributed as dist
 
-            box = [dict(ops._DECODE_TABLE) if lead else None]
+            box = [(dict(ops._DECODE_TABLE), dict(ops._WS_VARIANTS)) if lead else None]
             dist.broadcast_object_list(box, src=tp.ranks[0] if tp.ranks else 0, group=tp.ctrl or tp.group)
             ops._DECODE_TABLE.clear()
-            ops._DECODE_TABLE.update(box[0])
+            ops._DECODE_TABLE.update(box[0][0])
+            if not lead:
+                ops.apply_ws_variants(box[0][1])
         picks = {}
         for (m, n, k, sw), arm in sorted(ops._DECODE_TABLE.items()):
             picks.setdefault(f"N{n} K{k}{' swiglu' if sw else ''}", []).append(f"{m}:{arm}")
         log.info("decode GEMM routing (M bucket: kernel): %s", "; ".join(f"{k} {' '.join(v)}" for k, v in picks.items()))
+        if ops._WS_VARIANTS:
+            log.info("weight-streaming kernel per row tile (1 = loader waves): %s",
+                     "; ".join(f"M{m} N{n} K{k}{' swiglu' if sw else ''}: {v}"
+                               for (m, n, k, sw), v in sorted(ops._WS_VARIANTS.items())))
         return res
 
     @staticmethod

@@ -490,6 +490,22 @@ def tune_gemm(weights, max_m: int, min_m: int = 512, iters: int = 6, cold_bytes:
     return out
 
 
+# decode tuner: also pick the weight-streaming kernel variant per row tile (LK_WS_VARIANT_TUNE=0:
+# keep LK_WS_LOADER's default everywhere)
+WS_VARIANT_TUNE = os.environ.get("LK_WS_VARIANT_TUNE", "1") != "0"
+_WS_VARIANTS: dict = {}  # (row-tile top M, N, K, swiglu) -> 0 ring / 1 loader waves (also set in _C)
+
+
+def apply_ws_variants(table: dict):
+    """Install measured weight-streaming kernel variants (a TP worker applies its leader's)."""
+    _WS_VARIANTS.clear()
+    _WS_VARIANTS.update(table)
+    if table and available():
+        L = lib()
+        for (M, N, K, sw), v in table.items():
+            L.ws_set_variant(M, N, K, sw, v)
+
+
 def tune_decode(weights, ms: Sequence[int] = DECODE_TUNE_MS, iters: int = 5, cold_bytes: int = 640 << 20) -> dict:
     """For each decode-sized M bucket and each (weight, swiglu) pair, time the weight-streaming
     kernel against the prefill GEMM with the weights arriving from HBM (each launch reads the
@@ -503,6 +519,37 @@ def tune_decode(weights, ms: Sequence[int] = DECODE_TUNE_MS, iters: int = 5, col
         N, K = w.shape
         swiglu = bool(swiglu)
         copies = [w] + [w.clone() for _ in range(max(1, -(-cold_bytes // (N * K * 2)) - 1))]
+
+        def timed(fns):
+            ts = {k: [] for k in fns}
+            for fn in fns.values():  # warm-up (and first-launch attributes)
+                fn(copies[0])
+            torch.cuda.synchronize()
+            for _ in range(iters):
+                for k, fn in fns.items():
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record()
+                    for c in copies[1:] + copies[:1]:
+                        fn(c)
+                    b.record()
+                    b.synchronize()
+                    ts[k].append(a.elapsed_time(b) * 1e3 / len(copies))
+            return {k: statistics.median(v) for k, v in ts.items()}
+
+        # the weight-streaming kernel's variant per row tile (64 / 128 / 192 / 256 rows): one LDS
+        # ring vs loader waves (csrc/skinny_gemm.hip wsgemm_lw_kernel), measured at the tile's
+        # largest M, before the routing below times the ws arm with it
+        if WS_VARIANT_TUNE and _decode_static_ok(N, K, swiglu):
+            for M in [m for m in (64, 128, 192, 256) if m in ms]:
+                x = torch.randn(M, K, device=w.device, dtype=torch.bfloat16)
+                fns = {}
+                for v in (0, 1):
+                    fns[v] = (lambda c, v=v: (L.ws_set_variant(M, N, K, swiglu, v), L.ws_linear(x, c, swiglu)))
+                med = timed(fns)
+                best = min(med, key=med.get)
+                L.ws_set_variant(M, N, K, swiglu, best)
+                _WS_VARIANTS[(M, N, K, swiglu)] = best
+                out[(M, N, K, swiglu, "ws_variant")] = {("ring", "loader")[v]: round(t, 1) for v, t in med.items()}
         for M in ms:
             x = torch.randn(M, K, device=w.device, dtype=torch.bfloat16)
             arms = {}

@@ -876,3 +876,34 @@ def test_scatter_ids_and_gather_rows(hip):
     x = torch.randn(1000, 4096, device=DEV, dtype=torch.bfloat16)
     idx = torch.tensor([999, 0, 17, 17, 500], device=DEV)
     assert torch.equal(ops.gather_rows(x, idx).cpu(), x[idx].cpu())
+
+
+@pytest.mark.parametrize("M", [1, 40, 64, 100, 128, 160, 192, 230, 256])
+@pytest.mark.parametrize("NK,swiglu", [((6144, 4096), False), ((4096, 14336), False), ((28672, 4096), True),
+                                        ((1280, 8192), False)])
+def test_ws_loader_wave_variant_bit_identical(hip, M, NK, swiglu):
+    """The loader-wave weight-streaming kernel (wsgemm_lw_kernel) computes every tile with the
+    same MFMA sequence as the one-ring kernel: bit-identical output for each BN / split plan,
+    the split-K partial path and SwiGLU, and within tolerance of the fp32 product."""
+    N, K = NK
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    plans = [(None, None)] + ([(64, 1), (128, 2), (64, 4)] if not swiglu else [(128, 1), (64, 1)])
+    try:
+        for bn, S in plans:
+            if bn is not None and ((N // 2 if swiglu else N) % (bn // 2 if swiglu else bn) or K % (S * 64)):
+                continue
+            outs = []
+            for v in (0, 1):
+                hip.ws_set_variant(M, N, K, swiglu, v)
+                outs.append(hip.ws_linear(x, w, swiglu) if bn is None else hip.ws_linear(x, w, swiglu, bn, S))
+            torch.cuda.synchronize()
+            assert torch.equal(outs[0], outs[1]), (M, N, K, bn, S)
+        y = x.float() @ w.float().t()
+        if swiglu:
+            g, u = y[:, : N // 2], y[:, N // 2:]
+            y = torch.nn.functional.silu(g) * u
+        _close(outs[1], y, 0.03, 0.02, f"lw M{M} N{N} K{K}")
+    finally:
+        hip.ws_set_variant(M, N, K, swiglu, -1)
