@@ -510,7 +510,8 @@ def tune_decode(weights, ms: Sequence[int] = DECODE_TUNE_MS, iters: int = 5, col
     """For each decode-sized M bucket and each (weight, swiglu) pair, time the weight-streaming
     kernel against the prefill GEMM with the weights arriving from HBM (each launch reads the
     next of enough copies to overflow the 256 MB MALL, back-to-back launches as in a decode
-    graph) and record the faster in the dispatch table.  Returns {(M, N, K, swiglu): {arm: us}}."""
+    graph) and record the faster in the dispatch table.  Returns {(M, N, K, swiglu): {arm: us}}
+    plus, per measured row tile, {(M, N, K, swiglu, "ws_variant"): {"ring" / "loader": us}}."""
     import statistics
 
     L = lib()
@@ -554,27 +555,14 @@ def tune_decode(weights, ms: Sequence[int] = DECODE_TUNE_MS, iters: int = 5, col
             x = torch.randn(M, K, device=w.device, dtype=torch.bfloat16)
             arms = {}
             if M <= 256 and _decode_static_ok(N, K, swiglu):
-                arms["ws"] = lambda x, w: L.ws_linear(x, w, swiglu)
+                arms["ws"] = lambda c, x=x: L.ws_linear(x, c, swiglu)
             epi = 1 if swiglu else 0
             cfg = _gemm_default(M, N, K, epi)
             if cfg is not None and L.gemm_supported(M, N, K, epi, cfg[1], cfg[2]):
-                arms["gemm"] = lambda x, w, cfg=cfg: L.gemm(x, w, None, epi, cfg[1], None, cfg[0], cfg[2])
+                arms["gemm"] = lambda c, x=x, cfg=cfg: L.gemm(x, c, None, epi, cfg[1], None, cfg[0], cfg[2])
             if len(arms) < 2:
                 continue
-            ts = {k: [] for k in arms}
-            for k, fn in arms.items():  # warm-up (and first-launch attributes)
-                fn(x, copies[0])
-            torch.cuda.synchronize()
-            for it in range(iters):
-                for k, fn in arms.items():
-                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    a.record()
-                    for c in copies[1:] + copies[:1]:
-                        fn(x, c)
-                    b.record()
-                    b.synchronize()
-                    ts[k].append(a.elapsed_time(b) * 1e3 / len(copies))
-            med = {k: statistics.median(v) for k, v in ts.items()}
+            med = timed(arms)
             _DECODE_TABLE[(M, N, K, swiglu)] = min(med, key=med.get)
             out[(M, N, K, swiglu)] = {k: round(v, 1) for k, v in med.items()}
         del copies

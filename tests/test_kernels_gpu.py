@@ -743,14 +743,25 @@ def test_tune_decode_routes_by_measurement(hip):
     w = torch.randn(7168, 8192, device=DEV, dtype=torch.bfloat16) * 0.02  # 70B TP=8 gate_up shard
     o = torch.randn(8192, 1024, device=DEV, dtype=torch.bfloat16) * 0.02   # 70B TP=8 o shard
     saved = dict(ops._DECODE_TABLE)
+    saved_var = dict(ops._WS_VARIANTS)
+    shapes = ((7168, 8192, True), (8192, 1024, False))
+    variants = {}
     try:
         ops._DECODE_TABLE.clear()
         res = ops.tune_decode([(w, True), (o, False)], ms=(64, 192, 256), iters=3, cold_bytes=256 << 20)
-        assert set(res) == {(m, n, k, sw) for m in (64, 192, 256) for (n, k, sw) in ((7168, 8192, True), (8192, 1024, False))}
-        for (m, n, k, sw), arms in res.items():
+        routes = {key: v for key, v in res.items() if len(key) == 4}
+        variants = {key[:4]: v for key, v in res.items() if len(key) == 5}
+        assert set(routes) == {(m, n, k, sw) for m in (64, 192, 256) for (n, k, sw) in shapes}
+        # the weight-streaming kernel variant (one ring / loader waves) is measured per row tile too
+        assert set(variants) == set(routes) and all(key[4] == "ws_variant" for key in res if len(key) == 5)
+        for key, arms in variants.items():
+            assert set(arms) == {"ring", "loader"}
+            # the pick is the faster arm (the reported times are rounded to 0.1 us: ties allowed)
+            assert arms[("ring", "loader")[ops._WS_VARIANTS[key]]] == min(arms.values())
+        for (m, n, k, sw), arms in routes.items():
             assert set(arms) == {"ws", "gemm"} and all(v > 0 for v in arms.values())
             pick = ops._DECODE_TABLE[(m, n, k, sw)]
-            assert pick == min(arms, key=arms.get)
+            assert arms[pick] == min(arms.values())
             x = torch.randn(m - 7, k, device=DEV, dtype=torch.bfloat16)  # same bucket
             kind = ops._decode_gemm_kind(x, w if sw else o, sw)
             assert kind == ("ws" if pick == "ws" else None)
@@ -761,6 +772,9 @@ def test_tune_decode_routes_by_measurement(hip):
     finally:
         ops._DECODE_TABLE.clear()
         ops._DECODE_TABLE.update(saved)
+        for (m, n, k, sw) in variants:
+            hip.ws_set_variant(m, n, k, sw, -1)
+        ops.apply_ws_variants(saved_var)
 
 
 # ---------------------------------------------------------------- fused prefill chain epilogues
