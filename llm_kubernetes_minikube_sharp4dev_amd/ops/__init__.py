@@ -338,8 +338,10 @@ def _decode_gemm_kind(x, w, swiglu: bool) -> Optional[str]:
 # ``LIBRARY_FALLBACKS`` so a test can assert the serving path never takes it.
 EPI = {None: 0, "swiglu": 1, "bias": 2, "gelu": 3, "relu": 4}
 # measurement knob only: LK_GEMM_LIBRARY=1 sends the prefill-regime GEMMs to hipBLASLt (+ the
-# separate activation kernels) for in-situ A/B against the hand-written kernel
-GEMM_LIBRARY = os.environ.get("LK_GEMM_LIBRARY", "0") == "1"
+# separate activation kernels) for in-situ A/B against the hand-written kernel; =2 only the plain
+# ones (no bias / activation / SwiGLU epilogue: QKV, O, down), the fused ones stay hand-written.
+# Either turns the fused prefill chain off (its epilogues exist only in gemm.hip).
+GEMM_LIBRARY = int(os.environ.get("LK_GEMM_LIBRARY", "0") or 0)
 # K-loop schedule of untuned shapes (0: 4 phases per K-tile with per-cluster priority flips,
 # 1: 2 phases, 2: 4 phases with a static priority for the lagging half of the waves).  Default:
 # 2 for the decoder's K >= 4096 projections (1-5 % faster cold on every Llama-3-8B shape at
@@ -594,7 +596,8 @@ def linear(x, w, b=None, act: Optional[str] = None):
     if act is not None and b is None:
         b = torch.zeros(w.shape[0], device=x.device, dtype=x.dtype)
         epi = EPI[act]
-    y = gemm(x, w, b, epi) if _gemm_ok(x, w) and not GEMM_LIBRARY else None
+    lib_arm = GEMM_LIBRARY == 1 or (GEMM_LIBRARY == 2 and epi == 0)
+    y = gemm(x, w, b, epi) if _gemm_ok(x, w) and not lib_arm else None
     if y is None:
         y = _library(x, w, b, act, (x.shape[0] > WS_MAX_M, w.shape[0], w.shape[1], epi))
     return y
@@ -610,7 +613,7 @@ def linear_swiglu(x, w_gate_up):
         return lib().skinny_linear(x, w_gate_up, True)
     if kind == "ws":
         return lib().ws_linear(x, w_gate_up, True)
-    y = gemm(x, w_gate_up, None, 1) if _gemm_ok(x, w_gate_up) and not GEMM_LIBRARY else None
+    y = gemm(x, w_gate_up, None, 1) if _gemm_ok(x, w_gate_up) and GEMM_LIBRARY != 1 else None
     if y is None:
         y = silu_mul(_library(x, w_gate_up, None, None, (True, w_gate_up.shape[0], w_gate_up.shape[1], 1)))
     return y
