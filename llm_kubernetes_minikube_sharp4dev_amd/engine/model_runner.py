@@ -114,6 +114,11 @@ class ModelRunner:
         # are already served from the 256 MB Infinity Cache, so the extra flash pass and
         # the unconditional merge cost more than the HBM bytes they save.
         self.cascade = self.device.type == "cuda" and os.environ.get("LK_CASCADE", "0") == "1"
+        # sampled-logits steps return the LM head's bf16 output as is on the GPU: the HIP select /
+        # select_allowed kernels read bf16 and the fused sampler converts what it needs, so no
+        # [rows, vocab] fp32 copy is written per step (LK_LOWP_LOGITS=0: fp32 logits)
+        self.logits_dtype = (None if self.device.type == "cuda" and os.environ.get("LK_LOWP_LOGITS", "1") != "0"
+                             else torch.float32)
         # buckets up to twice the sequence cap: jump-forward extend chunks add decode rows
         self.graph_sizes = sorted(b for b in graph_batch_sizes if b <= 2 * max_num_seqs)
         self.graphs: dict = {}
@@ -425,7 +430,7 @@ class ModelRunner:
                 self.model(ids, meta, self.kv_caches)  # partial prefill chunks only: KV write, no logits
                 return None
             h = self.model(ids, meta, self.kv_caches)
-            out = self.model.greedy(h) if si.greedy else self.model.logits(h)
+            out = self.model.greedy(h) if si.greedy else self.model.logits(h, dtype=self.logits_dtype)
         if si.greedy:
             self.prev_ids = out  # every TP rank holds the same greedy ids (distributed argmax)
         return out
@@ -497,7 +502,7 @@ class ModelRunner:
         with torch.cuda.stream(s):
             for _ in range(2):  # warm-up (allocator + lazy library init) outside capture
                 h = self.model(st["ids"], st["meta"], self.kv_caches)
-                self.model.greedy(h) if greedy else self.model.logits(h)
+                self.model.greedy(h) if greedy else self.model.logits(h, dtype=self.logits_dtype)
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         if self._graph_pool is None:
@@ -507,7 +512,7 @@ class ModelRunner:
         # embedding engine's own stream) may touch the device while a bucket is captured
         with torch.cuda.graph(g, pool=self._graph_pool, capture_error_mode="thread_local"):
             h = self.model(st["ids"], st["meta"], self.kv_caches)
-            st["logits"] = self.model.greedy(h) if greedy else self.model.logits(h)
+            st["logits"] = self.model.greedy(h) if greedy else self.model.logits(h, dtype=self.logits_dtype)
         st["graph"] = g
         self.graphs[(B, greedy)] = st
         return st
@@ -546,7 +551,7 @@ class ModelRunner:
             self._apply_gather(st["ids"], views[1], views[2])
         st["graph"].replay()
         if subset:
-            return st["logits"].index_select(0, views[-1])
+            return ops.gather_rows(st["logits"], views[-1])
         return st["logits"][: si.num_decode]
 
 

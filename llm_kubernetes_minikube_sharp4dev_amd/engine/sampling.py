@@ -228,7 +228,7 @@ class Sampler:
             crow = list(rows)
             flat = [rows[i] + j * V for j, i in enumerate(crow)]
             idx = torch.from_numpy(np.concatenate(flat)).to(dev, non_blocking=True)
-            mask = torch.full((len(crow), V), float("-inf"), device=dev)
+            mask = torch.full((len(crow), V), float("-inf"), device=dev, dtype=logits.dtype)
             mask.view(-1).index_fill_(0, idx, 0.0)
             sel = torch.from_numpy(np.asarray(crow, dtype=np.int64)).to(dev, non_blocking=True)
             logits.index_add_(0, sel, mask)

@@ -596,7 +596,7 @@ def linear(x, w, b=None, act: Optional[str] = None):
     if act is not None and b is None:
         b = torch.zeros(w.shape[0], device=x.device, dtype=x.dtype)
         epi = EPI[act]
-    lib_arm = GEMM_LIBRARY == 1 or (GEMM_LIBRARY == 2 and epi == 0)
+    lib_arm = GEMM_LIBRARY == 1 or (GEMM_LIBRARY == 2 and epi == 0 and x.shape[0] > WS_MAX_M)
     y = gemm(x, w, b, epi) if _gemm_ok(x, w) and not lib_arm else None
     if y is None:
         y = _library(x, w, b, act, (x.shape[0] > WS_MAX_M, w.shape[0], w.shape[1], epi))
@@ -772,7 +772,8 @@ def scatter_ids(ids, dst, prev, src):
 
 def gather_rows(x, idx):
     """x[idx] (rows), one launch on the GPU."""
-    if use_hip(x) and x.dtype == torch.bfloat16 and idx.dtype == torch.int64 and x.stride(-1) == 1:
+    if (use_hip(x) and x.dtype == torch.bfloat16 and idx.dtype == torch.int64 and x.dim() == 2
+            and x.stride(-1) == 1 and x.shape[1] % 8 == 0 and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0):
         return lib().gather_rows(x, idx.contiguous())
     return x.index_select(0, idx)
 

@@ -97,6 +97,30 @@ def test_pipelined_steps_equal_synchronous(graphs):
         assert drive(True, mk) == ref
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_bf16_logits_same_tokens_as_fp32(monkeypatch, graphs):
+    """Sampled-logits steps hand the LM head's bf16 output to the HIP select kernels (no fp32
+    copy, extend-row logits gathered by the step_ops kernel): the same tokens as fp32 logits for
+    grammar-constrained greedy rows and for temperature sampling (the conversion is exact and
+    the kernels draw from the same values)."""
+    _, m = _gpu_llama()
+
+    def proc(hist):
+        return list(range(1 + (len(hist) % 5), 512, 3))
+
+    def run(lowp, mk):
+        monkeypatch.setenv("LK_LOWP_LOGITS", "1" if lowp else "0")
+        eng = _engine(m, use_graphs=graphs)  # decode graphs captured on first use
+        assert (eng.runner.logits_dtype is None) == lowp
+        return [s.output_ids for s in eng.generate(PROMPTS, mk())]
+
+    for mk in (lambda: SamplingParams.greedy(12, logits_processor=proc),
+               lambda: SamplingParams(max_tokens=12, temperature=0.8, top_k=0, top_p=1.0, repeat_penalty=1.0,
+                                      seed=7),
+               lambda: SamplingParams(max_tokens=12, seed=7)):  # Ollama defaults: the fused sampler
+        assert run(True, mk) == run(False, mk)
+
+
 def _assert_same_or_near_tie(hf, prompts, got, ref):
     """Greedy sequences from two bf16 paths that sum attention in a different order: equal,
     or first apart at a step where the fp32 model itself rates the two tokens within the
