@@ -549,9 +549,10 @@ std::vector<at::Tensor> knn_topk(const at::Tensor& corpus, const at::Tensor& cno
   auto fo = corpus.options().dtype(at::kFloat);
   auto io = corpus.options().dtype(at::kInt);
   const int kk = (int)std::min<long>(K, std::max<long>(N, 1));
-  at::Tensor out_s = at::full({nq, (long)K}, -INFINITY, fo);
-  at::Tensor out_i = at::full({nq, (long)K}, -1, io);
-  if (N == 0 || nq == 0) return {out_s, out_i};
+  // the merge kernel writes every one of the K slots of every query (-inf / -1 pads)
+  if (N == 0 || nq == 0) return {at::full({nq, (long)K}, -INFINITY, fo), at::full({nq, (long)K}, -1, io)};
+  at::Tensor out_s = at::empty({nq, (long)K}, fo);
+  at::Tensor out_i = at::empty({nq, (long)K}, io);
   if (D % 64 == 0 && nq <= 256 && !force_fused) {
     // corpus streamed once by the LDS-DMA weight-streaming GEMM (dots in f32), then a
     // normalise + chunked top-k pass and the shared merge

@@ -178,7 +178,10 @@ class RagIndex:
         if n == 0 or not self._use_gpu():
             return PendingSearch(done=self.search_vectors(q, top_k) if n else [[] for _ in range(len(q))])
         corpus, norms = self.gpu_tensors()
-        qt = torch.as_tensor(q).to(self.device, torch.bfloat16).reshape(-1, corpus.shape[1]).contiguous()
+        qt = torch.as_tensor(q)
+        # host queries are cast on the host (a few KB) and copied once: no device cast kernel
+        qt = (qt.to(torch.bfloat16).to(self.device) if qt.device.type == "cpu"
+              else qt.to(self.device, torch.bfloat16)).reshape(-1, corpus.shape[1]).contiguous()
         if getattr(self, "_sharded", None) is not None:
             s, i = self._sharded(qt, min(k, 64))
         else:

@@ -100,6 +100,13 @@ def main(path, window_s, top=25):
     print("\n| idle gap | count | total ms |\n|---|---|---|")
     for k in ["<5us", "5-20us", "20-100us", "0.1-1ms", ">1ms"]:
         print(f"| {k} | {b[k]} | {bt[k] / 1e6:.1f} |")
+    # every kernel that is not ours (PyTorch eager ops, runtime copies): what still runs outside
+    # the HIP kernel library inside the timed steps
+    foreign = {k: v for k, v in agg.items() if "anon::" not in k and "lk_" not in k}
+    if foreign:
+        print("\n| kernel outside the HIP library | calls | total ms |\n|---|---|---|")
+        for k, (t, n) in sorted(foreign.items(), key=lambda x: -x[1][0]):
+            print(f"| `{k[:90]}` | {n} | {t / 1e6:.2f} |")
     if big:
         print(f"\nIdle gaps >= 100 us ({len(big)}, {sum(g for g, *_ in big) / 1e6:.1f} ms), largest first:\n")
         print("| gap us | at s | last kernel before | first kernel after |\n|---|---|---|---|")
