@@ -594,13 +594,20 @@ std::vector<at::Tensor> knn_merge(const at::Tensor& cand_s, const at::Tensor& ca
   return {out_s, out_i};
 }
 
-at::Tensor pool_normalize(const at::Tensor& hidden, const at::Tensor& cu, int64_t mode, bool normalize) {
+// out: optional destination rows [B, H] (f32 or bf16, unit last stride, 16-byte rows), e.g. a
+// slice of the caller's embedding matrix; default a new f32 [B, H]
+at::Tensor pool_normalize(const at::Tensor& hidden, const at::Tensor& cu, int64_t mode, bool normalize,
+                          const c10::optional<at::Tensor>& out_) {
   CHECK_CUDA(hidden); CHECK_BF16(hidden); CHECK_LASTDIM(hidden); CHECK_I32(cu); CHECK_CONTIG(cu);
   check_rows16(hidden, "hidden");
   const int B = cu.numel() - 1, H = hidden.size(1);
-  at::Tensor out = at::empty({B, H}, hidden.options().dtype(at::kFloat));
+  at::Tensor out = out_ ? *out_ : at::empty({B, H}, hidden.options().dtype(at::kFloat));
+  const bool obf = out.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(obf || out.scalar_type() == at::kFloat, "out must be f32 or bf16");
+  CHECK_CUDA(out); CHECK_LASTDIM(out); check_rows16(out, "out");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == B && out.size(1) == H, "out [B, H]");
   int rc = lk_pool_normalize(bp(hidden), hidden.stride(0), ip(cu), B, H, (int)mode, normalize ? 1 : 0,
-                             out.data_ptr<float>(), cur_stream());
+                             out.data_ptr(), out.stride(0), obf ? 1 : 0, cur_stream());
   CHECK_RC(rc, "pool_normalize");
   return out;
 }
@@ -893,7 +900,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("knn_topk", &knn_topk, "", py::arg("corpus"), py::arg("cnorm"), py::arg("queries"), py::arg("qnorm"),
         py::arg("K"), py::arg("force_fused") = false);
   m.def("knn_merge", &knn_merge);
-  m.def("pool_normalize", &pool_normalize);
+  m.def("pool_normalize", &pool_normalize, "", py::arg("hidden"), py::arg("cu"), py::arg("mode"), py::arg("normalize"),
+        py::arg("out") = py::none());
   m.def("row_norms", &row_norms);
   m.def("select_allowed", &select_allowed, "", py::arg("logits"), py::arg("plan"), py::arg("temps") = py::none(),
         py::arg("seed") = 0, py::arg("step") = 0);

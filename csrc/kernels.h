@@ -136,7 +136,7 @@ int lk_knn_merge(const float* cand_s, const int* cand_i, int nq, int ncand, int 
 
 // pooling.hip
 int lk_pool_normalize(const bf16_t* hidden, long hs, const int* cu, int B, int H, int mode,
-                      int normalize, float* out, hipStream_t st);
+                      int normalize, void* out, long os, int out_bf16, hipStream_t st);
 int lk_row_norms(const bf16_t* x, long N, int D, float* out, hipStream_t st);
 
 // sampling.hip

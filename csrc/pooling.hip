@@ -1,16 +1,19 @@
 // K5 sentence-embedding pooling fused with L2 normalisation.
 //   mode 0 = mean over the sequence's tokens (MiniLM, nomic-embed), 1 = CLS (bge)
-// hidden: [T, H] packed varlen rows (cu_seqlens [B+1]); out: [B, H] f32.
+// hidden: [T, H] packed varlen rows (cu_seqlens [B+1]); out: [B, H] rows of stride `os`, f32 or
+// bf16 (the query path hands the bf16 rows straight to the kNN kernels: no cast pass).
 // One workgroup per sequence; 16-byte loads along H, f32 accumulation.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
 namespace {
 
-template <int MAXV>
+template <int MAXV, typename OutT>
 __global__ __launch_bounds__(128) void pool_norm_kernel(const bf16_t* __restrict__ hidden, long hs,
                                                         const int* __restrict__ cu, int H, int mode,
-                                                        int normalize, float* __restrict__ out) {
+                                                        int normalize, OutT* __restrict__ out, long os) {
   __shared__ float red[2];
   const int b = blockIdx.x;
   const int beg = cu[b], end = cu[b + 1];
@@ -49,9 +52,18 @@ __global__ __launch_bounds__(128) void pool_norm_kernel(const bf16_t* __restrict
   for (int i = 0; i < MAXV; ++i) {
     const int c = threadIdx.x + i * 128;
     if (c < nvec) {
-      float4* op = reinterpret_cast<float4*>(out + (long)b * H + c * 8);
-      op[0] = make_float4(acc[i][0] * inv, acc[i][1] * inv, acc[i][2] * inv, acc[i][3] * inv);
-      op[1] = make_float4(acc[i][4] * inv, acc[i][5] * inv, acc[i][6] * inv, acc[i][7] * inv);
+      if constexpr (std::is_same<OutT, float>::value) {
+        float4* op = reinterpret_cast<float4*>(out + (long)b * os + c * 8);
+        op[0] = make_float4(acc[i][0] * inv, acc[i][1] * inv, acc[i][2] * inv, acc[i][3] * inv);
+        op[1] = make_float4(acc[i][4] * inv, acc[i][5] * inv, acc[i][6] * inv, acc[i][7] * inv);
+      } else {
+        uint4 pk;
+        pk.x = pack_bf2(acc[i][0] * inv, acc[i][1] * inv);
+        pk.y = pack_bf2(acc[i][2] * inv, acc[i][3] * inv);
+        pk.z = pack_bf2(acc[i][4] * inv, acc[i][5] * inv);
+        pk.w = pack_bf2(acc[i][6] * inv, acc[i][7] * inv);
+        *reinterpret_cast<uint4*>(out + (long)b * os + c * 8) = pk;
+      }
     }
   }
 }
@@ -75,16 +87,23 @@ __global__ __launch_bounds__(256) void row_norm_kernel(const bf16_t* __restrict_
 
 }  // namespace
 
-int lk_pool_normalize(const bf16_t* hidden, long hs, const int* cu, int B, int H, int mode,
-                      int normalize, float* out, hipStream_t st) {
-  if (B <= 0) return 0;
-  if (H % 8) return -1;
+template <typename OutT>
+static int launch_pool(const bf16_t* hidden, long hs, const int* cu, int B, int H, int mode, int normalize,
+                       OutT* out, long os, hipStream_t st) {
   const int nvec = H / 8;
-  if (nvec <= 128) pool_norm_kernel<1><<<B, 128, 0, st>>>(hidden, hs, cu, H, mode, normalize, out);
-  else if (nvec <= 256) pool_norm_kernel<2><<<B, 128, 0, st>>>(hidden, hs, cu, H, mode, normalize, out);
-  else if (nvec <= 512) pool_norm_kernel<4><<<B, 128, 0, st>>>(hidden, hs, cu, H, mode, normalize, out);
+  if (nvec <= 128) pool_norm_kernel<1, OutT><<<B, 128, 0, st>>>(hidden, hs, cu, H, mode, normalize, out, os);
+  else if (nvec <= 256) pool_norm_kernel<2, OutT><<<B, 128, 0, st>>>(hidden, hs, cu, H, mode, normalize, out, os);
+  else if (nvec <= 512) pool_norm_kernel<4, OutT><<<B, 128, 0, st>>>(hidden, hs, cu, H, mode, normalize, out, os);
   else return -2;
   return 0;
+}
+
+int lk_pool_normalize(const bf16_t* hidden, long hs, const int* cu, int B, int H, int mode,
+                      int normalize, void* out, long os, int out_bf16, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (H % 8 || os < H || os % 8) return -1;
+  return out_bf16 ? launch_pool(hidden, hs, cu, B, H, mode, normalize, reinterpret_cast<bf16_t*>(out), os, st)
+                  : launch_pool(hidden, hs, cu, B, H, mode, normalize, reinterpret_cast<float*>(out), os, st);
 }
 
 int lk_row_norms(const bf16_t* x, long N, int D, float* out, hipStream_t st) {

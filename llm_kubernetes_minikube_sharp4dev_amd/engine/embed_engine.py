@@ -81,10 +81,14 @@ class EmbeddingEngine:
             cu = (starts[i:j + 1] - a).astype(np.int32)
             st = streams[k % len(streams)] if streams else None
             with torch.cuda.stream(st) if st is not None else _nullctx():
+                dst = out[row0 + i:row0 + j]
+                # on the GPU the pooling kernel writes the rows of ``out`` (f32 or bf16) itself
                 emb = self.model(torch.from_numpy(flat[a:b]).to(d, non_blocking=True),
                                  torch.from_numpy(cu).to(d, non_blocking=True),
-                                 torch.from_numpy(pos).to(d, non_blocking=True), ln.tolist())
-                out[row0 + i:row0 + j] = emb
+                                 torch.from_numpy(pos).to(d, non_blocking=True), ln.tolist(),
+                                 out=dst if d.type == "cuda" else None)
+                if emb.data_ptr() != dst.data_ptr():
+                    dst.copy_(emb)
             i, k = j, k + 1
 
     @torch.inference_mode()
@@ -96,11 +100,14 @@ class EmbeddingEngine:
         return out
 
     @torch.inference_mode()
-    def _embed_texts(self, texts: list[str], group: int = 4096, bulk: bool = False) -> torch.Tensor:
+    def _embed_texts(self, texts: list[str], group: int = 4096, bulk: bool = False,
+                     dtype=torch.float32) -> torch.Tensor:
         """Tokenise group by group: group g+1 is tokenised on the CPU (native encoder,
         GIL released) while the device runs group g's encoder batches.  ``bulk`` (index
-        builds): the micro-batches alternate over BUILD_STREAMS streams, joined at the end."""
-        out = torch.empty((len(texts), self.dim), dtype=torch.float32, device=self.device)
+        builds): the micro-batches alternate over BUILD_STREAMS streams, joined at the end.
+        ``dtype``: of the returned rows (bf16: the kNN query operand, written by the pooling
+        kernel)."""
+        out = torch.empty((len(texts), self.dim), dtype=dtype, device=self.device)
         streams = None
         if bulk and self.device.type == "cuda" and BUILD_STREAMS > 1 and len(texts) > group:
             if getattr(self, "_build_streams", None) is None:
@@ -147,9 +154,10 @@ class EmbeddingEngine:
         M.EMBED_LAT.observe(time.perf_counter() - t0)
         return host
 
-    def embed(self, texts: list[str]) -> torch.Tensor:
+    def embed(self, texts: list[str], dtype=torch.float32) -> torch.Tensor:
         t0 = time.perf_counter()
         with self.lock:
-            r = self._embed_texts(list(texts), bulk=True) if texts else torch.zeros((0, self.dim))
+            r = (self._embed_texts(list(texts), bulk=True, dtype=dtype) if texts
+                 else torch.zeros((0, self.dim), dtype=dtype))
         M.EMBED_LAT.observe(time.perf_counter() - t0)
         return r

@@ -80,8 +80,9 @@ class EncoderModel(nn.Module):
         return self
 
     def forward(self, ids: torch.Tensor, cu: torch.Tensor, positions: torch.Tensor,
-                lens_cpu: list, type_ids=None, pool: bool = True):
-        """ids/positions [T] int32 packed; cu [B+1] int32 -> [B, H] f32 embeddings."""
+                lens_cpu: list, type_ids=None, pool: bool = True, out=None):
+        """ids/positions [T] int32 packed; cu [B+1] int32 -> [B, H] f32 embeddings (``out``: the
+        pooling kernel writes these rows instead, f32 or bf16)."""
         cfg, nh, D, H = self.cfg, self.nh, self.D, self.cfg.hidden
         h = ops.embed_layernorm(ids, None if cfg.rotary else positions, type_ids, self.tok, self.pos,
                                 self.typ, self.emb_ln_w, self.emb_ln_b, cfg.norm_eps)
@@ -101,7 +102,7 @@ class EncoderModel(nn.Module):
             h = ops.layernorm(d, L.ln2_w, L.ln2_b, cfg.norm_eps, residual=h)
         if not pool:
             return h
-        return ops.pool_normalize(h, cu, 1 if cfg.pooling == "cls" else 0, cfg.normalize)
+        return ops.pool_normalize(h, cu, 1 if cfg.pooling == "cls" else 0, cfg.normalize, out=out)
 
     @torch.no_grad()
     def load_hf_state_dict(self, sd: dict):

@@ -229,10 +229,16 @@ def knn_merge(cand_s, cand_i, K: int):
     return out_s, out_i
 
 
-def pool_normalize(hidden, cu, mode: int, normalize: bool = True):
+def pool_normalize(hidden, cu, mode: int, normalize: bool = True, out=None):
+    """Pooled (mean / CLS), L2-normalised sentence vectors; ``out``: destination rows [B, H]
+    (f32 or bf16; the kernel writes them directly), default a new f32 [B, H]."""
     if use_hip(hidden):
-        return lib().pool_normalize(hidden, cu, mode, normalize)
-    return ref.pool_normalize(hidden, cu, mode, normalize)
+        return lib().pool_normalize(hidden, cu, mode, normalize, out)
+    y = ref.pool_normalize(hidden, cu, mode, normalize)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
 
 
 def row_norms(x):

@@ -19,6 +19,7 @@ import re
 from typing import Optional, Sequence
 
 import numpy as np
+import torch
 
 
 class EmbeddingError(RuntimeError):
@@ -118,7 +119,10 @@ class LocalEmbedder:
         return self.engine.embed(list(texts)).float().cpu().numpy()
 
     def embed_tensor(self, texts: Sequence[str]):
-        return self.engine.embed(list(texts))
+        """Device query vectors for the kNN kernels: bf16 rows written by the pooling kernel on
+        the GPU (the corpus operand's dtype), f32 on the CPU."""
+        dt = torch.bfloat16 if self.engine.device.type == "cuda" else torch.float32
+        return self.engine.embed(list(texts), dtype=dt)
 
 
 _TOKEN = re.compile(r"\w+", re.UNICODE)

@@ -283,7 +283,17 @@ def test_pool_normalize(hip):
     x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
     cu = torch.tensor([0, 3, 4, 44], dtype=torch.int32, device=DEV)
     for mode in (0, 1):
-        _close(hip.pool_normalize(x, cu, mode, True), ref.pool_normalize(x, cu.cpu(), mode, True), 1e-3, 0.0)
+        want = ref.pool_normalize(x, cu.cpu(), mode, True)
+        _close(hip.pool_normalize(x, cu, mode, True), want, 1e-3, 0.0)
+        # destination rows: a strided slice of a bigger f32 / bf16 matrix, written in place and
+        # nothing else touched (the embed engine's rows, the bf16 kNN query operand)
+        for dt in (torch.float32, torch.bfloat16):
+            big = torch.full((6, H + 64), 7.0, device=DEV, dtype=dt)
+            dst = big[2:5, :H]
+            got = hip.pool_normalize(x, cu, mode, True, dst)
+            assert got.data_ptr() == dst.data_ptr()
+            _close(dst.float(), want, 1e-3 if dt == torch.float32 else 8e-3, 0.0)
+            assert bool((big[:2] == 7).all()) and bool((big[5:] == 7).all()) and bool((big[:, H:] == 7).all())
 
 
 def test_select_tokens(hip):
