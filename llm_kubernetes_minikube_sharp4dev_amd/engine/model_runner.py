@@ -130,16 +130,37 @@ class ModelRunner:
         self._stager = (_PinnedStager(self.device) if self.device.type == "cuda"
                         and os.environ.get("LK_PINNED_STAGE", "1") != "0" else None)
         self.gemm_tuning = {}
-        if self.device.type == "cuda" and os.environ.get("LK_GEMM_TUNE", "0") == "1" and hasattr(model, "gemm_shapes"):
-            # opt-in: pick the prefill GEMM's column tile / K-loop schedule per M bucket by
-            # micro-benchmark (~2 s).  Off by default: in the serving A/B the static choice of
-            # ops._gemm_default was as fast or faster (profiles/r2_gemm.md)
-            self.gemm_tuning = ops.tune_gemm(model.gemm_shapes(), int(os.environ.get("LK_GEMM_TUNE_MAX_M", "4096")))
+        if self.device.type == "cuda" and hasattr(model, "gemm_shapes") and self._gemm_tune_on(model):
+            # opt-in (LK_GEMM_TUNE=1): pick the prefill GEMM's column tile / K-loop schedule per
+            # 256-row M bucket by a cold-weight micro-benchmark at load (< 1 s for Llama-3-8B).
+            # Off by default: in situ it is within the run-to-run spread of the static policy
+            # (round 2, profiles/r2_gemm.md; round 4, profiles/r4_gemm_tune/: -1.1 .. +2.7 % per pair)
+            self.gemm_tuning = self._tune_gemm(model)
             log.info("prefill GEMM tuned for %d (M bucket, N, K, epilogue) shapes", len(self.gemm_tuning))
         self.decode_tuning = {}
         if (self.device.type == "cuda" and os.environ.get("LK_DECODE_TUNE", "1") == "1"
                 and hasattr(model, "decode_gemm_shapes")):
             self.decode_tuning = self._tune_decode(model)
+
+    @staticmethod
+    def _gemm_tune_on(model) -> bool:
+        return os.environ.get("LK_GEMM_TUNE", "0") == "1"
+
+    @staticmethod
+    def _tune_gemm(model) -> dict:
+        """ops.tune_gemm over the model's projections; under TP the leader's table is used by
+        every rank (the ranks of a group run the same kernels)."""
+        tp = getattr(model, "tp", None)
+        lead = tp is None or not tp.enabled or getattr(tp, "simulated", False) or tp.rank == 0
+        res = ops.tune_gemm(model.gemm_shapes(), int(os.environ.get("LK_GEMM_TUNE_MAX_M", "4096"))) if lead else {}
+        if tp is not None and tp.enabled and not getattr(tp, "simulated", False):
+            import torch.distributed as dist
+
+            box = [dict(ops._GEMM_TABLE) if lead else None]
+            dist.broadcast_object_list(box, src=tp.ranks[0] if tp.ranks else 0, group=tp.ctrl or tp.group)
+            ops._GEMM_TABLE.clear()
+            ops._GEMM_TABLE.update(box[0])
+        return res
 
     @staticmethod
     def _tune_decode(model) -> dict:
