@@ -24,6 +24,12 @@ inline bf16_t* bpo(const c10::optional<at::Tensor>& t) { return t ? bp(*t) : nul
 inline const int* ip(const at::Tensor& t) { return t.data_ptr<int>(); }
 inline const int* ipo(const c10::optional<at::Tensor>& t) { return t ? ip(*t) : nullptr; }
 
+// shape support of the prefill GEMM for a schedule variant (3: gemm1w.hip, 256-wide tiles)
+bool gemm_shape_ok(int M, int N, int K, int epi, int bn, int splits, int variant) {
+  if (variant == 3) return bn == 256 && lk_gemm1w_supported(M, N, K, epi, splits) != 0;
+  return lk_gemm_supported(M, N, K, epi, bn, splits) != 0;
+}
+
 // 16-byte alignment of every row start (vector loads)
 void check_rows16(const at::Tensor& t, const char* name) {
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
@@ -240,7 +246,7 @@ at::Tensor gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "x [M,K], w [N,K]");
   check_rows16(x, "x"); check_rows16(w, "w");
   const int M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(lk_gemm_supported(M, N, K, (int)epi, (int)bn, (int)splits), "gemm: unsupported shape M", M, " N", N,
+  TORCH_CHECK(gemm_shape_ok(M, N, K, (int)epi, (int)bn, (int)splits, (int)variant), "gemm: unsupported shape M", M, " N", N,
               " K", K, " epi", epi, " bn", bn, " splits", splits);
   if (epi >= 2) {
     TORCH_CHECK(bias.has_value(), "gemm: this epilogue needs a bias");
@@ -276,7 +282,7 @@ at::Tensor gemm_fused(const at::Tensor& x, const at::Tensor& w, int64_t epi, int
   check_rows16(x, "x"); check_rows16(w, "w");
   const int M = x.size(0), K = x.size(1), N = w.size(0);
   TORCH_CHECK(epi == 0 || epi == 1 || epi == 6 || epi == 7, "gemm_fused: epi must be NONE / SWIGLU / RESID / QKV");
-  TORCH_CHECK(lk_gemm_supported(M, N, K, (int)epi, (int)bn, (int)splits), "gemm_fused: unsupported shape M", M, " N", N,
+  TORCH_CHECK(gemm_shape_ok(M, N, K, (int)epi, (int)bn, (int)splits, (int)variant), "gemm_fused: unsupported shape M", M, " N", N,
               " K", K, " epi", epi, " bn", bn, " splits", splits);
   LkEpi ea;
   const int H = K;
@@ -369,8 +375,8 @@ at::Tensor gather_rows(const at::Tensor& x, const at::Tensor& idx) {
 
 int64_t gemm_streamk(int64_t mode) { return lk_gemm_streamk((int)mode); }
 
-bool gemm_supported(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bn, int64_t splits) {
-  return lk_gemm_supported((int)M, (int)N, (int)K, (int)epi, (int)bn, (int)splits) != 0;
+bool gemm_supported(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bn, int64_t splits, int64_t variant) {
+  return gemm_shape_ok((int)M, (int)N, (int)K, (int)epi, (int)bn, (int)splits, (int)variant);
 }
 
 std::vector<int64_t> ws_plan(int64_t M, int64_t N, int64_t K, bool swiglu) {
@@ -876,7 +882,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "stream-K policy of the prefill GEMM (mode 0 off / 1 on / -1 keep); returns the waits that gave up since the last call",
         py::arg("mode") = -1);
   m.def("gemm_supported", &gemm_supported, "", py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bn"),
-        py::arg("splits") = 1);
+        py::arg("splits") = 1, py::arg("variant") = -1);
   m.def("silu_mul", &silu_mul, "", py::arg("x"), py::arg("out") = py::none());
   m.def("activation_", &activation_);
   m.def("rope_kv_", &rope_kv_);

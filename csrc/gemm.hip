@@ -719,6 +719,10 @@ __device__ __forceinline__ void gemm8_body(const bf16_t* __restrict__ X, long ld
       }
     }
   }
+  // the scale / RESID epilogues read LDS (scl, red) after the K loop; a persistent or stream-K
+  // workgroup goes on to its next tile, whose first LDS-DMA would overwrite them under a slower
+  // wave still reading: every wave is done with them before any wave leaves the tile
+  if constexpr (has_scale || EPI == EPI_RESID) __syncthreads();
 }
 
 // split-K reduction: out[r, c..c+3] = epi(sum_z part[z, r, c..c+3] (+ bias)), rounded like the
@@ -1060,9 +1064,15 @@ int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks) {
 // 8-B aligned output rows; any M >= 1.
 int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
             int variant, bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, const LkEpi* ea_) {
+  if (variant == 3) {  // the one-wave-per-SIMD kernel (csrc/gemm1w.hip): 256-wide tiles only
+    if (bn != 256) return -1;
+    return lk_gemm1w(x, ldx, w, bias, M, N, K, epi, out, ldo, st, ks, ws, ea_, 0);
+  }
   LkEpi ea = ea_ ? *ea_ : LkEpi{};
   // fused-chain epilogue arguments (checked here: a bad pointer / shape would fault the device)
   if (ea.ss_in && (ea.ss_nt < 1 || ea.ss_nt > 32 || ea.ss_ld < M || ea.inv_h <= 0.f)) return -1;
+  // the split-K partial / reduce kernels carry no row scale: refuse instead of dropping it
+  if (ea.ss_in && ks > 1) return -1;
   if (epi == EPI_RESID && (!ea.resid || !ea.ss_out || ea.ldr % 8 || ea.ss_out_ld < M)) return -1;
   if (epi == EPI_QKV && (!ea.pos || !ea.cos_sin || ea.hd % 16 || ea.hd <= 0 ||
                          N != (ea.hq + 2 * ea.hkv) * ea.hd || ((ea.kc || ea.vc) && (!ea.slots || ea.bs < 1))))

@@ -91,9 +91,17 @@ struct LkEpi {
   bf16_t* vc = nullptr;
   int bs = 0, hq = 0, hkv = 0, hd = 0;
 };
+// variant: K-loop schedule of gemm.hip (0 / 1 / 2), or 3 = gemm1w.hip (bn 256)
 int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
             int variant, bf16_t* out, long ldo, hipStream_t st, int ks = 1, float* ws = nullptr,
             const LkEpi* ea = nullptr);
+
+// gemm1w.hip: the one-wave-per-SIMD 256 x 256 prefill GEMM (hipBLASLt's gfx950 K-loop schedule,
+// every lk_gemm epilogue); lk_gemm routes variant 3 here.  Needs K % 64 == 0 and >= 3 K-tiles per
+// split, N % 256 == 0 (SwiGLU: N/2 % 128).  group_m <= 0: LK_GEMM_GROUP_M (4).
+int lk_gemm1w_supported(int M, int N, int K, int epi, int ks);
+int lk_gemm1w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi,
+              bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, const LkEpi* ea, int group_m);
 
 // rope_kv.hip
 int lk_rope_kv(bf16_t* qkv, long qs, const int* positions, const float* cos_sin, long T, int Hq,

@@ -419,7 +419,8 @@ def test_ws_swiglu(hip, M, IK):
     _close(hip.ws_linear(x, w, True, 64, 2), a_ref, 0.03, 0.01, "ws swiglu bn64 S2")
 
 
-GEMM_CFGS = [(0, 256), (1, 256), (2, 256), (0, 192), (1, 192), (2, 192)]
+# (schedule, column tile): gemm.hip schedules 0-2, and variant 3 = csrc/gemm1w.hip (256-wide only)
+GEMM_CFGS = [(0, 256), (1, 256), (2, 256), (0, 192), (1, 192), (2, 192), (3, 256)]
 
 
 @pytest.mark.parametrize("M", [1, 257, 1000, 3584])
@@ -434,7 +435,7 @@ def test_gemm(hip, M, NK):
     y_ref = x.float() @ w.float().t()
     ran = 0
     for sched, bn in GEMM_CFGS:
-        if hip.gemm_supported(M, N, K, 0, bn):
+        if hip.gemm_supported(M, N, K, 0, bn, 1, sched):
             _close(hip.gemm(x, w, None, 0, bn, None, sched), y_ref, 0.02, 0.01, f"gemm s{sched}/{bn} M{M} N{N} K{K}")
             ran += 1
     assert ran >= 2
@@ -458,9 +459,9 @@ def test_gemm_splitk(hip, MNK, splits, epi):
         y = torch.nn.functional.gelu(y)
     elif epi == 4:
         y = torch.relu(y)
-    for sched in (0, 1):
+    for sched in (0, 1, 3):
         for bn in (256, 192):
-            if hip.gemm_supported(M, N, K, epi, bn, splits):
+            if hip.gemm_supported(M, N, K, epi, bn, splits, sched):
                 _close(hip.gemm(x, w, b, epi, bn, None, sched, splits), y, 0.03, 0.01,
                        f"gemm split{splits} epi{epi} s{sched}/{bn} M{M} N{N} K{K}")
 
@@ -540,7 +541,7 @@ def test_gemm_asymmetric_layout(hip):
     M = N = K = 256
     x = torch.eye(M, K, device=DEV, dtype=torch.bfloat16)
     w = (torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K) % 97 - 48).to(torch.bfloat16)
-    for sched, bn in [(0, 256), (1, 256)]:
+    for sched, bn in [(0, 256), (1, 256), (3, 256)]:
         y = hip.gemm(x, w, None, 0, bn, None, sched)
         assert torch.equal(y.float().cpu(), w.float().t().cpu()), f"s{sched}/{bn}"
 
@@ -553,7 +554,7 @@ def test_gemm_swiglu_matches_unfused(hip, M, IK):
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(2 * I, K, device=DEV, dtype=torch.bfloat16) * 0.05
     a_ref = ref.silu_mul((x.float() @ w.float().t()).to(torch.bfloat16))
-    for sched in (0, 1):
+    for sched in (0, 1, 3):
         _close(hip.gemm(x, w, None, 1, 256, None, sched), a_ref, 0.03, 0.01, f"gemm s{sched} swiglu M{M} I{I}")
 
 
@@ -573,7 +574,7 @@ def test_gemm_bias_epilogues(hip, M, NK, epi):
     elif epi == 4:
         y = torch.relu(y)
     for sched, bn in GEMM_CFGS:
-        if hip.gemm_supported(M, N, K, epi, bn):
+        if hip.gemm_supported(M, N, K, epi, bn, 1, sched):
             _close(hip.gemm(x, w, b, epi, bn, None, sched), y, 0.03, 0.01, f"gemm epi{epi} s{sched}/{bn} M{M} N{N}")
 
 
@@ -802,7 +803,8 @@ def _qkv_setup(M, Hq=32, Hkv=8, D=128, H=4096, nb=600, bs=16, seed=0):
 
 @pytest.mark.parametrize("M,N,K,splits", [(300, 1024, 512, 1), (1000, 4096, 1024, 1), (2304, 4096, 14336, 3),
                                           (777, 2048, 4096, 2), (4352, 4096, 4096, 1)])
-def test_gemm_resid_epilogue(hip, M, N, K, splits):
+@pytest.mark.parametrize("variant", [2, 3])
+def test_gemm_resid_epilogue(hip, M, N, K, splits, variant):
     """RESID (producer side of the folded norm): r = bf16(r + bf16(x W^T)) in place and the
     per-256-column partial sums of squares of the new r, in-kernel and through the split-K
     reduce, M tails; 4352 x 4096 engages stream-K (17 x 16 tiles)."""
@@ -814,43 +816,46 @@ def test_gemm_resid_epilogue(hip, M, N, K, splits):
     ref.linear_resid(x, w, r_ref, ss_ref)
     ss = torch.full((N // 256, M), float("nan"), device=DEV)
     n0 = hip.gemm_streamk(-2)
-    hip.gemm_fused(x, w, 6, 256, None, 2, splits, resid=r, ss_out=ss)
+    hip.gemm_fused(x, w, 6, 256, None, variant, splits, resid=r, ss_out=ss)
     torch.cuda.synchronize()
-    _close(r, r_ref, 0.02, 0.01, f"resid M{M} N{N} K{K} s{splits}")
+    _close(r, r_ref, 0.02, 0.01, f"resid M{M} N{N} K{K} s{splits} v{variant}")
     _close(ss, ss_ref, 0.5, 0.01, f"ss partials M{M} N{N}")
     assert hip.gemm_streamk(-1) == 0
-    if M == 4352:
+    if M == 4352 and variant == 2:
         assert hip.gemm_streamk(-2) > n0, "stream-K did not engage"
 
 
 @pytest.mark.parametrize("M", [300, 2048, 4352])
 @pytest.mark.parametrize("scaled", [False, True])
-def test_gemm_swiglu_row_scale(hip, M, scaled):
-    """SwiGLU epilogue with the folded post-norm's row scale s = rsqrt(sum(ss) / H + eps)."""
+@pytest.mark.parametrize("variant,H", [(2, 4096), (3, 4096), (3, 8192)])
+def test_gemm_swiglu_row_scale(hip, M, scaled, variant, H):
+    """SwiGLU epilogue with the folded post-norm's row scale s = rsqrt(sum(ss) / H + eps) (H 8192:
+    32 partial planes, the 70B width)."""
     torch.manual_seed(M)
-    H, I = 4096, 1792
+    I = 1792
     r = torch.randn(M, H, device=DEV, dtype=torch.bfloat16) * 3
     w = torch.randn(2 * I, H, device=DEV, dtype=torch.bfloat16) * 0.02
     ss = ref.ss_partials(r) if scaled else None
-    y = hip.gemm_fused(r, w, 1, 256, None, 2, 1, ss_in=ss, eps=1e-5)
+    y = hip.gemm_fused(r, w, 1, 256, None, variant, 1, ss_in=ss, eps=1e-5)
     y_ref = ref.gemm_scaled(r, w, ss, H, 1e-5, swiglu=True)
-    _close(y, y_ref, 0.03, 0.02, f"swiglu scaled={scaled} M{M}")
+    _close(y, y_ref, 0.03, 0.02, f"swiglu scaled={scaled} M{M} v{variant} H{H}")
 
 
-@pytest.mark.parametrize("M,bn", [(300, 192), (1111, 256), (4352, 192), (2560, 256)])
+@pytest.mark.parametrize("M,bn,variant", [(300, 192, 2), (1111, 256, 2), (4352, 192, 2), (2560, 256, 2),
+                                          (300, 256, 3), (1111, 256, 3), (4352, 256, 3)])
 @pytest.mark.parametrize("scaled", [False, True])
-def test_gemm_qkv_epilogue(hip, M, bn, scaled):
+def test_gemm_qkv_epilogue(hip, M, bn, variant, scaled):
     """QKV epilogue: row scale, interleaved-pair RoPE on q / k, K / V into the paged cache at
     slots[row] (-1 skipped), the qkv row written back -- vs GEMM -> rope_kv_ in fp32; 4352 rows
     at bn 192 engage stream-K."""
     x, w, pos, cs, slots, kc, vc = _qkv_setup(M, seed=M + bn)
     ss = ref.ss_partials(x) if scaled else None
     kc2, vc2 = kc.clone(), vc.clone()
-    out = hip.gemm_fused(x, w, 7, bn, None, 2, 1, ss_in=ss, eps=1e-5, positions=pos, cos_sin=cs, slots=slots,
+    out = hip.gemm_fused(x, w, 7, bn, None, variant, 1, ss_in=ss, eps=1e-5, positions=pos, cos_sin=cs, slots=slots,
                          k_cache=kc, v_cache=vc, hq=32, hkv=8, hd=128)
     want = ref.qkv_fused(x, w, ss, 4096, 1e-5, pos, cs, 32, 8, 128, kc2, vc2, slots)
     torch.cuda.synchronize()
-    _close(out, want, 0.03, 0.02, f"qkv M{M} bn{bn}")
+    _close(out, want, 0.03, 0.02, f"qkv M{M} bn{bn} v{variant}")
     _close(kc, kc2, 0.03, 0.02, "k cache")
     _close(vc, vc2, 0.03, 0.02, "v cache")
     assert hip.gemm_streamk(-1) == 0
@@ -869,10 +874,12 @@ def test_gemm_qkv_epilogue_layout(hip):
     slots = torch.arange(M, device=DEV, dtype=torch.int32)
     kc = torch.zeros(M // 16, Hkv, 16, D, device=DEV, dtype=torch.bfloat16)
     vc, kc2, vc2 = kc.clone(), kc.clone(), kc.clone()
-    out = hip.gemm_fused(x, w, 7, 256, None, 2, 1, positions=pos, cos_sin=cs, slots=slots, k_cache=kc, v_cache=vc,
-                         hq=Hq, hkv=Hkv, hd=D)
-    want = ref.qkv_fused(x, w, None, H, 1e-5, pos, cs, Hq, Hkv, D, kc2, vc2, slots)
-    assert torch.equal(out.cpu(), want.cpu()) and torch.equal(kc.cpu(), kc2.cpu()) and torch.equal(vc.cpu(), vc2.cpu())
+    for variant in (2, 3):
+        kc.zero_(), vc.zero_(), kc2.zero_(), vc2.zero_()
+        out = hip.gemm_fused(x, w, 7, 256, None, variant, 1, positions=pos, cos_sin=cs, slots=slots, k_cache=kc,
+                             v_cache=vc, hq=Hq, hkv=Hkv, hd=D)
+        want = ref.qkv_fused(x, w, None, H, 1e-5, pos, cs, Hq, Hkv, D, kc2, vc2, slots)
+        assert torch.equal(out.cpu(), want.cpu()) and torch.equal(kc.cpu(), kc2.cpu()) and torch.equal(vc.cpu(), vc2.cpu())
 
 
 @pytest.mark.parametrize("lo,n_local", [(0, None), (0, 300), (300, 300), (600, 424)])
