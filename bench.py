@@ -475,7 +475,8 @@ def main():
     lat = [r.timings.get("e2e_s", 0.0) for r in results if r.timings]
     ptok = [r.prompt_tokens for r in results if r.prompt_tokens]
     pre = [r.timings.get("cached_prefix_tokens", 0) for r in results if r.timings]
-    stats = torch.tensor([elapsed, float(len(results)), float(sum(ptok)), float(len(ptok))],
+    stats = torch.tensor([elapsed, float(len(results)), float(sum(ptok)), float(len(ptok)),
+                          float(torch.cuda.current_device() if on_gpu else -1)],
                          dtype=torch.float64, device=dev)
     if world > 1:
         if args.one_device:
@@ -546,14 +547,35 @@ def main():
                                         "jumped_tokens", "prompt_tokens", "preemptions")
                               if any(r.timings.get(k) is not None for r in grp)}
         par = f"dp{n_replicas}" if args.tp == 1 else f"tp{args.tp}" + (f"xdp{n_replicas}" if n_replicas > 1 else "")
+        # what the process group really was, and what every replica (its TP leader) contributed:
+        # a scaling record can show that all N ranks ran and every replica completed requests
+        import socket
+
+        dist_info = {
+            "initialized": dist.is_initialized(),
+            "world_size": dist.get_world_size() if dist.is_initialized() else 1,
+            "backend": dist.get_backend() if dist.is_initialized() else None,
+            "env_world_size": world,
+            "visible_devices": torch.cuda.device_count() if on_gpu else 0,
+            "devices_used": sorted({int(d) for d in allst[:, 4].tolist()}) if on_gpu else [],
+            "host": socket.gethostname(),
+            "per_replica": [{"replica": rk // args.tp, "rank": rk, "completions": int(allst[rk, 1]),
+                             "elapsed_s": round(float(allst[rk, 0]), 3),
+                             "qps": round(float(allst[rk, 1]) / float(allst[rk, 0]), 3) if float(allst[rk, 0]) else None}
+                            for rk in range(allst.shape[0]) if rk % args.tp == 0],
+        }
         sim = {}
         if args.tp > 1 and getattr(tpg, "xgmi", None) is not None:
             # the measured collective table the TP group routes by (parallel/xgmi_ar.py tune)
             sim["tp_collectives"] = {"routes": {str(k): v for k, v in tpg.xgmi.table.items()},
                                      "us_by_rows": {str(k): v for k, v in tpg.xgmi.timings.items()},
                                      "mode": "ipc-only" if tpg.ipc_only else "auto (ipc1 / ipc2 / rccl measured)",
+                                     # the start-up check of every IPC collective against the reference
+                                     "self_check": tpg.xgmi.check,
                                      # handshakes that hit the bounded spin (a peer late by > ~4 s)
                                      "handshake_timeouts": int(tpg.xgmi.error())}
+        elif args.tp > 1:
+            sim["tp_collectives"] = {"mode": "rccl", "self_check": getattr(tpg, "xgmi_check", None)}
         if args.tp_sim > 1:
             par = f"tp{args.tp_sim}-sim (rank-0 shard on one GPU, collectives elided)"
             # what the real group moves per rank: every step's rows through 2 all-reduces per layer
@@ -643,6 +665,7 @@ def main():
                 "knn": knn_info,
                 "setup_s": round(tim_setup, 1),
                 "http_status_counts_rank0": statuses,
+                "distributed": dist_info,
                 **sim,
             },
         }

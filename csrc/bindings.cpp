@@ -644,6 +644,32 @@ at::Tensor select_tokens(const at::Tensor& logits, const c10::optional<at::Tenso
   return out;
 }
 
+// vocab-parallel greedy (parallel/tp.py TPGroup.greedy_ids): per-row packed (value, id) keys
+at::Tensor argmax_key(const at::Tensor& logits, int64_t vocab_lo) {
+  CHECK_CUDA(logits); CHECK_LASTDIM(logits);
+  TORCH_CHECK(logits.dim() == 2, "logits [B, V]");
+  const bool is_bf16 = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(is_bf16 || logits.scalar_type() == at::kFloat, "logits must be bf16 or f32");
+  TORCH_CHECK(logits.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(logits.data_ptr()) % 32 == 0, "logits rows must be 32-byte aligned");
+  TORCH_CHECK(vocab_lo >= 0 && vocab_lo + logits.size(1) < (1ll << 31), "vocab_lo");
+  const int B = logits.size(0), V = logits.size(1);
+  at::Tensor keys = at::empty({B}, logits.options().dtype(at::kLong));
+  int rc = lk_argmax_key(logits.data_ptr(), is_bf16 ? 1 : 0, logits.stride(0), B, V, (int)vocab_lo,
+                         reinterpret_cast<long long*>(keys.data_ptr<int64_t>()), cur_stream());
+  CHECK_RC(rc, "argmax_key");
+  return keys;
+}
+
+at::Tensor keys_to_ids(const at::Tensor& keys) {
+  CHECK_CUDA(keys); CHECK_CONTIG(keys);
+  TORCH_CHECK(keys.scalar_type() == at::kLong && keys.dim() == 2, "keys [W, R] int64");
+  const int W = keys.size(0), R = keys.size(1);
+  at::Tensor ids = at::empty({R}, keys.options().dtype(at::kInt));
+  int rc = lk_keys_to_ids(reinterpret_cast<const long long*>(keys.data_ptr<int64_t>()), W, R, ids.data_ptr<int>(), cur_stream());
+  CHECK_RC(rc, "keys_to_ids");
+  return ids;
+}
+
 // token selection restricted per row to an allowed id list (grammar-constrained decoding)
 at::Tensor select_allowed(const at::Tensor& logits, const at::Tensor& plan, const c10::optional<at::Tensor>& temps,
                           int64_t seed, int64_t step) {
@@ -878,6 +904,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_rows", &embed_rows, "", py::arg("table"), py::arg("ids"), py::arg("lo") = 0, py::arg("n_local") = -1);
   m.def("scatter_ids", &scatter_ids);
   m.def("gather_rows", &gather_rows);
+  m.def("argmax_key", &argmax_key, "", py::arg("logits"), py::arg("vocab_lo") = 0);
+  m.def("keys_to_ids", &keys_to_ids);
   m.def("gemm_streamk", &gemm_streamk,
         "stream-K policy of the prefill GEMM (mode 0 off / 1 on / -1 keep); returns the waits that gave up since the last call",
         py::arg("mode") = -1);

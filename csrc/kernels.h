@@ -153,6 +153,10 @@ int lk_select_allowed(const void* logits, int is_bf16, long ls, int B, int V, co
                       unsigned long long seed, int step, const int* plan, int* out, hipStream_t st);
 int lk_select_tokens(const void* logits, int is_bf16, long ls, int B, int V, const float* temps,
                      unsigned long long seed, int step, int* out, hipStream_t st);
+// vocab-parallel greedy: per row an order-preserving int64 key of (max value, vocab_lo + argmax)
+// (larger = larger value, then lower id); keys_to_ids: the max over W gathered key rows -> ids
+int lk_argmax_key(const void* logits, int is_bf16, long ls, int B, int V, int vocab_lo, long long* keys, hipStream_t st);
+int lk_keys_to_ids(const long long* keys, int W, int R, int* ids, hipStream_t st);
 int lk_repeat_penalty(void* logits, int is_bf16, long ls, int B, const int* window, int W,
                       const float* penalty, hipStream_t st);
 // Ollama-default sampling (repeat penalty from a device history ring, top-k, top-p,

@@ -26,11 +26,14 @@ LK_DEVICE unsigned hash3(unsigned a, unsigned b, unsigned c) {
 // Gumbel noise per (row, step, id) and the same tie order as scanning the row with every
 // other id masked to -inf -- without materialising the [B, V] mask (3 full passes over
 // the logits) or scanning 128k entries per row.
-template <bool BF16, bool SAMPLE, bool ALLOWED = false>
+// KEY: greedy only; instead of the id, write the row's order-preserving int64 (value, id) key
+// (ops.argmax_key: vocab-parallel greedy = ONE all-gather of these + a max) to key_out
+template <bool BF16, bool SAMPLE, bool ALLOWED = false, bool KEY = false>
 __global__ __launch_bounds__(256) void select_kernel(const void* __restrict__ logits, long ls, int V,
                                                      const float* __restrict__ temps,
                                                      unsigned long long seed, int step,
-                                                     int* __restrict__ out, const int* __restrict__ plan = nullptr) {
+                                                     int* __restrict__ out, const int* __restrict__ plan = nullptr,
+                                                     long long* __restrict__ key_out = nullptr, int key_lo = 0) {
   __shared__ float rs[4];
   __shared__ int ri[4];
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -101,8 +104,25 @@ __global__ __launch_bounds__(256) void select_kernel(const void* __restrict__ lo
         bi = ri[j];
       }
     if (bi == 0x7fffffff) bi = 0;  // all -inf / NaN row: fall back to token 0
-    out[row] = bi;
+    if constexpr (KEY) {
+      // high word: the max's float bits made order-preserving and signed; low word: ~global id
+      // (the larger key is the larger value, then the lower id -- torch.argmax's tie order)
+      const unsigned fb = __float_as_uint(best == best ? best : -INFINITY);
+      const unsigned u = (fb & 0x80000000u) ? ~fb : (fb | 0x80000000u);
+      key_out[row] = (long long)(((unsigned long long)(u ^ 0x80000000u) << 32) | (unsigned)(~(unsigned)(bi + key_lo)));
+    } else {
+      out[row] = bi;
+    }
   }
+}
+
+// ids[r] = the id of max_w keys[w, r] (the gathered per-rank argmax keys)
+__global__ void keys_to_ids_kernel(const long long* __restrict__ keys, int W, int R, int* __restrict__ ids) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  long long k = keys[r];
+  for (int w = 1; w < W; ++w) k = max(k, keys[(long)w * R + r]);
+  ids[r] = (int)(~(unsigned)(k & 0xFFFFFFFFll));
 }
 
 // logits[row, tok] = l > 0 ? l / p : l * p for each UNIQUE token of the row's window
@@ -144,6 +164,21 @@ int lk_select_tokens(const void* logits, int is_bf16, long ls, int B, int V, con
     if (temps) select_kernel<false, true><<<B, 256, 0, st>>>(logits, ls, V, temps, seed, step, out);
     else select_kernel<false, false><<<B, 256, 0, st>>>(logits, ls, V, temps, seed, step, out);
   }
+  return 0;
+}
+
+int lk_argmax_key(const void* logits, int is_bf16, long ls, int B, int V, int vocab_lo, long long* keys, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (ls % 8 && is_bf16) return -1;
+  if (is_bf16) select_kernel<true, false, false, true><<<B, 256, 0, st>>>(logits, ls, V, nullptr, 0, 0, nullptr, nullptr, keys, vocab_lo);
+  else select_kernel<false, false, false, true><<<B, 256, 0, st>>>(logits, ls, V, nullptr, 0, 0, nullptr, nullptr, keys, vocab_lo);
+  return 0;
+}
+
+int lk_keys_to_ids(const long long* keys, int W, int R, int* ids, hipStream_t st) {
+  if (R <= 0) return 0;
+  if (W < 1) return -1;
+  keys_to_ids_kernel<<<(R + 255) / 256, 256, 0, st>>>(keys, W, R, ids);
   return 0;
 }
 

@@ -19,7 +19,7 @@ __all__ = [
     "rmsnorm", "layernorm", "embed_layernorm", "silu_mul", "gelu_", "relu_", "rope_kv_",
     "kv_write", "paged_decode", "flash_prefill", "prefill_tiles", "knn_topk", "knn_merge",
     "pool_normalize", "row_norms", "select_tokens", "repeat_penalty_", "sample", "linear", "linear_swiglu",
-    "decode_splits", "rope_cos_sin", "tune_gemm", "tune_decode", "gemm", "linear_add_rmsnorm", "linear_rope_kv",
+    "decode_splits", "rope_cos_sin", "argmax_key", "key_to_id", "tune_gemm", "tune_decode", "gemm", "linear_add_rmsnorm", "linear_rope_kv",
     "prefill_chain_ok", "linear_resid", "linear_qkv_fused", "linear_swiglu_scaled", "embed_rows", "scatter_ids",
     "gather_rows",
 ]
@@ -251,6 +251,25 @@ def select_tokens(logits, temps=None, seed: int = 0, step: int = 0, out=None):
     if use_hip(logits):
         return lib().select_tokens(logits, temps, int(seed) & ((1 << 63) - 1), int(step), out)
     return ref.select_tokens(logits, temps, seed, step)
+
+
+def argmax_key(logits, vocab_lo: int = 0):
+    """Per row an order-preserving int64 key of (max value, vocab_lo + first argmax): the larger
+    key is the larger value, then the LOWER id (torch.argmax's tie order), so the max of the
+    keys gathered from the vocab shards picks the global greedy token (parallel/tp.py)."""
+    if use_hip(logits):
+        return lib().argmax_key(logits, int(vocab_lo))
+    return ref.argmax_key(logits, vocab_lo)
+
+
+def key_to_id(keys):
+    """Global ids from [W, R] gathered argmax keys (max over W), int32 [R]; a [R] key row
+    decodes directly."""
+    if keys.dim() == 1:
+        keys = keys[None]
+    if use_hip(keys):
+        return lib().keys_to_ids(keys.contiguous())
+    return ref.keys_to_ids(keys)
 
 
 def sample(logits, prm, hist, hist_len, seed: int = 0, out=None):

@@ -244,6 +244,25 @@ def select_tokens(logits, temps=None, seed=0, step=0):
     return torch.tensor(out, dtype=torch.int32, device=logits.device)
 
 
+def argmax_key(logits, vocab_lo: int = 0):
+    """Order-preserving int64 (max value, ~(vocab_lo + first argmax)) key per row (the HIP
+    kernel's encoding: csrc/sampling.hip select_kernel<..., KEY>)."""
+    x = logits.float()
+    idx = x.argmax(-1)
+    best = x.gather(1, idx[:, None]).squeeze(1)
+    best = torch.where(torch.isnan(best), torch.full_like(best, float("-inf")), best)
+    fb = best.view(torch.int32).long() & 0xFFFFFFFF
+    u = torch.where(fb >= 0x80000000, (~fb) & 0xFFFFFFFF, fb | 0x80000000)
+    hi = (u ^ 0x80000000) - ((u ^ 0x80000000) >= 0x80000000).long() * (1 << 32)  # signed 32-bit
+    lo = (~(idx + vocab_lo)) & 0xFFFFFFFF
+    return hi * (1 << 32) + lo
+
+
+def keys_to_ids(keys):
+    k = keys.max(dim=0).values
+    return ((~(k & 0xFFFFFFFF)) & 0xFFFFFFFF).int()
+
+
 def repeat_penalty_(logits, window, penalty):
     for b in range(logits.shape[0]):
         p = float(penalty[b])

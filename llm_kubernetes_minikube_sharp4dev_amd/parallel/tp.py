@@ -34,6 +34,8 @@ class TPGroup:
     # xGMI collectives over IPC-mapped peer memory (parallel.xgmi_ar, K14): the fused
     # all-reduce + norm tails by the start-up-measured table, all-gathers / broadcasts
     xgmi: Optional[object] = None
+    # the IPC self-check report of a group taken OFF the IPC path by it (xgmi is then None)
+    xgmi_check: Optional[dict] = None
     # every device collective on the IPC path, never RCCL (several ranks on one device, where
     # RCCL refuses the communicator; LK_TP_COLLECTIVES=ipc)
     ipc_only: bool = False
@@ -44,6 +46,12 @@ class TPGroup:
 
     def _ipc(self, t: torch.Tensor) -> bool:
         return self.xgmi is not None and t.is_cuda
+
+    def _ipc_gather(self, t: torch.Tensor) -> bool:
+        """IPC all-gather / broadcast: attached, verified against the reference at start-up
+        (XgmiAllReduce.self_check), and the message fits the staging region."""
+        return (self._ipc(t) and getattr(self.xgmi, "gather_ok", True)
+                and t.numel() * t.element_size() <= self.xgmi.max_bytes)
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
@@ -89,7 +97,7 @@ class TPGroup:
         """Concatenation over ranks of t [n, ...] -> [size*n, ...]."""
         if self.size == 1:
             return t
-        if self._ipc(t) and t.numel() * t.element_size() <= self.xgmi.max_bytes:
+        if self._ipc_gather(t):
             return self.xgmi.all_gather(t).reshape((t.shape[0] * self.size,) + tuple(t.shape[1:]))
         if dist.get_backend(self.group) == "gloo":
             return self.all_gather_cat(t, dim=0)
@@ -100,7 +108,7 @@ class TPGroup:
     def all_gather_cat(self, t: torch.Tensor, dim: int = -1) -> torch.Tensor:
         if self.size == 1:
             return t
-        if self._ipc(t) and t.numel() * t.element_size() <= self.xgmi.max_bytes:
+        if self._ipc_gather(t):
             return torch.cat(list(self.xgmi.all_gather(t)), dim=dim)
         parts = [torch.empty_like(t) for _ in range(self.size)]
         dist.all_gather(parts, t.contiguous(), group=self.group)
@@ -112,21 +120,20 @@ class TPGroup:
         max (first rank on ties = lowest id, the single-GPU argmax order)."""
         from .. import ops
 
-        ids = ops.select_tokens(local_logits)  # HIP argmax on the bf16 logits (first max), int32
         if self.size == 1:
+            ids = ops.select_tokens(local_logits)  # HIP argmax on the bf16 logits (first max), int32
             return ids if vocab_lo == 0 else ids + vocab_lo
-        idx = ids.long()
-        vals = local_logits.gather(1, idx[:, None]).squeeze(1).float()
-        idx = idx + vocab_lo
-        v = self.all_gather_cat(vals[None], dim=0)
-        i = self.all_gather_cat(idx[None], dim=0)
-        k = v.argmax(dim=0)
-        return i.gather(0, k[None]).squeeze(0).int()
+        # ONE all-gather of packed (value, global id) pairs -- an order-preserving int64 key per
+        # row (ops.argmax_key: the max's float bits high, ~id low, so the largest key is the
+        # largest value and, on ties, the lowest id) -- then the max key over ranks
+        key = ops.argmax_key(local_logits, vocab_lo)
+        keys = self.all_gather_cat(key[None], dim=0)
+        return ops.key_to_id(keys.max(dim=0).values)
 
     def broadcast_(self, t: torch.Tensor) -> torch.Tensor:
         """In place: the group leader's ``t`` on every rank."""
         if self.size > 1:
-            if self._ipc(t) and t.numel() * t.element_size() <= self.xgmi.max_bytes:
+            if self._ipc_gather(t):
                 return self.xgmi.broadcast_(t, root=0)
             dist.broadcast(t, src=self.ranks[0] if self.ranks else 0, group=self.group)
         return t
@@ -220,11 +227,23 @@ def new_tp_groups(tp_size: int, with_ctrl: bool = True) -> TPGroup:
         mode = collectives_mode()
         if mode == "ipc":
             mine.ipc_only = True
+        if mode == "auto" and not _same_host(mine):
+            mode = "rccl"  # IPC handles map only within one host: a group spanning nodes stays on RCCL
         if mode in ("ipc", "auto") and torch.cuda.is_available():
             from .xgmi_ar import attach  # xGMI IPC collectives (K14); the table is tuned with the model
 
             attach(mine, rccl=mode == "auto" and dist.get_backend(mine.group) == "nccl")
     return mine
+
+
+def _same_host(tp: TPGroup) -> bool:
+    """Every rank of the group on this rank's host (gathered over the control group)."""
+    import socket
+
+    group = tp.ctrl if tp.ctrl is not None else tp.group
+    names = [None] * tp.size
+    dist.all_gather_object(names, socket.gethostname(), group=group)
+    return len(set(names)) == 1
 
 
 def collectives_mode() -> str:

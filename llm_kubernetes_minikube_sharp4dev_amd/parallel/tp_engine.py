@@ -325,12 +325,31 @@ def _agree_num_blocks(model, tp: TPGroup, **kw) -> int:
 
 
 def tune_collectives(model, tp: TPGroup):
-    """Measure the group's all-reduce algorithms at the model's hidden size (every rank in
-    lockstep; the leader's table is used by all): xgmi_ar.XgmiAllReduce.tune."""
+    """Self-check the group's IPC collectives against the reference on the real peers, then
+    measure the all-reduce algorithms at the model's hidden size (every rank in lockstep; the
+    leader's table is used by all): xgmi_ar.XgmiAllReduce.self_check / tune.  A group whose
+    IPC all-gather or handshakes failed the check leaves the IPC path (RCCL only); without a
+    usable RCCL communicator (several ranks on one device) that is an error."""
     x = getattr(tp, "xgmi", None)
-    if x is None or x.table or tp.size == 1 or os.environ.get("LK_XGMI_TUNE", "1") == "0":
+    if x is None or x.table or tp.size == 1:
         return
     if not (torch.cuda.is_available() and model.device.type == "cuda"):
+        return
+    if not x.check and os.environ.get("LK_XGMI_SELFCHECK", "1") != "0":
+        t0 = time.perf_counter()
+        rep = x.self_check(model.cfg.hidden)
+        rep["seconds"] = round(time.perf_counter() - t0, 2)
+        if tp.rank == 0 or rep["vetoed_buckets"] or rep["ipc_disabled"]:
+            log.info("TP collectives self-check (rank %d): %s", tp.rank, rep)
+        if rep["ipc_disabled"]:
+            if not x.rccl:
+                raise RuntimeError(f"IPC collectives failed their start-up self-check and the group has no "
+                                   f"RCCL communicator to fall back to: {rep}")
+            log.warning("IPC collectives disabled for this TP group (self-check): %s", rep["reasons_on_rank"])
+            tp.xgmi_check = rep
+            tp.xgmi = None
+            return
+    if os.environ.get("LK_XGMI_TUNE", "1") == "0":
         return
     t0 = time.perf_counter()
     x.tune(model.cfg.hidden)

@@ -17,6 +17,16 @@ live in device memory):
 The all-reduces have a fused residual + RMSNorm form (:meth:`XgmiAllReduce.all_reduce_rmsnorm_`),
 the tail of every row-parallel projection.
 
+Before any of it routes production traffic, :meth:`XgmiAllReduce.self_check` runs every
+all-reduce form (one-shot, two-shot, fused with the residual + RMSNorm tail) per row bucket and
+the all-gather on the real peers against a reference (RCCL where the group has a communicator,
+else a gloo all-reduce of host copies), on small-integer data whose sums are exact in bf16 in any
+order -- so the all-reduce and residual results must be bit-identical; the normalised output
+within one bf16 rounding.  A mismatch routes that (bucket, algorithm) away from the IPC kernel
+with the reason logged; a handshake timeout or a broken all-gather takes the group off the IPC
+path.  Every rank applies the MAX of the flags (one agreement over the control group), and the
+outcome is reported (``self.check``, the bench JSON's ``tp_collectives.self_check``).
+
 Which algorithm serves a message is MEASURED at attach time (:meth:`XgmiAllReduce.tune`): for
 each row bucket the fused tail is timed as one-shot, two-shot and (when the group has a usable
 RCCL communicator) RCCL all-reduce + the norm kernel; the leader's fastest choice per bucket is
@@ -53,6 +63,9 @@ class XgmiAllReduce:
         self.rccl = rccl          # the group's device communicator is usable (not several ranks per device)
         self.table: dict = {}     # rows bucket -> algorithm (tune())
         self.timings: dict = {}   # rows bucket -> {algorithm: us} (leader's measurement)
+        self.bad: dict = {}       # rows bucket -> {algorithms the self-check failed}
+        self.gather_ok = True     # the IPC all-gather / broadcast matched the reference
+        self.check: dict = {}     # self_check() report
         self.state = lib().XgmiAr(tp.rank, tp.size, self.max_bytes)
         mine = self.state.handles()
         blobs = [None] * tp.size
@@ -80,7 +93,15 @@ class XgmiAllReduce:
         if b is not None:
             a = self.table[b]
             return a if (a != "rccl" or self.rccl) else "ipc1"
-        return "ipc2" if self.tp.size >= 4 and nbytes >= self.two_shot_min else "ipc1"
+        a = "ipc2" if self.tp.size >= 4 and nbytes >= self.two_shot_min else "ipc1"
+        bad = self.bad.get(self._check_bucket(rows), ())
+        if a in bad:  # untuned group: the self-check still vetoes a failing kernel
+            a = "rccl" if self.rccl else next((o for o in ("ipc1", "ipc2") if o not in bad), a)
+        return a
+
+    def _check_bucket(self, rows: int):
+        ks = sorted(self.bad)
+        return next((b for b in ks if rows <= b), ks[-1] if ks else None)
 
     def use_two_shot(self, t: torch.Tensor) -> bool:
         rows = t.shape[0] if t.dim() >= 2 else 1
@@ -206,14 +227,111 @@ class XgmiAllReduce:
         group = self.tp.ctrl if self.tp.ctrl is not None else self.tp.group
         dist.broadcast_object_list(box, src=self.tp.ranks[0] if self.tp.ranks else 0, group=group)
         self.timings = box[0]
-        self.table = {T: min(v, key=v.get) for T, v in self.timings.items()}
+        self.table = route_table(self.timings, self.bad, self.rccl)
         if self.error():
             raise RuntimeError("xGMI collective handshake timed out during tuning")
         return self.timings
 
+    # ------------------------------------------------------------------ start-up self-check
+    def _reference_all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        """The trusted all-reduce: RCCL on the device, else gloo on host copies."""
+        if self.rccl:
+            y = t.clone()
+            dist.all_reduce(y, group=self.tp.group)
+            return y
+        y = t.float().cpu()
+        dist.all_reduce(y, group=self.tp.ctrl if self.tp.ctrl is not None else self.tp.group)
+        return y.to(t.dtype).to(t.device)
+
+    def _reference_all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        if self.rccl:
+            parts = [torch.empty_like(t) for _ in range(self.tp.size)]
+            dist.all_gather(parts, t.contiguous(), group=self.tp.group)
+            return torch.stack(parts)
+        parts = [torch.empty_like(t.cpu()) for _ in range(self.tp.size)]
+        dist.all_gather(parts, t.cpu().contiguous(), group=self.tp.ctrl if self.tp.ctrl is not None else self.tp.group)
+        return torch.stack(parts).to(t.device)
+
+    @torch.inference_mode()
+    def self_check(self, hidden: int, rows=TUNE_ROWS, eps: float = 1e-5) -> dict:
+        """Run every IPC collective on the real peers against the reference (see the module
+        doc); record per-bucket failures in ``self.bad`` / ``self.gather_ok`` after a MAX
+        agreement over the group, and return the report (also kept in ``self.check``)."""
+        from .. import ops
+
+        dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+        buckets = [T for T in rows if T * hidden * 2 <= self.max_bytes]
+        algos = ("ipc1", "ipc2")
+        flags = torch.zeros(len(buckets) * 2 + 2, dtype=torch.int64)  # per (bucket, algo); gather; timeout
+        why: dict = {}
+        w = (torch.arange(hidden, device=dev) % 7 + 1).to(torch.bfloat16) / 4  # non-unit norm weight
+        for bi, T in enumerate(buckets):
+            g = torch.Generator().manual_seed(7919 * (self.tp.rank + 1) + T)
+            x = torch.randint(-4, 5, (T, hidden), generator=g).to(torch.bfloat16).to(dev)
+            r = torch.randint(-4, 5, (T, hidden), generator=g).to(torch.bfloat16).to(dev)
+            ref = self._reference_all_reduce(x)
+            r_ref = r.clone()
+            out_ref = ops.rmsnorm(ref.clone(), w, eps, residual=r_ref)
+            for ai, a in enumerate(algos):
+                bad = []
+                y = x.clone()
+                if a == "ipc2":
+                    v = y.view(-1, y.shape[-1])
+                    self.state.all_reduce2(v, v)
+                else:
+                    self.state.all_reduce(y, y)
+                if not torch.equal(y, ref):
+                    bad.append(f"all-reduce differs in {int((y != ref).sum())} of {y.numel()} elements")
+                rr = r.clone()
+                out = self.all_reduce_rmsnorm_(x.clone(), rr, w, eps, algo=a)
+                if not torch.equal(rr, r_ref):
+                    bad.append("fused tail: residual differs")
+                if not torch.allclose(out.float(), out_ref.float(), rtol=2 ** -7, atol=1e-3):
+                    bad.append(f"fused tail: norm output off by {float((out.float() - out_ref.float()).abs().max()):.3g}")
+                if bad:
+                    flags[bi * 2 + ai] = 1
+                    why[f"{T}/{a}"] = "; ".join(bad)
+        probe = torch.arange(1000, dtype=torch.int32, device=dev) * (self.tp.rank + 3)
+        got = self.all_gather(probe)
+        if not torch.equal(got.cpu(), self._reference_all_gather(probe).cpu()):
+            flags[-2] = 1
+            why["all_gather"] = "IPC all-gather differs from the reference"
+        if self.error():
+            flags[-1] = 1
+            why["handshake"] = "an IPC handshake timed out (a peer never arrived)"
+        dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.tp.ctrl if self.tp.ctrl is not None else self.tp.group)
+        self.bad = {T: {a for ai, a in enumerate(algos) if flags[bi * 2 + ai]} for bi, T in enumerate(buckets)}
+        self.gather_ok = not bool(flags[-2])
+        report = {"reference": "rccl" if self.rccl else "gloo (host copies)",
+                  "buckets": {str(T): {a: ("FAILED" if a in self.bad[T] else "ok") for a in algos} for T in buckets},
+                  "all_gather": "ok" if self.gather_ok else "FAILED",
+                  "handshake_timeout": bool(flags[-1]),
+                  "reasons_on_rank": why}
+        vetoed = sorted(T for T, s in self.bad.items() if s)
+        report["vetoed_buckets"] = vetoed
+        report["ipc_disabled"] = bool(flags[-1]) or (not self.gather_ok)
+        if self.table:  # re-route an already-tuned table
+            self.table = route_table(self.timings, self.bad, self.rccl)
+        self.check = report
+        return report
+
     def describe(self) -> str:
         return "; ".join(f"<= {T} rows: {a} ({', '.join(f'{k} {v} us' for k, v in self.timings.get(T, {}).items())})"
                          for T, a in sorted(self.table.items()))
+
+
+def route_table(timings: dict, bad: dict, rccl: bool) -> dict:
+    """Per row bucket the fastest algorithm the self-check did not veto; a bucket where every
+    IPC form failed goes to RCCL (or, without a communicator, keeps its fastest IPC form --
+    ``XgmiAllReduce.check`` then says the group is unusable)."""
+    table = {}
+    for T, v in timings.items():
+        veto = bad.get(T) or bad.get(int(T)) or set()
+        ok = {a: t for a, t in v.items() if a not in veto and (a != "rccl" or rccl)}
+        if not ok:
+            ok = {"rccl": 0.0} if rccl else dict(v)
+        table[T] = min(ok, key=ok.get)
+    return table
 
 
 def attach(tp, max_bytes: int | None = None, rccl: bool = True, tune_hidden: int | None = None) -> XgmiAllReduce:

@@ -592,3 +592,157 @@ def test_shm_control_send_fails_when_a_worker_stops_acknowledging(monkeypatch):
     finally:
         wk.close()
         drv.close()
+
+
+# ---------------------------------------------------------------- IPC self-check / packed greedy
+def test_route_table_respects_self_check_vetoes():
+    """A (bucket, algorithm) the self-check failed is never routed, whatever its timing; a bucket
+    with every IPC form failed goes to RCCL when the group has a communicator."""
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.xgmi_ar import route_table
+
+    timings = {1: {"ipc1": 5.0, "ipc2": 9.0, "rccl": 30.0}, 64: {"ipc1": 20.0, "ipc2": 12.0, "rccl": 25.0},
+               4096: {"ipc1": 900.0, "ipc2": 300.0, "rccl": 200.0}}
+    assert route_table(timings, {}, True) == {1: "ipc1", 64: "ipc2", 4096: "rccl"}
+    assert route_table(timings, {1: {"ipc1"}, 64: {"ipc2"}}, True) == {1: "ipc2", 64: "ipc1", 4096: "rccl"}
+    assert route_table(timings, {1: {"ipc1", "ipc2"}}, True)[1] == "rccl"
+    # no communicator: rccl is never chosen
+    no_rccl = {T: {a: v for a, v in d.items() if a != "rccl"} for T, d in timings.items()}
+    assert route_table(no_rccl, {64: {"ipc2"}}, False) == {1: "ipc1", 64: "ipc1", 4096: "ipc2"}
+
+
+class _FakeIpcState:
+    """CPU stand-in for the HIP IPC state (xgmi_ar): gloo sums; ``broken`` corrupts one
+    algorithm on THIS rank only (the group must still agree to veto it)."""
+
+    def __init__(self, tp, broken=None, gather_broken=False):
+        self.tp, self.broken, self.gather_broken = tp, broken, gather_broken
+
+    def _sum(self, x):
+        y = x.float().clone()
+        dist.all_reduce(y)
+        return y
+
+    def all_reduce(self, inp, out):
+        y = self._sum(inp)
+        if self.broken == "ipc1":
+            y[0, 0] += 1
+        out.copy_(y.to(out.dtype))
+
+    def all_reduce2(self, inp, out, residual=None, w=None, eps=None):
+        y = self._sum(inp)
+        if self.broken == "ipc2":
+            y.view(-1)[-1] += 2
+        if residual is None:
+            out.copy_(y.to(out.dtype))
+            return
+        residual.copy_((residual.float() + y).to(residual.dtype))
+        from llm_kubernetes_minikube_sharp4dev_amd.ops import reference as ref
+
+        out.copy_(ref.rmsnorm(residual.clone(), w, eps))
+
+    def all_reduce_rmsnorm(self, x, residual, w, eps, out):
+        y = self._sum(x)
+        if self.broken == "ipc1":
+            y[0, 0] += 1
+        residual.copy_((residual.float() + y).to(residual.dtype))
+        from llm_kubernetes_minikube_sharp4dev_amd.ops import reference as ref
+
+        out.copy_(ref.rmsnorm(residual.clone(), w, eps))
+
+    def gather(self, src, out, root):
+        parts = [torch.empty_like(src) for _ in range(self.tp.size)]
+        dist.all_gather(parts, src)
+        if self.gather_broken:
+            parts[0] = parts[0].flip(0)
+        out.copy_(torch.cat(parts))
+
+    def error(self):
+        return 0
+
+
+def _selfcheck_worker(rank, world, port, out_path, broken_rank, broken_algo, gather_broken):
+    _init(rank, world, port)
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp import TPGroup
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.xgmi_ar import XgmiAllReduce, route_table
+
+    tp = TPGroup(rank, world, dist.group.WORLD, dist.group.WORLD, list(range(world)))
+    x = XgmiAllReduce.__new__(XgmiAllReduce)
+    x.tp, x.max_bytes, x.two_shot, x.two_shot_min, x.rccl = tp, 1 << 20, None, 1 << 20, False
+    x.table, x.timings, x.bad, x.gather_ok, x.check = {}, {}, {}, True, {}
+    x.state = _FakeIpcState(tp, broken_algo if rank == broken_rank else None, gather_broken and rank == broken_rank)
+    rep = x.self_check(64, rows=(1, 4, 16))
+    table = route_table({T: {"ipc1": 1.0, "ipc2": 2.0} for T in (1, 4, 16)}, x.bad, False)
+    torch.save((rep, {T: sorted(s) for T, s in x.bad.items()}, x.gather_ok, table), f"{out_path}.{rank}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("broken_algo,gather_broken", [(None, False), ("ipc1", False), ("ipc2", False), (None, True)])
+def test_ipc_self_check_agrees_and_vetoes(broken_algo, gather_broken):
+    """The start-up self-check (xgmi_ar.XgmiAllReduce.self_check) on a gloo world of 2 with a
+    fake IPC state: a collective that is wrong on ONE rank is vetoed on BOTH (MAX agreement),
+    the routing table then avoids it, and a broken all-gather takes the group off the IPC path."""
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "sc")
+        mp.spawn(_selfcheck_worker, args=(2, port, path, 1, broken_algo, gather_broken), nprocs=2, join=True)
+        res = [torch.load(f"{path}.{r}", weights_only=False) for r in range(2)]
+    (rep0, bad0, g0, t0), (rep1, bad1, g1, t1) = res
+    assert bad0 == bad1 and g0 == g1 and t0 == t1  # every rank routes alike
+    want = {T: ([broken_algo] if broken_algo else []) for T in (1, 4, 16)}
+    assert bad0 == want
+    if broken_algo:
+        other = "ipc2" if broken_algo == "ipc1" else "ipc1"
+        assert set(t0.values()) == {other}
+        assert rep0["vetoed_buckets"] == [1, 4, 16] and not rep0["ipc_disabled"]
+        assert all(v[broken_algo] == "FAILED" for v in rep0["buckets"].values())
+    assert g0 is (not gather_broken) and rep0["ipc_disabled"] is gather_broken
+    assert rep0["reference"].startswith("gloo")
+
+
+def _greedy_worker(rank, world, port, out_path):
+    _init(rank, world, port)
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.tp import TPGroup
+
+    tp = TPGroup(rank, world, dist.group.WORLD)
+    torch.manual_seed(3)
+    V = 64
+    full = torch.randn(9, world * V)
+    full[1, 5] = 7.0
+    full[1, V + 5] = 7.0      # tie across shards: the lower id wins
+    full[2] = -1.5            # all equal: id 0
+    full[3, world * V - 1] = 50.0
+    shard = full[:, rank * V:(rank + 1) * V].clone()
+    ids = tp.greedy_ids(shard, vocab_lo=rank * V)
+    torch.save((ids, full.argmax(-1).int()), f"{out_path}.{rank}")
+    dist.destroy_process_group()
+
+
+def test_vocab_parallel_greedy_one_packed_all_gather():
+    """TPGroup.greedy_ids: ONE all-gather of packed (value, id) keys over the vocab shards picks
+    exactly torch.argmax over the full row (ties -> lowest global id), on every rank."""
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "g")
+        mp.spawn(_greedy_worker, args=(2, port, path), nprocs=2, join=True)
+        for r in range(2):
+            ids, want = torch.load(f"{path}.{r}", weights_only=True)
+            assert torch.equal(ids, want), (r, ids, want)
+
+
+def test_same_host_gate(monkeypatch):
+    """Auto IPC attach only when every rank of the group is on this host (IPC handles do not map
+    across nodes): the host names come from an all-gather over the control group."""
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel import tp as tpmod
+
+    calls = []
+
+    def fake_gather(out, obj, group=None):
+        calls.append(obj)
+        out[0], out[1] = obj, "other-node" if fake_gather.split else obj
+
+    monkeypatch.setattr(tpmod.dist, "all_gather_object", fake_gather)
+    g = tpmod.TPGroup(0, 2, None, None, [0, 1])
+    fake_gather.split = False
+    assert tpmod._same_host(g)
+    fake_gather.split = True
+    assert not tpmod._same_host(g)
