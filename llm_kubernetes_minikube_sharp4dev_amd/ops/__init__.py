@@ -387,15 +387,28 @@ def _gemm_key(M: int, N: int, K: int, epi: int):
     return ((M + 255) // 256, N, K, epi)
 
 
+# Variant 3 = csrc/gemm1w.hip, the one-wave-per-SIMD 256 x 256 kernel on hipBLASLt's gfx950
+# K-loop schedule: 1.04-1.09x gemm.hip and 0.95-1.10x hipBLASLt on the Llama-3-8B projections
+# (profiles/r5_gemm1w/).  The default for 256-wide tiles once they fill at least one wave of CUs;
+# gemm.hip keeps the 192-wide tiles (QKV at M 4096: 512 tiles = 2 whole waves, where 256-wide
+# tiles leave half a wave idle) and the split-K shapes.  LK_GEMM1W=0 restores round 4's choice.
+GEMM1W = os.environ.get("LK_GEMM1W", "1") != "0"
+GEMM1W_MIN_TILES = 256
+
+
 def _gemm_configs(N: int, epi: int):
-    """(schedule, column tile) candidates the kernel supports for this N / epilogue."""
+    """(schedule, column tile) candidates the kernels support for this N / epilogue."""
     bns = [256] if epi == 1 else [bn for bn in (256, 192) if N % bn == 0]
-    return [(sched, bn) for bn in bns for sched in (0, 1, 2)]
+    cfgs = [(sched, bn) for bn in bns for sched in (0, 1, 2)]
+    if 256 in bns:
+        cfgs.append((3, 256))
+    return cfgs
 
 
 def _gemm_default(M: int, N: int, K: int, epi: int):
-    """Fewest tile-columns x waves: cost(bn) = ceil(tiles / 256 CUs) * bn (ties -> 256), with
-    the 4-phase schedule (fastest on most serving shapes with weights streamed from HBM:
+    """Fewest tile-columns x waves: cost(bn) = ceil(tiles / 256 CUs) * bn (ties -> 256); 256-wide
+    tiles on gemm1w.hip (variant 3) when they fill a wave, else gemm.hip's 4-phase schedule
+    (fastest of its schedules on the serving shapes with weights streamed from HBM:
     profiles/r2_gemm.md)."""
     tm = (M + 255) // 256
     best = None
@@ -406,7 +419,12 @@ def _gemm_default(M: int, N: int, K: int, epi: int):
             best = (cost, bn)
     if best is None:
         return None
-    return (_gemm_sched(K), best[1], _gemm_splits(M, N, K, epi, best[1]))
+    bn = best[1]
+    ks = _gemm_splits(M, N, K, epi, bn)
+    tiles = tm * (N // 2 // 128 if epi == 1 else N // bn)
+    if GEMM1W and bn == 256 and ks == 1 and tiles >= GEMM1W_MIN_TILES and K // 64 >= 3:
+        return (3, 256, 1)
+    return (_gemm_sched(K), bn, ks)
 
 
 # split-K for shapes with at most half as many tiles as CUs (M <= 2048 O / down projections,
@@ -447,7 +465,7 @@ def gemm(x, w, b=None, epi: int = 0, out=None):
     cfg = _GEMM_TABLE.get(key)
     if cfg is None:
         cfg = _gemm_default(M, N, K, epi)
-        if cfg is None or not lib().gemm_supported(M, N, K, epi, cfg[1], cfg[2]):
+        if cfg is None or not lib().gemm_supported(M, N, K, epi, cfg[1], cfg[2], cfg[0]):
             return None
     return lib().gemm(x, w, b, epi, cfg[1], out, cfg[0], cfg[2])
 
@@ -484,7 +502,7 @@ def tune_gemm(weights, max_m: int, min_m: int = 512, iters: int = 6, cold_bytes:
 
     for w, epi in weights:
         N, K = w.shape
-        cfgs = [c for c in _gemm_configs(N, epi) if L.gemm_supported(max_m, N, K, epi, c[1])]
+        cfgs = [c for c in _gemm_configs(N, epi) if L.gemm_supported(max_m, N, K, epi, c[1], 1, c[0])]
         if not cfgs:
             continue
         copies = [w] + [w.clone() for _ in range(max(0, -(-cold_bytes // (N * K * 2)) - 1))]
@@ -511,7 +529,7 @@ def tune_gemm(weights, max_m: int, min_m: int = 512, iters: int = 6, cold_bytes:
             # keep the default policy's split-K for the winning tile (a 2-tuple
             # entry silently dropped it on the low-tile-count O / down shapes)
             ks = _gemm_splits(mb * 256, N, K, epi, bn)
-            _GEMM_TABLE[key] = (sched, bn, ks if L.gemm_supported(mb * 256, N, K, epi, bn, ks) else 1)
+            _GEMM_TABLE[key] = (sched, bn, ks if L.gemm_supported(mb * 256, N, K, epi, bn, ks, sched) else 1)
             out[key] = {f"s{c[0]}/{c[1]}": round(t, 1) for c, t in med.items()}
         del copies
     return out
@@ -585,7 +603,7 @@ def tune_decode(weights, ms: Sequence[int] = DECODE_TUNE_MS, iters: int = 5, col
                 arms["ws"] = lambda c, x=x: L.ws_linear(x, c, swiglu)
             epi = 1 if swiglu else 0
             cfg = _gemm_default(M, N, K, epi)
-            if cfg is not None and L.gemm_supported(M, N, K, epi, cfg[1], cfg[2]):
+            if cfg is not None and L.gemm_supported(M, N, K, epi, cfg[1], cfg[2], cfg[0]):
                 arms["gemm"] = lambda c, x=x, cfg=cfg: L.gemm(x, c, None, epi, cfg[1], None, cfg[0], cfg[2])
             if len(arms) < 2:
                 continue
@@ -721,16 +739,16 @@ def prefill_chain_ok(x, w_qkv, w_o, w_gate_up, w_down) -> bool:
     L = lib()
     N, K = w_qkv.shape
     c = _cfg_of(M, N, K, 0)
-    if c is None or c[2] != 1 or not L.gemm_supported(M, N, K, EPI_QKV, c[1], 1):
+    if c is None or c[2] != 1 or not L.gemm_supported(M, N, K, EPI_QKV, c[1], 1, c[0]):
         return False
     N, K = w_gate_up.shape
     c = _cfg_of(M, N, K, 1)
-    if c is None or c[2] != 1 or not L.gemm_supported(M, N, K, 1, c[1], 1):
+    if c is None or c[2] != 1 or not L.gemm_supported(M, N, K, 1, c[1], 1, c[0]):
         return False
     for w in (w_o, w_down):
         N, K = w.shape
-        _, bn, ks = _resid_cfg(M, N, K)
-        if not L.gemm_supported(M, N, K, EPI_RESID, bn, ks):
+        sched, bn, ks = _resid_cfg(M, N, K)
+        if not L.gemm_supported(M, N, K, EPI_RESID, bn, ks, sched):
             return False
     return True
 

@@ -308,6 +308,25 @@ def test_gemm_split_k_policy():
     assert ops._gemm_default(256, 768, 768, 2)[2] == 1  # 12 K-tiles: < 8 per split at S 2
 
 
+def test_gemm1w_default_policy(monkeypatch):
+    """256-wide prefill tiles go to the one-wave-per-SIMD kernel (variant 3, csrc/gemm1w.hip) once
+    they fill a wave of 256 CUs; QKV at M 4096 keeps gemm.hip's 192-wide tiles (2 whole waves),
+    split-K shapes stay on gemm.hip; LK_GEMM1W=0 turns it off."""
+    from llm_kubernetes_minikube_sharp4dev_amd import ops
+
+    monkeypatch.setattr(ops, "GEMM1W", True)
+    assert ops._gemm_default(4096, 4096, 4096, 0) == (3, 256, 1)      # O
+    assert ops._gemm_default(4096, 4096, 14336, 6) == (3, 256, 1)     # down, RESID
+    assert ops._gemm_default(4096, 28672, 4096, 1) == (3, 256, 1)     # gate_up + SwiGLU
+    assert ops._gemm_default(4096, 6144, 4096, 7)[:2] == (ops._gemm_sched(4096), 192)  # QKV: 2 whole waves
+    assert ops._gemm_default(8192, 6144, 4096, 0) == (3, 256, 1)      # tie on waves -> 256
+    assert ops._gemm_default(1024, 4096, 4096, 0)[0] != 3             # 64 tiles: split-K on gemm.hip
+    assert (3, 256) in ops._gemm_configs(4096, 0) and (3, 256) in ops._gemm_configs(28672, 1)
+    assert all(c[0] != 3 for c in ops._gemm_configs(1152, 0))         # no 256-wide tile
+    monkeypatch.setattr(ops, "GEMM1W", False)
+    assert ops._gemm_default(4096, 4096, 4096, 0)[0] == ops._gemm_sched(4096)
+
+
 def test_lib_path_ab_knob_loads_the_named_build():
     """LK_LIB_PATH (same-box A/B of two builds of the kernel library) loads the extension from
     the given file instead of the in-tree one."""
