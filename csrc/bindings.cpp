@@ -345,11 +345,13 @@ at::Tensor gemm_fused(const at::Tensor& x, const at::Tensor& w, int64_t epi, int
 // embedding rows from int32 ids (vocab shard [lo, lo + n_local) of a vocab-parallel table: others 0)
 at::Tensor embed_rows(const at::Tensor& table, const at::Tensor& ids, int64_t lo, int64_t n_local) {
   CHECK_CUDA(table); CHECK_BF16(table); CHECK_CONTIG(table); CHECK_CUDA(ids); CHECK_I32(ids); CHECK_CONTIG(ids);
+  const int strict = (lo == 0 && n_local < 0) ? 1 : 0;  // the whole table: an id outside it is an error
   if (n_local < 0) n_local = table.size(0);
   TORCH_CHECK(table.dim() == 2 && table.size(1) % 8 == 0 && n_local <= table.size(0), "table [V, H], H % 8");
   check_rows16(table, "table");
   at::Tensor out = at::empty({ids.numel(), table.size(1)}, table.options());
-  CHECK_RC(lk_embed_rows(bp(out), bp(table), ip(ids), ids.numel(), table.size(1), lo, n_local, cur_stream()), "embed_rows");
+  CHECK_RC(lk_embed_rows(bp(out), bp(table), ip(ids), ids.numel(), table.size(1), lo, n_local, cur_stream(), strict),
+           "embed_rows");
   return out;
 }
 
@@ -902,6 +904,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("cos_sin") = py::none(), py::arg("slots") = py::none(), py::arg("k_cache") = py::none(),
         py::arg("v_cache") = py::none(), py::arg("hq") = 0, py::arg("hkv") = 0, py::arg("hd") = 0);
   m.def("embed_rows", &embed_rows, "", py::arg("table"), py::arg("ids"), py::arg("lo") = 0, py::arg("n_local") = -1);
+  m.def("embed_errors", []() { return (int64_t)lk_embed_errors(); },
+        "token ids outside the (whole) embedding table seen since the last call (resets)");
   m.def("scatter_ids", &scatter_ids);
   m.def("gather_rows", &gather_rows);
   m.def("argmax_key", &argmax_key, "", py::arg("logits"), py::arg("vocab_lo") = 0);

@@ -171,6 +171,7 @@ int lk_window_mark(int id, hipStream_t st);
 
 // csrc/step_ops.hip: the forward's small per-step gathers (no framework kernels in a step)
 int lk_embed_rows(bf16_t* out, const bf16_t* table, const int* ids, long T, int H, long lo, long n_local,
-                  hipStream_t st);
+                  hipStream_t st, int strict = 0);
+int lk_embed_errors();  // out-of-table ids seen by strict lk_embed_rows since the last call
 int lk_scatter_ids(int* ids, const long* dst, const int* prev, const long* src, int n, hipStream_t st);
 int lk_gather_rows(bf16_t* out, const bf16_t* x, long xs, const long* idx, long R, int H, hipStream_t st);

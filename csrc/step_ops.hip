@@ -5,12 +5,17 @@
 #include "common.h"
 #include "kernels.h"
 
+// token ids outside a whole (non-sharded) table since the last lk_embed_errors() read: a bad id
+// must not pass as a silent zero embedding (the engine polls this with the GEMM health check)
+__device__ int g_embed_bad_ids = 0;
+
 namespace {
 
-// out[t, :] = table[ids[t] - lo, :] if lo <= ids[t] < lo + n_local else 0   (row of H bf16)
+// out[t, :] = table[ids[t] - lo, :] if lo <= ids[t] < lo + n_local else 0   (row of H bf16);
+// strict (the whole table, no vocab shard): an id outside it is also counted in g_embed_bad_ids
 __global__ __launch_bounds__(256) void embed_rows_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ table,
                                                          const int* __restrict__ ids, long T, int H, long lo,
-                                                         long n_local) {
+                                                         long n_local, int strict) {
   const int vpr = H >> 3;
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= T * vpr) return;
@@ -19,6 +24,7 @@ __global__ __launch_bounds__(256) void embed_rows_kernel(bf16_t* __restrict__ ou
   const long id = (long)ids[t] - lo;
   uint4_t v = {0u, 0u, 0u, 0u};
   if (id >= 0 && id < n_local) v = *reinterpret_cast<const uint4_t*>(table + id * H + c * 8);
+  else if (strict && c == 0) atomicAdd(&g_embed_bad_ids, 1);
   *reinterpret_cast<uint4_t*>(out + t * H + c * 8) = v;
 }
 
@@ -44,12 +50,23 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(bf16_t* __restrict__ o
 }  // namespace
 
 int lk_embed_rows(bf16_t* out, const bf16_t* table, const int* ids, long T, int H, long lo, long n_local,
-                  hipStream_t st) {
+                  hipStream_t st, int strict) {
   if (H % 8 || T < 0) return -1;
   if (T == 0) return 0;
   const long n = T * (H / 8);
-  embed_rows_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(out, table, ids, T, H, lo, n_local);
+  embed_rows_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(out, table, ids, T, H, lo, n_local, strict);
   return 0;
+}
+
+// ids outside the table counted by strict embed_rows launches since the last call (resets)
+int lk_embed_errors() {
+  int v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_embed_bad_ids), sizeof(int)) != hipSuccess) return -1;
+  if (v) {
+    const int zero = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_embed_bad_ids), &zero, sizeof(int));
+  }
+  return v;
 }
 
 int lk_scatter_ids(int* ids, const long* dst, const int* prev, const long* src, int n, hipStream_t st) {

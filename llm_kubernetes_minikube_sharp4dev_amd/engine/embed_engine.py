@@ -31,6 +31,14 @@ EMBED_STREAMS = int(os.environ.get("LK_EMBED_STREAMS", "2"))
 # so one batch's memory-bound kernels (attention, LayerNorm, pooling) and its GEMMs' partial last
 # waves overlap the next batch's work instead of draining the device between kernels
 BUILD_STREAMS = int(os.environ.get("LK_EMBED_BUILD_STREAMS", "2"))
+# The LK_GEMM_LIBRARY=1 measurement arm sends the encoder's GEMMs to hipBLASLt, whose gfx950
+# stream-K kernels (..._SK3_...) keep workgroups waiting on other workgroups' partial tiles: two
+# such persistent grids on two streams can fill the CUs with waiters whose producers cannot be
+# dispatched (round 4 recorded a 485k-chunk index build that stalled 180 s under that arm).  Our
+# own kernels never wait across workgroups outside gemm.hip's guarded stream-K path, so only that
+# arm drops to ONE stream for builds and serving embeddings.
+if os.environ.get("LK_GEMM_LIBRARY", "0") == "1":
+    BUILD_STREAMS = EMBED_STREAMS = 1
 
 
 class EmbeddingEngine:

@@ -303,7 +303,8 @@ class LLMEngine:
     def _check_gemm_health():
         """Fail loudly if a stream-K prefill GEMM gave up waiting for a partial tile since the
         last check (csrc/gemm.hip poisons such a tile with NaN; never expected: the wait is a
-        bound instead of a hang).  One 4-byte device read per GEMM_HEALTH_EVERY steps."""
+        bound instead of a hang), or a token id outside the vocabulary reached the embedding
+        (csrc/step_ops.hip counts them).  Two 4-byte device reads per GEMM_HEALTH_EVERY steps."""
         from .. import ops
 
         if not ops.available():
@@ -311,6 +312,10 @@ class LLMEngine:
         errs = int(ops.lib().gemm_streamk(-1))
         if errs:
             raise RuntimeError(f"stream-K GEMM: {errs} partial-tile wait(s) timed out; outputs were poisoned")
+        bad = int(ops.lib().embed_errors())
+        if bad:
+            raise RuntimeError(f"embedding: {bad} token id(s) outside the vocabulary were looked up (a tokenizer / "
+                               f"model vocab mismatch); their rows were zero")
 
     def _jump(self, seq: Sequence, now: float):
         """Grammar jump-forward: append the tokens ``seq``'s grammar allows exactly one choice

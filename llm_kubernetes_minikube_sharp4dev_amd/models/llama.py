@@ -3,7 +3,8 @@
 
 MI355X layout decisions:
   * fused QKV and fused gate|up weights -> one hand-written MFMA GEMM each instead of 3 / 2
-    (csrc/gemm.hip for prefill-sized steps, csrc/skinny_gemm.hip weight streaming for decode);
+    (csrc/gemm1w.hip / csrc/gemm.hip for prefill-sized steps, csrc/skinny_gemm.hip weight
+    streaming for decode);
   * the residual stream is carried separately and folded into the RMSNorm kernel
     (``x = norm(res += y)``), so no standalone add pass ever touches HBM;
   * RoPE and the paged-KV write are one kernel on the QKV output;
@@ -13,8 +14,11 @@ MI355X layout decisions:
     per-row rsqrt the consumer GEMM applies in its epilogue from partial sums of squares the
     producing O / down GEMM wrote, and RoPE + the paged-KV write are the QKV GEMM's epilogue;
   * attention reads K/V from the paged cache (flash prefill / split-K decode);
-  * tensor parallel: column-parallel QKV / gate_up, row-parallel o / down with one
-    RCCL all-reduce each, vocab-parallel embedding + LM head;
+  * tensor parallel: column-parallel QKV / gate_up, row-parallel o / down, each followed by
+    one all-reduce fused with the residual add + RMSNorm -- the xGMI IPC kernel
+    (csrc/xgmi_allreduce.hip, one- or two-shot) or RCCL + the norm kernel, per row bucket as
+    measured at start-up (parallel/xgmi_ar.py); vocab-parallel embedding + LM head (greedy: one
+    all-gather of packed (value, id) keys);
   * sequence parallel for prefill-sized steps (``sp_min_tokens``): residual stream and
     norms sharded over the T rows, reduce-scatter / all-gather instead of all-reduce.
 """

@@ -796,9 +796,14 @@ def linear_qkv_fused(x, w, ss, eps: float, positions, cos_sin, Hq: int, Hkv: int
 def embed_rows(table, ids, lo: int = 0, n_local: Optional[int] = None):
     """Rows of ``table`` for int32 ``ids``; with ``lo`` / ``n_local`` a vocab-parallel shard:
     ids outside [lo, lo + n_local) give zero rows (summed over the TP group afterwards)."""
+    whole = lo == 0 and n_local is None
     n_local = table.shape[0] if n_local is None else n_local
     if use_hip(table) and ids.dtype == torch.int32:
-        return lib().embed_rows(table, ids.contiguous(), lo, n_local)
+        # the whole table: an out-of-range id is counted on the device (lib().embed_errors(),
+        # polled by the engine's health check) instead of becoming a silent zero row
+        return lib().embed_rows(table, ids.contiguous(), lo, -1 if whole else n_local)
+    if whole:
+        return table[ids.long()]  # raises on a bad id, like an nn.Embedding lookup
     local = ids.long() - lo
     mask = (local < 0) | (local >= n_local)
     return table[local.clamp(0, max(0, n_local - 1))].masked_fill(mask[:, None], 0)

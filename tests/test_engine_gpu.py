@@ -19,18 +19,24 @@ PROMPTS = [[5, 17, 99, 3, 250, 7, 7, 1, 400, 33, 21, 8, 2, 9, 11, 60, 61, 62, 63
            list(range(10, 90)), [300, 301], list(range(200, 237))]
 
 
-def _hf_llama():
+def _hf_llama(random_norms: bool = False):
     cfg = transformers.LlamaConfig(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
                                    num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=1024,
                                    rope_theta=10000.0, rms_norm_eps=1e-5, tie_word_embeddings=False)
     torch.manual_seed(0)
     hf = transformers.LlamaForCausalLM(cfg).eval()
+    if random_norms:  # HF initialises RMSNorm weights to 1: real checkpoints do not
+        g = torch.Generator().manual_seed(11)
+        with torch.no_grad():
+            for mod in hf.modules():
+                if isinstance(mod, transformers.models.llama.modeling_llama.LlamaRMSNorm):
+                    mod.weight.copy_(torch.rand(mod.weight.shape, generator=g) * 1.5 + 0.25)
     ours = DecoderConfig("t", "llama", 2, 256, 4, 2, 64, 512, 512, max_position=1024, rope_theta=10000.0)
     return hf, ours
 
 
-def _gpu_llama():
-    hf, cfg = _hf_llama()
+def _gpu_llama(random_norms: bool = False):
+    hf, cfg = _hf_llama(random_norms)
     m = build_decoder(cfg, device=DEV, dtype=torch.bfloat16)
     m.load_hf_state_dict(hf.state_dict())
     return hf, m
@@ -282,17 +288,24 @@ def test_forced_reference_fails_loudly_not_silently():
         del os.environ["LK_FORCE_REFERENCE"]
 
 
-def test_fused_prefill_chain_matches_hf(monkeypatch):
+@pytest.mark.parametrize("random_norms,gemm1w", [(False, False), (True, False), (True, True)])
+def test_fused_prefill_chain_matches_hf(monkeypatch, random_norms, gemm1w):
     """A folded GPU model runs prefill-sized steps (> 256 rows) as the fused GEMM chain (RoPE +
     KV write in the QKV epilogue, norms folded into the GEMMs) -- logits vs HF fp32 -- and the
-    same greedy tokens as the unfused path (LK_PREFILL_CHAIN=0), up to near-ties."""
+    same greedy tokens as the unfused path (LK_PREFILL_CHAIN=0), up to near-ties.  With
+    non-unit RMSNorm weights (folded into the bf16 QKV / gate_up weights, as a real checkpoint's
+    are) and on either prefill GEMM (gemm.hip, or gemm1w.hip forced past its tile-count gate)."""
     from llm_kubernetes_minikube_sharp4dev_amd import ops
 
-    hf, m = _gpu_llama()
+    hf, m = _gpu_llama(random_norms)
     assert m.folded and not m.rope_neox
     # the toy QKV GEMM has 4 tiles, which the default dispatch would split over K (and a split
     # QKV GEMM has no in-kernel epilogue, so the chain would not be taken)
     monkeypatch.setattr(ops, "GEMM_SPLITK", False)
+    monkeypatch.setattr(ops, "GEMM1W", gemm1w)
+    if gemm1w:
+        monkeypatch.setattr(ops, "GEMM1W_MIN_TILES", 0)
+        assert ops._gemm_default(512, 1024, 256, 1)[0] == 3
     # 512 prefill rows in one step (a multiple of the scheduler's 256-row alignment, so no chunk
     # is trimmed and every prompt's last row is in this step)
     prompts = [list(range(3 + i, 3 + i + 128)) for i in range(4)]
@@ -315,6 +328,26 @@ def test_fused_prefill_chain_matches_hf(monkeypatch):
     monkeypatch.setattr(ops, "PREFILL_CHAIN", False)
     plain = [s.output_ids for s in _engine(m, use_graphs=True).generate(prompts, SamplingParams.greedy(10))]
     _assert_same_or_near_tie(hf, prompts, fused, plain)
+
+
+def test_folded_norms_greedy_parity_long_decode(monkeypatch):
+    """Folding the RMSNorm weights into the bf16 QKV / gate_up weights (LK_FOLD_NORMS, the GPU
+    default) rounds w * g back to bf16: over 200 greedy decode steps per prompt the folded model
+    emits the unfolded model's tokens, up to near-ties (checked in fp32 against HF)."""
+    from llm_kubernetes_minikube_sharp4dev_amd.models import llama as llama_mod
+
+    hf, cfg = _hf_llama(random_norms=True)
+    monkeypatch.setattr(llama_mod, "FOLD_NORMS", False)
+    plain_m = build_decoder(cfg, device=DEV, dtype=torch.bfloat16)
+    plain_m.load_hf_state_dict(hf.state_dict())
+    monkeypatch.setattr(llama_mod, "FOLD_NORMS", True)
+    fold_m = build_decoder(cfg, device=DEV, dtype=torch.bfloat16)
+    fold_m.load_hf_state_dict(hf.state_dict())
+    assert fold_m.folded and not getattr(plain_m, "folded", False)
+    prompts = [p for p in PROMPTS[:3]]
+    a = [s.output_ids for s in _engine(fold_m, use_graphs=True).generate(prompts, SamplingParams.greedy(200))]
+    b = [s.output_ids for s in _engine(plain_m, use_graphs=True).generate(prompts, SamplingParams.greedy(200))]
+    _assert_same_or_near_tie(hf, prompts, a, b)
 
 
 def test_bulk_embedding_two_streams_bit_identical(monkeypatch):

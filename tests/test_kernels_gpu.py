@@ -895,6 +895,27 @@ def test_embed_rows(hip, lo, n_local):
     assert torch.equal(got.cpu(), want.cpu())
 
 
+def test_embed_rows_counts_out_of_vocab_ids(hip):
+    """The whole-table lookup (no vocab shard) counts ids outside the table on the device, so a
+    tokenizer / model vocab mismatch fails the engine's health check instead of passing as
+    silent zero embeddings; a vocab-parallel shard's out-of-shard ids are not errors."""
+    V, H = 512, 1024
+    table = torch.randn(V, H, device=DEV, dtype=torch.bfloat16)
+    hip.embed_errors()  # reset
+    ids = torch.tensor([0, 5, V - 1, 3], device=DEV, dtype=torch.int32)
+    ops.embed_rows(table, ids)
+    torch.cuda.synchronize()
+    assert hip.embed_errors() == 0
+    bad = torch.tensor([1, V, V + 7, -2, 4], device=DEV, dtype=torch.int32)
+    out = ops.embed_rows(table, bad)
+    torch.cuda.synchronize()
+    assert hip.embed_errors() == 3 and hip.embed_errors() == 0
+    assert torch.equal(out[1].cpu(), torch.zeros(H, dtype=torch.bfloat16))
+    ops.embed_rows(table, bad, 0, 256)  # shard [0, 256): out-of-shard ids are the TP contract
+    torch.cuda.synchronize()
+    assert hip.embed_errors() == 0
+
+
 def test_scatter_ids_and_gather_rows(hip):
     ids = torch.arange(64, device=DEV, dtype=torch.int32)
     prev = torch.randint(0, 1000, (16,), device=DEV, dtype=torch.int32)
