@@ -33,7 +33,7 @@ from .tp import TPGroup
 log = get_logger("tp")
 
 
-_CMDS = ("stop", "step", "capture", "barrier", "knn")
+_CMDS = ("stop", "step", "capture", "barrier", "knn", "shard")
 # StepInputs array fields in wire order (lists travel as int32 arrays; gather = (dst, src))
 _FIELDS = ("ids", "positions", "slots", "q_lens", "ctx_lens", "tables_p", "ctx_d", "tables_d", "logits_rows",
            "gather_dst", "gather_src")
@@ -65,6 +65,8 @@ def encode_msg(cmd: str, arg=None) -> tuple[np.ndarray, np.ndarray]:
         raw = q.contiguous().view(-1).view(torch.uint8).numpy()
         h[2], h[7], h[8], h[9] = int(q.dtype == torch.float32), q.shape[0], q.shape[1], int(k)
         parts.append(np.frombuffer(np.ascontiguousarray(np.pad(raw, (0, (-raw.size) % 4))).tobytes(), dtype=np.int32))
+    elif cmd == "shard":  # (rows, dim, f32): the corpus rows follow as one scatter over the control group
+        h[7], h[8], h[2] = int(arg[0]), int(arg[1]), int(bool(arg[2]))
     elif cmd == "step":
         si = arg
         h[2], h[3], h[4], h[5], h[6] = si.num_decode, si.decode_graph, int(si.greedy), si.shared_len, si.prev_bcast
@@ -99,6 +101,8 @@ def decode_msg(h: np.ndarray, payload: np.ndarray):
         dt, esz = (torch.float32, 4) if h[2] else (torch.bfloat16, 2)
         raw = torch.from_numpy(payload.copy().view(np.uint8)[: nq * d * esz].copy())
         return cmd, (raw.view(dt).view(nq, d), k)
+    if cmd == "shard":
+        return cmd, (int(h[7]), int(h[8]), bool(h[2]))
     if cmd != "step":
         return cmd, None
     out, off = {}, 0
@@ -163,6 +167,9 @@ class _ShmChannel:
             self.acks[:] = 0
         self.me, self.n_workers, self.next = worker_index, n_workers, 1
         self.created = create
+        # a follower whose parent (the serving supervisor, or the leader that spawned it) is
+        # gone stops waiting: the leader can no longer send it "stop"
+        self.ppid = os.getppid()
         # a worker that stops acknowledging (crash, hang) fails the driver's step instead of
         # spinning it forever: the engine's failure path then ends the in-flight requests
         self.timeout_s = float(os.environ.get("LK_TP_CTRL_TIMEOUT_S", "120"))
@@ -196,6 +203,8 @@ class _ShmChannel:
             if spins > 20000:
                 time.sleep(sleep)
                 sleep = min(sleep * 1.5, 1e-3)
+                if spins % 4096 == 0 and os.getppid() != self.ppid:
+                    raise RuntimeError("TP control channel: the parent process is gone; leaving")
         slot = self.slots[self.next & 1]
         h = slot[: _HDR * 8].view(np.int64).copy()
         n = int(h[1])
@@ -402,12 +411,96 @@ def tp_knn_search(engine, shard, queries: torch.Tensor, k: int):
     queries over the control channel, search this rank's shard, gather every rank's top-k over
     the CPU control group and merge with the HIP merge (stable (score desc, id asc) order:
     identical to one full scan).  The workers answer in order with their steps, so the exchange
-    never interleaves with the step collectives on the device."""
+    never interleaves with the step collectives on the device.  A served index searches from
+    HTTP threads while the engine thread steps: the engine lock keeps the control channel's
+    messages (one producer) and the control group's collectives in one order."""
     q = queries.to(shard.corpus.dtype)
     ctrl = getattr(engine, "tp_ctrl", None)
-    if ctrl is not None and ctrl.tp.size > 1:
-        ctrl.send("knn", (q.cpu(), k))
-    return shard.search(q.to(shard.corpus.device), k)
+    lock = getattr(engine, "lock", None)
+    with lock if lock is not None else _NoLock():
+        if ctrl is not None and ctrl.tp.size > 1:
+            ctrl.send("knn", (q.cpu(), k))
+        return shard.search(q.to(shard.corpus.device), k)
+
+
+class _NoLock:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _scatter_rows(ctrl, n: int, d: int, f32: bool, host: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Rows [lo, hi) of an n x d corpus to each rank of the control group (one gloo scatter of
+    equal padded slices from the leader; bf16 travels as int16 words).  Returns this rank's rows."""
+    from .sharded_index import shard_bounds
+
+    tp = ctrl.tp
+    per = (n + tp.size - 1) // tp.size
+    wire = torch.float32 if f32 else torch.int16
+    buf = torch.zeros((per, d), dtype=wire)
+    parts = None
+    if host is not None:
+        h = host.contiguous() if f32 else host.to(torch.bfloat16).contiguous().view(torch.int16)
+        parts = []
+        for r in range(tp.size):
+            lo, hi = shard_bounds(n, r, tp.size)
+            p = torch.zeros((per, d), dtype=wire)
+            p[: hi - lo] = h[lo:hi]
+            parts.append(p)
+    dist.scatter(buf, parts, src=ctrl.src, group=ctrl.group)
+    lo, hi = shard_bounds(n, tp.rank, tp.size)
+    rows = buf[: hi - lo]
+    return rows if f32 else rows.view(torch.bfloat16)
+
+
+def _shard_index(ctrl, rows: torch.Tensor, n: int, device):
+    from .sharded_index import ShardedKnnIndex, shard_bounds
+
+    lo, _ = shard_bounds(n, ctrl.tp.rank, ctrl.tp.size)
+    return ShardedKnnIndex(rows.to(device).contiguous(), lo, None, host_group=ctrl.group if ctrl.tp.size > 1 else None)
+
+
+def tp_shard_corpus(engine, corpus: torch.Tensor, device=None):
+    """Leader: distribute an n x d corpus over the TP group (each rank keeps rows
+    shard_bounds(n, rank, T); workers get a "shard" command, then their rows by one scatter)
+    and return the leader's ShardedKnnIndex (``tp_knn_search(engine, shard, ...)`` searches the
+    whole group).  bf16 on the GPU (the single-GPU index's dtype), f32 on the CPU."""
+    ctrl = engine.tp_ctrl
+    dev = torch.device(device) if device is not None else engine_device(engine)
+    f32 = dev.type != "cuda"
+    n, d = corpus.shape
+    host = corpus.detach().to("cpu", torch.float32 if f32 else torch.bfloat16)
+    lock = getattr(engine, "lock", None)
+    with lock if lock is not None else _NoLock():
+        ctrl.send("shard", (n, d, f32))
+        rows = _scatter_rows(ctrl, n, d, f32, host)
+    return _shard_index(ctrl, rows, n, dev)
+
+
+def engine_device(engine):
+    m = getattr(engine, "model", None)
+    return m.device if m is not None else getattr(engine, "device", torch.device("cpu"))
+
+
+class KnnGroup:
+    """Leader handle of a TP group that holds only corpus shards (``rag-app --tp T``: no
+    model; the workers run ``run_tp_worker(None, tp)``): ``tp_shard_corpus`` /
+    ``tp_knn_search`` accept it in place of an engine."""
+
+    def __init__(self, tp: TPGroup, device):
+        import threading
+
+        self.tp = tp
+        self.device = torch.device(device)
+        self.model = None
+        self.tp_ctrl = _Ctrl(tp)
+        self.lock = threading.Lock()
+
+    def shutdown(self):
+        with self.lock:
+            self.tp_ctrl.send("stop")
 
 
 def tp_barrier(engine):
@@ -422,13 +515,20 @@ def tp_barrier(engine):
 
 
 @torch.inference_mode()
-def run_tp_worker(model, tp: TPGroup, knn=None, **runner_kw):
+def run_tp_worker(model, tp: TPGroup, knn=None, device=None, **runner_kw):
     """Ranks > 0: execute whatever rank 0 schedules until it says stop (``knn``: this rank's
-    ShardedKnnIndex, answering the leader's sharded searches)."""
+    ShardedKnnIndex, answering the leader's sharded searches; a "shard" command replaces it with
+    rows the leader scatters).  ``model=None``: a kNN-only rank (the leader is a KnnGroup)."""
     from ..utils.watchdog import StepWatchdog
 
     stall_s = float(runner_kw.pop("stall_s", 600.0)) if "stall_s" in runner_kw else 600.0
-    runner, ctrl = make_tp_runner(model, tp, **runner_kw)
+    if model is not None:
+        runner, ctrl = make_tp_runner(model, tp, **runner_kw)
+        device = model.device
+    else:
+        runner, ctrl = None, _Ctrl(tp)
+        device = torch.device(device) if device is not None else torch.device("cpu")
+    on_gpu = torch.cuda.is_available() and device.type == "cuda"
     wd = StepWatchdog(f"tp-worker-{tp.rank}", stall_s=stall_s)
     n = 0
     pending: list = []
@@ -439,12 +539,17 @@ def run_tp_worker(model, tp: TPGroup, knn=None, **runner_kw):
             for ev in pending:
                 ev.synchronize()
             break
+        if cmd in ("capture", "step") and runner is None:
+            raise RuntimeError(f"kNN-only TP worker got a {cmd!r} command")
         if cmd == "capture":
             runner.capture(*arg)
         elif cmd == "barrier":
-            if torch.cuda.is_available() and model.device.type == "cuda":
+            if on_gpu:
                 torch.cuda.synchronize()
             dist.barrier()
+        elif cmd == "shard":
+            rows, d, f32 = arg
+            knn = _shard_index(ctrl, _scatter_rows(ctrl, rows, d, f32), rows, device)
         elif cmd == "knn":
             if knn is None:
                 raise RuntimeError("TP worker got a sharded kNN search but holds no corpus shard")
@@ -453,7 +558,7 @@ def run_tp_worker(model, tp: TPGroup, knn=None, **runner_kw):
         elif cmd == "step":
             with wd.busy():  # a step that never returns (dead peer in an all-reduce) is a stall
                 runner.execute(arg)
-                if torch.cuda.is_available() and model.device.type == "cuda":
+                if on_gpu:
                     # keep <= 2 steps in flight (the driver pipelines: step N+1's inputs
                     # arrive before step N is done, so the device never idles waiting here)
                     ev = torch.cuda.Event()

@@ -145,6 +145,8 @@ class RagIndex:
         return self._mat
 
     def _use_gpu(self) -> bool:
+        if getattr(self, "_sharded", None) is not None:
+            return True
         if self.backend == "gpu":
             return True
         if self.backend == "exact":
@@ -164,8 +166,11 @@ class RagIndex:
     def set_sharded(self, search_fn):
         """Route searches through a corpus-sharded kNN: ``search_fn(queries [nq, D] bf16, k) ->
         (scores f32 [nq, k], ids int32 [nq, k])`` (parallel.tp_engine.tp_knn_search: every TP
-        rank scans its shard, merged in the single-scan order).  None restores the local scan."""
+        rank scans its shard, merged in the single-scan order).  None restores the local scan.
+        With a sharded search this process keeps no device copy of the corpus."""
         self._sharded = search_fn
+        if search_fn is not None:
+            self._gpu = None
 
     def search_vectors_async(self, q: np.ndarray | torch.Tensor, top_k: int) -> "PendingSearch":
         """Launch a batched search without blocking the host: on the GPU the kNN kernel and
@@ -177,14 +182,16 @@ class RagIndex:
         n = len(self.chunks)
         if n == 0 or not self._use_gpu():
             return PendingSearch(done=self.search_vectors(q, top_k) if n else [[] for _ in range(len(q))])
-        corpus, norms = self.gpu_tensors()
         qt = torch.as_tensor(q)
-        # host queries are cast on the host (a few KB) and copied once: no device cast kernel
-        qt = (qt.to(torch.bfloat16).to(self.device) if qt.device.type == "cpu"
-              else qt.to(self.device, torch.bfloat16)).reshape(-1, corpus.shape[1]).contiguous()
-        if getattr(self, "_sharded", None) is not None:
-            s, i = self._sharded(qt, min(k, 64))
+        sharded = getattr(self, "_sharded", None)
+        if sharded is not None:
+            # the shard's dtype (bf16 on the GPU, f32 on the CPU) is applied by the search
+            s, i = sharded(qt.reshape(-1, qt.shape[-1]), min(k, 64))
         else:
+            corpus, norms = self.gpu_tensors()
+            # host queries are cast on the host (a few KB) and copied once: no device cast kernel
+            qt = (qt.to(torch.bfloat16).to(self.device) if qt.device.type == "cpu"
+                  else qt.to(self.device, torch.bfloat16)).reshape(-1, corpus.shape[1]).contiguous()
             qn = ops.row_norms(qt) if qt.is_cuda else qt.float().norm(dim=-1)
             s, i = ops.knn_topk(corpus, norms, qt, qn, min(k, 64))
         if not s.is_cuda:

@@ -153,6 +153,12 @@ class _Conn:
             pass
 
 
+def _tp_size(engine) -> int:
+    """Ranks of the engine's tensor-parallel group (1: a single-GPU engine)."""
+    ctrl = getattr(engine, "tp_ctrl", None)
+    return int(ctrl.tp.size) if ctrl is not None else 1
+
+
 class EngineCore:
     """Serve ``manager``'s engines (loaded in this process, on its GPU) to front-end
     processes over a Unix socket at ``path``."""
@@ -194,7 +200,7 @@ class EngineCore:
     def _meta(self, h) -> dict:
         return {"name": h.name, "preset": h.preset, "max_model_len": h.engine.max_model_len,
                 "eos_ids": sorted(int(t) for t in h.engine.eos_ids), "chat_style": h.chat_style,
-                "load_s": h.load_s, "vocab_size": int(h.engine.model.cfg.vocab_size)}
+                "load_s": h.load_s, "vocab_size": int(h.engine.model.cfg.vocab_size), "tp": _tp_size(h.engine)}
 
     def dispatch(self, conn: _Conn, msg):
         op = msg[0]

@@ -63,6 +63,14 @@ def _chat_to_prompt(messages: list) -> tuple[Optional[str], str]:
     return ("\n".join(sys_parts) if sys_parts else None), prompt
 
 
+def _tp_of(h) -> int:
+    """Tensor-parallel ranks behind a generator handle (local engine or remote core)."""
+    if hasattr(h, "tp"):
+        return int(h.tp)
+    ctrl = getattr(getattr(h, "engine", None), "tp_ctrl", None)
+    return int(ctrl.tp.size) if ctrl is not None else 1
+
+
 def create_app(manager: Optional[ModelManager] = None, cfg=None):
     from .batcher import MicroBatcher
 
@@ -354,7 +362,7 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
     async def health():
         """Engine health (watchdog): 503 while a loaded generator's step loop is stalled."""
         eng = {n: {"healthy": h.async_engine.healthy, "steps": h.async_engine.watchdog.steps,
-                   "stalls": h.async_engine.watchdog.stalls} for n, h in list(mgr.generators.items())}
+                   "stalls": h.async_engine.watchdog.stalls, "tp": _tp_of(h)} for n, h in list(mgr.generators.items())}
         ok = all(v["healthy"] for v in eng.values())
         return JSONResponse({"status": "ok" if ok else "degraded", "generators": eng}, status_code=200 if ok else 503)
 

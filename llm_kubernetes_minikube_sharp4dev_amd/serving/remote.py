@@ -240,6 +240,7 @@ class RemoteGeneratorHandle:
     chat_style: str
     loaded_at: float = field(default_factory=time.time)
     load_s: float = 0.0
+    tp: int = 1  # ranks of the cores' tensor-parallel groups (serve --tp)
 
 
 class _RemoteEmbed:
@@ -325,7 +326,8 @@ class RemoteModelManager(ModelManager):
             ck = self.checkpoints.get(name) or self.checkpoints.get(preset)
             h = RemoteGeneratorHandle(name, preset, _EngineView(meta["max_model_len"], set(meta["eos_ids"])),
                                       _RemoteAsync(self.pool, name, self.cfg.agent.request_timeout_s),
-                                      load_tokenizer(ck), meta["chat_style"], load_s=meta["load_s"])
+                                      load_tokenizer(ck), meta["chat_style"], load_s=meta["load_s"],
+                                      tp=int(meta.get("tp", 1)))
             self.generators[name] = h
             return h
 

@@ -19,7 +19,7 @@ BY_GRID = os.environ.get("SUMMARY_BY_GRID") == "1"
 # coarse classes for the budget table (first match wins)
 CLASSES = [
     ("decode GEMM (wsgemm / skinny, weight streaming)", ("wsgemm", "skinny", "ws_linear")),
-    ("prefill GEMM (gemm_kernel, MFMA 256x256/192)", ("gemm_kernel",)),
+    ("prefill GEMM (gemm_kernel / gemm1w, MFMA)", ("gemm_kernel", "gemm1w", "reduce1w")),
     ("hipBLASLt / rocBLAS", ("Cijk", "rocblas")),
     ("flash prefill + cascade", ("flash_prefill",)),
     ("paged decode attention", ("paged_decode", "decode_reduce", "split_reduce")),
@@ -47,7 +47,7 @@ def window(rows, window_s):
     return end - window_s * 1e9, end, f"last {window_s:.1f} s of the trace (no window markers)"
 
 
-def main(path, window_s, top=25):
+def main(path, window_s, top=int(os.environ.get("SUMMARY_TOP", "25"))):
     rows = list(csv.DictReader(open(path)))
     t0, t1, how = window(rows, window_s)
     window_s = (t1 - t0) / 1e9

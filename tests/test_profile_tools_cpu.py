@@ -49,7 +49,7 @@ def test_summarize_trace_window_and_foreign_kernels(tmp_path):
     assert "between the lk_window_mark kernels" in out
     assert "warmup_kernel" not in out and "drain_kernel" not in out
     assert "4 kernels" in out
-    assert "| prefill GEMM (gemm_kernel, MFMA 256x256/192) | 0.5 |" in out
+    assert "| prefill GEMM (gemm_kernel / gemm1w, MFMA) | 0.5 |" in out
     # the 180 us gap is itemised with the kernels on either side
     assert "| 180 |" in out
     # kernels outside the HIP library: the eager PyTorch op and the runtime copy, not ours
