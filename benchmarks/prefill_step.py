@@ -32,18 +32,29 @@ def child(a):
 
     torch.cuda.set_device(0)
     m = build_decoder(a.model, device="cuda", seed=0)
-    eng = LLMEngine(m, None, max_model_len=8192, max_num_seqs=64, max_num_batched_tokens=a.seqs * a.len,
-                    enable_prefix_caching=False, use_graphs=False, kv_cache_gb=16, eos_ids=set())
+    M = a.seqs * a.len
+    eng = LLMEngine(m, None, max_model_len=8192, max_num_seqs=a.decode_rows + a.seqs + 8,
+                    max_num_batched_tokens=M + a.decode_rows, enable_prefix_caching=False, use_graphs=False,
+                    kv_cache_gb=32, eos_ids=set(), token_align=1)
     eng.step_trace = []
     g = torch.Generator().manual_seed(1)
     gpu = []
+    # --decode-rows R: R long-running requests (context --ctx) decode in every measured step beside
+    # the new prompts' prefill, as in the serving bench's mixed steps
+    for _ in range(a.decode_rows):
+        eng.add_request(torch.randint(10, 120000, (a.ctx,), generator=g).tolist(),
+                        SamplingParams.greedy(8000 - a.ctx, ignore_eos=True))
+    while any(s.num_computed < len(s.prompt_ids) for s in eng.scheduler.running) or eng.scheduler.waiting:
+        eng.step()
+    eng.step_trace.clear()
     for it in range(a.warmup + a.iters):
         for _ in range(a.seqs):
             eng.add_request(torch.randint(10, 120000, (a.len,), generator=g).tolist(), SamplingParams.greedy(1))
-        while eng.has_work():
+        eng.step()  # the new prompts' prefill (+ one decode row per running request)
+        while a.decode_rows == 0 and eng.has_work():
             eng.step()
         if it >= a.warmup:
-            gpu += [t[7] for t in eng.step_trace if t[0] == a.seqs * a.len]
+            gpu += [t[7] for t in eng.step_trace if t[0] == M]
         eng.step_trace.clear()
     late = gpu[len(gpu) * 2 // 3:]  # the last third: after seconds of sustained load
     print(json.dumps({"median_ms": round(statistics.median(gpu) * 1e3, 3), "min_ms": round(min(gpu) * 1e3, 3),
@@ -59,6 +70,8 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--decode-rows", type=int, default=0)
+    ap.add_argument("--ctx", type=int, default=900)
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
     if a.child:
@@ -73,7 +86,8 @@ def main():
             t0 = time.time()
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--model", a.model,
                                   "--seqs", str(a.seqs), "--len", str(a.len), "--iters", str(a.iters),
-                                  "--warmup", str(a.warmup)], env=dict(os.environ, **env), capture_output=True,
+                                  "--warmup", str(a.warmup), "--decode-rows", str(a.decode_rows), "--ctx", str(a.ctx)],
+                                 env=dict(os.environ, **env), capture_output=True,
                                  text=True, timeout=600)
             if out.returncode != 0:
                 print(out.stdout[-2000:], out.stderr[-4000:], flush=True)
