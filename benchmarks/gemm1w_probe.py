@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--ms", default="4096,8192")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--group", type=int, default=4)
+    ap.add_argument("--bm", type=int, default=256, help="row tile of the probed kernel (256 / 192 / 128)")
     ap.add_argument("--no-cur", action="store_true", help="skip the gemm.hip arm")
     ap.add_argument("--shapes", default="")
     ap.add_argument("--extra", default="", help="extra shapes name:N:K[:swiglu],...")
@@ -40,7 +41,8 @@ def main():
         fn = so.lk_gemm1w_c
         fn.restype = ctypes.c_int
         fn.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                       ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_int]
+                       ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_int,
+                       ctypes.c_int]
         name = os.path.basename(path).replace("libgemm1w", "new").replace(".so", "") + (f"g{grp}" if grp else "")
         fns[name] = (fn, int(grp) if grp else a.group)
     ops = None
@@ -53,7 +55,7 @@ def main():
     def new(x, w, out, epi, arm=None):
         fn, grp = fns[arm or next(iter(fns))]
         rc = fn(x.data_ptr(), x.stride(0), w.data_ptr(), None, x.shape[0], w.shape[0], x.shape[1], epi,
-                out.data_ptr(), out.stride(0), stream, grp)
+                out.data_ptr(), out.stride(0), stream, grp, a.bm)
         assert rc == 0, rc
         return out
 

@@ -28,13 +28,14 @@ def main():
     fn = so.lk_gemm1w_c
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                   ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_int]
+                   ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_int,
+                   ctypes.c_int]
     x = torch.randn(a.M, a.K, device="cuda", dtype=torch.bfloat16)
     w = torch.randn(a.N, a.K, device="cuda", dtype=torch.bfloat16) * 0.02
     out = torch.empty(a.M, a.N, device="cuda", dtype=torch.bfloat16)
     st = torch.cuda.current_stream().cuda_stream
     for _ in range(400):  # ~2 s of back-to-back launches: clocks settle
-        assert fn(x.data_ptr(), a.K, w.data_ptr(), None, a.M, a.N, a.K, 0, out.data_ptr(), a.N, st, 4) == 0
+        assert fn(x.data_ptr(), a.K, w.data_ptr(), None, a.M, a.N, a.K, 0, out.data_ptr(), a.N, st, 4, 256) == 0
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * (256 * 4 * 8))()
     assert so.lk_gemm1w_stamps(buf) == 0

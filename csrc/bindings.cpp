@@ -24,9 +24,10 @@ inline bf16_t* bpo(const c10::optional<at::Tensor>& t) { return t ? bp(*t) : nul
 inline const int* ip(const at::Tensor& t) { return t.data_ptr<int>(); }
 inline const int* ipo(const c10::optional<at::Tensor>& t) { return t ? ip(*t) : nullptr; }
 
-// shape support of the prefill GEMM for a schedule variant (3: gemm1w.hip, 256-wide tiles)
+// shape support of the prefill GEMM for a schedule variant (3 / 4 / 5: gemm1w.hip, 256-wide column
+// tiles, 256 / 192 / 128-row tiles)
 bool gemm_shape_ok(int M, int N, int K, int epi, int bn, int splits, int variant) {
-  if (variant == 3) return bn == 256 && lk_gemm1w_supported(M, N, K, epi, splits) != 0;
+  if (lk_gemm1w_bm(variant)) return bn == 256 && lk_gemm1w_supported(M, N, K, epi, splits, lk_gemm1w_bm(variant)) != 0;
   return lk_gemm_supported(M, N, K, epi, bn, splits) != 0;
 }
 

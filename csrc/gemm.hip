@@ -1064,9 +1064,9 @@ int lk_gemm_supported(int M, int N, int K, int epi, int bn, int ks) {
 // 8-B aligned output rows; any M >= 1.
 int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi, int bn,
             int variant, bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, const LkEpi* ea_) {
-  if (variant == 3) {  // the one-wave-per-SIMD kernel (csrc/gemm1w.hip): 256-wide tiles only
+  if (lk_gemm1w_bm(variant)) {  // the one-wave-per-SIMD kernel (csrc/gemm1w.hip): 256-wide column tiles
     if (bn != 256) return -1;
-    return lk_gemm1w(x, ldx, w, bias, M, N, K, epi, out, ldo, st, ks, ws, ea_, 0);
+    return lk_gemm1w(x, ldx, w, bias, M, N, K, epi, out, ldo, st, ks, ws, ea_, 0, lk_gemm1w_bm(variant));
   }
   LkEpi ea = ea_ ? *ea_ : LkEpi{};
   // fused-chain epilogue arguments (checked here: a bad pointer / shape would fault the device)

@@ -3,14 +3,15 @@
 // The 256 x 256-tile schedule of hipBLASLt's gfx950 bf16 kernels
 // (Cijk_..._MT256x256x64_MI16x16x1_..._DTLA1_DTLB1_PGR2_PLR1_..._WG32_8_1: its K loop read from
 // the disassembly of the installed library), rebuilt in HIP for our K-contiguous operands and
-// extended with the fused serving epilogues of gemm.hip:
-//   * 256 threads = 4 waves, ONE per SIMD, as 2 (M) x 2 (N); each wave owns 128 x 128 outputs =
-//     8 x 8 v_mfma_f32_16x16x32_bf16 accumulators (256 floats per lane) pinned to AGPRs by
+// extended with the fused serving epilogues of gemm.hip and with 192 / 128-row tiles:
+//   * 256 threads = 4 waves, ONE per SIMD, as 2 (M) x 2 (N); each wave owns (BM / 2) x 128 outputs =
+//     MB x 8 v_mfma_f32_16x16x32_bf16 accumulators (MB = BM / 32: 8 / 6 / 4) pinned to AGPRs by
 //     inline-asm MFMAs ("+a"); the first K-tile's MFMAs take an inline 0 as C (no zeroing pass);
-//   * BK = 64, two LDS stages of 64 KB (X rows | W rows, 128-B rows, (row >> 1) & 7 chunk XOR
+//   * BK = 64, two LDS stages of (BM + 256) x 128 B (X rows | W rows, (row >> 1) & 7 chunk XOR
 //     applied on the DMA SOURCE: lane-linear LDS image, conflict-free ds_read_b128);
-//   * a full K-tile of fragments lives in registers (kk 0 and kk 1 sets, 128 VGPRs); every LDS
-//     read, LDS-DMA issue and wait is inline asm placed by hand among the 128 MFMAs of a K-tile:
+//   * a full K-tile of fragments lives in registers (kk 0 and kk 1 sets); every LDS read, LDS-DMA
+//     issue and wait is inline asm placed by hand among the NM = 16 MB MFMAs of a K-tile (BM 256:
+//     positions below; 192 / 128: Tile<BM>):
 //       top          : lgkmcnt(0) -- the (t, kk 0) fragments read at the end of K-tile t-1
 //       MFMA  0..15  : the 16 fragment reads of (t, kk 1), one per MFMA
 //       MFMA 26      : lgkmcnt(0) + s_barrier -- every wave is done with stage t & 1
@@ -20,6 +21,9 @@
 //       MFMA 108..123: the 16 fragment reads of (t+1, kk 0)
 //     (probe sweeps of these positions, the wait placement and the M0 lag:
 //     benchmarks/gemm1w_probe.py, profiles/r5_gemm1w/);
+//   * row tiles of 192 / 128 fill the 256 CUs where 256-row tiles leave most of a wave idle (the
+//     serving bench's mixed steps: M = prefill chunk + ~105 decode rows); the dispatch picks the
+//     row tile per M bucket from measurements (ops.tune_gemm, benchmarks/gemm_tiles.py);
 //   * one tile per workgroup: the hardware starts the next workgroup on a CU while the finished
 //     one's epilogue stores drain (a persistent walk with the next tile's first K-tiles DMA'd
 //     during the last one measured 1-3 % slower);
@@ -42,17 +46,31 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
 
-constexpr int kBM = 256, kBN = 256, kBK = 64;
+constexpr int kBN = 256, kBK = 64;
 constexpr int kRowB = kBK * 2;          // 128-B LDS rows
-constexpr int kOp = 256 * kRowB;        // 32 KB: one operand of one stage
-constexpr int kStage = 2 * kOp;         // X rows then W rows
-constexpr int kLdsStages = 2 * kStage;  // 128 KB
 constexpr int kLdsEpi = 8192;           // epilogue scratch above the stages (row scales, RESID sums)
-constexpr int kLds = kLdsStages + kLdsEpi;
 
-// K-loop schedule: MFMA indices within the 128 of a K-tile
-constexpr int kB1 = 26, kD0 = 28, kDS = 5, kB2 = 108, kLag = 2;
-static_assert(15 < kB1 && kB1 < kD0 && kD0 + kDS * 15 + kLag < kB2 && kB2 + 16 <= 128, "schedule");
+// Row-tile height BM (256, 192 or 128; the column tile is always 256): the 4 waves sit 2 (M) x 2 (N),
+// each owning (BM / 2) x 128 outputs = MB x 8 accumulators of 16 x 16.  A K-tile is NM = 16 MB
+// MFMAs, NR = MB + 8 fragment reads per kk set and NP = BM / 32 + 8 LDS-DMA pieces per wave.
+// Smaller row tiles fill the 256 CUs where 256-row tiles leave most of a wave idle (M 2664,
+// N 4096: 176 tiles of 256 rows, 224 of 192 rows -- the row tile hipBLASLt picks there).
+template <int BM>
+struct Tile {
+  static constexpr int MB = BM / 32, NM = 16 * MB, NR = MB + 8, PX = BM / 32, NP = PX + 8;
+  static constexpr int kOpX = BM * kRowB;                // X rows of one stage
+  static constexpr int kStage = kOpX + 256 * kRowB;      // X rows then W rows
+  static constexpr int kLdsStages = 2 * kStage;          // 128 / 112 / 96 KB
+  static constexpr int kLds = kLdsStages + kLdsEpi;
+  // K-loop schedule (MFMA indices within the NM of a K-tile): barrier 1, first DMA piece, DMA
+  // spacing, M0 lag, barrier 2
+  static constexpr int B1 = BM == 256 ? 26 : BM == 192 ? 24 : 14;
+  static constexpr int D0 = B1 + 2;
+  static constexpr int DS = BM == 256 ? 5 : BM == 192 ? 4 : 2;
+  static constexpr int LAG = BM == 128 ? 1 : 2;
+  static constexpr int B2 = BM == 256 ? 108 : BM == 192 ? 82 : 48;
+  static_assert(NR - 1 < B1 && B1 < D0 && LAG < DS && D0 + DS * (NP - 1) + LAG < B2 && B2 + NR <= NM, "schedule");
+};
 
 enum { E_NONE = 0, E_SWIGLU = 1, E_BIAS = 2, E_BIAS_GELU = 3, E_BIAS_RELU = 4, E_PARTIAL = 5, E_RESID = 6,
        E_QKV = 7 };
@@ -100,7 +118,7 @@ LK_DEVICE u32x4_t srd(const void* p, long bytes) {  // buffer descriptor words, 
 
 // SCP: partial-sum planes of the folded-RMSNorm row scale loaded per row (0: no row scale; 16 covers
 // a 4096-wide producer, 32 an 8192-wide one)
-template <int EPI, int SCP>
+template <int EPI, int SCP, int BM>
 __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict__ X, long ldx,
                                                         const bf16_t* __restrict__ W,
                                                         const bf16_t* __restrict__ bias, int M, int K, int I,
@@ -108,6 +126,9 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
                                                         int group_m, LkEpi ea) {
   constexpr bool SC = SCP > 0;
   static_assert(!SC || scalable(EPI), "row scale");
+  using TL = Tile<BM>;
+  constexpr int MB = TL::MB, NM = TL::NM, NR = TL::NR, PX = TL::PX, NP = TL::NP, WM = BM / 2;
+  constexpr int kOpX = TL::kOpX, kStage = TL::kStage, kLdsStages = TL::kLdsStages;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -129,39 +150,40 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
   const u32x4_t xsrd = srd(X, (long)M * ldx * 2);
   const u32x4_t wsrd = srd(W, (long)(EPI == E_SWIGLU ? 2 * I : TN * kBN) * K * 2);
   const unsigned lds0 = static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_ptr_t)smem));
-  const unsigned ldsw = rfl(lds0 + 64 * w * kRowB);
+  const unsigned ldsx = rfl(lds0 + (BM / 4) * w * kRowB), ldsw = rfl(lds0 + kOpX + 64 * w * kRowB);
 
-  // ---- LDS-DMA piece i (0..15) of a K-tile: rows 64 w + 8 (i & 7) + (lane >> 3) of X (i < 8) or
-  // W (i >= 8), 16-B chunk lane & 7 (source chunk swizzled); per-lane row offsets of the tile
+  // ---- LDS-DMA piece i (0..NP-1) of a K-tile: rows BM/4 w + 8 i + (lane >> 3) of X (i < PX) or
+  // 64 w + 8 (i - PX) + (lane >> 3) of W, 16-B chunk lane & 7 (source chunk swizzled); per-lane
+  // row offsets of the tile
   const int lr8 = lane >> 3, lc8 = lane & 7;
-  unsigned xo[8], wo[8];
+  unsigned xo[PX], wo[8];
   // (32-bit: the host keeps every operand under 2^31 bytes).  Closed forms with the piece index
   // i in immediates only -- per-i lane constants held across the tile loop spill:
-  //   row = 64 w + 8 i + lr8;  swz(row) = (lr8 >> 1) ^ 4 (i & 1);
+  //   row = BM/4 w + 8 i + lr8;  swz(row) = (lr8 >> 1) ^ 4 (i & 1)  (BM/8 w is a multiple of 8);
   //   W row = lane part + 32 (i >> 2) + 16 (i & 1) + 4 ((i >> 1) & 1)   (pair_col of row & 31)
   const unsigned ldxb = (unsigned)ldx * 2, kb = (unsigned)K * 2;
   const unsigned ch0 = (unsigned)((lc8 ^ (lr8 >> 1)) << 4);
   auto offsets = [&](int tm, int tn) {
-    const unsigned xb = (unsigned)(tm * kBM + 64 * w + lr8) * ldxb;
+    const unsigned xb = (unsigned)(tm * BM + (BM / 4) * w + lr8) * ldxb;
     const int lanew = 8 * (lr8 >> 2) + (lr8 & 3);
     const unsigned wl = EPI == E_SWIGLU ? (unsigned)((w & 1) * I + tn * 128 + (w >> 1) * 64 + lanew)
                                         : (unsigned)(tn * kBN + 64 * w + lanew);
     const unsigned wb = wl * kb;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const unsigned ch = ch0 ^ (unsigned)((i & 1) << 6);
-      xo[i] = xb + (unsigned)(8 * i) * ldxb + ch;
-      wo[i] = wb + (unsigned)(32 * (i >> 2) + 16 * (i & 1) + 4 * ((i >> 1) & 1)) * kb + ch;
-    }
+    for (int i = 0; i < PX; ++i) xo[i] = xb + (unsigned)(8 * i) * ldxb + (ch0 ^ (unsigned)((i & 1) << 6));
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      wo[i] = wb + (unsigned)(32 * (i >> 2) + 16 * (i & 1) + 4 * ((i >> 1) & 1)) * kb + (ch0 ^ (unsigned)((i & 1) << 6));
   };
   auto piece_m0 = [&](int t, int i) -> unsigned {  // LDS base of piece i of (tile-relative) K-tile t
-    return ldsw + (unsigned)((t & 1) * kStage + (i < 8 ? 0 : kOp) + 8 * (i & 7) * kRowB);
+    return i < PX ? ldsx + (unsigned)((t & 1) * kStage + 8 * i * kRowB)
+                  : ldsw + (unsigned)((t & 1) * kStage + 8 * (i - PX) * kRowB);
   };
   // issue piece i of K-tile t (M0 already holds its LDS base)
   auto dma = [&](int t, int i) {
     const unsigned so = rfl((unsigned)(kt0 + t) * (kBK * 2));
-    if (i < 8) asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(xo[i & 7]), "s"(xsrd), "s"(so) : "memory");
-    else asm volatile("buffer_load_dwordx4 %0, %1, %2 offen sc0 sc1 lds" ::"v"(wo[i & 7]), "s"(wsrd), "s"(so) : "memory");
+    if (i < PX) asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(xo[i]), "s"(xsrd), "s"(so) : "memory");
+    else asm volatile("buffer_load_dwordx4 %0, %1, %2 offen sc0 sc1 lds" ::"v"(wo[i - PX]), "s"(wsrd), "s"(so) : "memory");
   };
 
   // ---- fragments: lane reads stage row (16-row base + r), 16-B chunk 4 kk + g, from per-(kk,
@@ -171,21 +193,21 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
     const unsigned b = lds0 + (((4 * kk + g) ^ rs) << 4) + r * kRowB;
-    bx[kk] = b + wr * 128 * kRowB;
-    bw[kk] = b + kOp + wc * 128 * kRowB;
+    bx[kk] = b + wr * WM * kRowB;
+    bw[kk] = b + kOpX + wc * 128 * kRowB;
   }
-  short8 fx0[8], fw0[8], fx1[8], fw1[8];
-  // read j in the consumption order of the MFMA loop: fw[0], fx[0..7], fw[1..7]
-  auto rd = [](unsigned bxv, unsigned bwv, auto j_t, short8(&fx)[8], short8(&fw)[8]) {
+  short8 fx0[MB], fw0[8], fx1[MB], fw1[8];
+  // read j in the consumption order of the MFMA loop: fw[0], fx[0..MB-1], fw[1..7]
+  auto rd = [](unsigned bxv, unsigned bwv, auto j_t, short8(&fx)[MB], short8(&fw)[8]) {
     constexpr int j = decltype(j_t)::value;
     if constexpr (j == 0)
       asm volatile("ds_read_b128 %0, %1" : "=v"(fw[0]) : "v"(bwv));
-    else if constexpr (j <= 8)
+    else if constexpr (j <= MB)
       asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fx[j - 1]) : "v"(bxv), "i"((j - 1) * 16 * kRowB));
     else
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fw[j - 8]) : "v"(bwv), "i"((j - 8) * 16 * kRowB));
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fw[j - MB]) : "v"(bwv), "i"((j - MB) * 16 * kRowB));
   };
-  floatx4 acc[8][8];
+  floatx4 acc[MB][8];
   using T = std::true_type;
   using F = std::false_type;
 
@@ -199,47 +221,48 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
   auto ss_issue = [&](int tm_) {
     if constexpr (SC) {
       const u32x4_t s = srd(ea.ss_in, (long)ea.ss_nt * ea.ss_ld * 4);
-      const unsigned base = (unsigned)((tm_ * kBM + tid) * 4);
+      const unsigned base = (unsigned)((tm_ * BM + tid) * 4);
 #pragma unroll
       for (int p = 0; p < SCP; ++p)  // planes >= ss_nt read past the range: 0
         asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(ssp[p]) : "v"(base), "s"(s), "s"(rfl((unsigned)(p * ea.ss_ld * 4))) : "memory");
     }
   };
 
-  // K-tile t: 128 MFMAs (kk 0 set: n-major 0..63, kk 1 set: 64..127) with the reads / DMA /
-  // barriers of the file comment.  FIRST: C = 0.  DMA: K-tile t+2 exists.  NXT: K-tile t+1
+  // K-tile t: NM MFMAs (kk 0 set: n-major 0..NM/2-1, kk 1 set: the rest) with the reads / DMA /
+  // barriers of the file comment (positions: Tile<BM>).  FIRST: C = 0.  DMA: K-tile t+2 exists.  NXT: K-tile t+1
   // exists.  LAST: the final K-tile.
   auto ktile = [&](auto first_t, auto dma_t, auto nxt_t, int t) {
     constexpr bool FIRST = decltype(first_t)::value, DMA = decltype(dma_t)::value;
     constexpr bool NXT = decltype(nxt_t)::value;
     const unsigned so = (unsigned)(t & 1) * kStage, sn = (unsigned)kStage - so;  // this / next stage
-    unroll<128>([&](auto i_t) {
+    unroll<NM>([&](auto i_t) {
       constexpr int i = decltype(i_t)::value;
+      constexpr int B1 = TL::B1, D0 = TL::D0, DS = TL::DS, LAG = TL::LAG, B2 = TL::B2;
       if constexpr (i == 0) lgkm0();
-      if constexpr (i < 16) rd(bx[1] + so, bw[1] + so, std::integral_constant<int, i>{}, fx1, fw1);
-      if constexpr (i == kB1) {
+      if constexpr (i < NR) rd(bx[1] + so, bw[1] + so, std::integral_constant<int, i>{}, fx1, fw1);
+      if constexpr (i == B1) {
         lgkm0();
         barrier_raw();
       }
-      if constexpr (DMA && i >= kD0 && i < kD0 + kDS * 16 && (i - kD0) % kDS == 0) {
+      if constexpr (DMA && i >= D0 && i < D0 + DS * NP && (i - D0) % DS == 0) {
         fence();
-        dma(t + 2, (i - kD0) / kDS);
-        fence();
-      }
-      if constexpr (DMA && i >= kD0 + kLag && i < kD0 + kLag + kDS * 16 && (i - kD0 - kLag) % kDS == 0) {
-        constexpr int k = (i - kD0 - kLag) / kDS;
-        fence();
-        set_m0(k < 15 ? piece_m0(t + 2, k + 1) : piece_m0(t + 3, 0));
+        dma(t + 2, (i - D0) / DS);
         fence();
       }
-      if constexpr (NXT && i == kB2) {
-        if constexpr (DMA) wait_vm<16>();
+      if constexpr (DMA && i >= D0 + LAG && i < D0 + LAG + DS * NP && (i - D0 - LAG) % DS == 0) {
+        constexpr int k = (i - D0 - LAG) / DS;
+        fence();
+        set_m0(k < NP - 1 ? piece_m0(t + 2, k + 1) : piece_m0(t + 3, 0));
+        fence();
+      }
+      if constexpr (NXT && i == B2) {
+        if constexpr (DMA) wait_vm<NP>();
         else wait_vm<0>();
         barrier_raw();
       }
-      if constexpr (NXT && i >= kB2 && i < kB2 + 16)
-        rd(bx[0] + sn, bw[0] + sn, std::integral_constant<int, i - kB2>{}, fx0, fw0);
-      constexpr int kk = i >> 6, n = (i >> 3) & 7, m = i & 7;
+      if constexpr (NXT && i >= B2 && i < B2 + NR)
+        rd(bx[0] + sn, bw[0] + sn, std::integral_constant<int, i - B2>{}, fx0, fw0);
+      constexpr int kk = i / (NM / 2), n = (i % (NM / 2)) / MB, m = i % MB;
       if constexpr (kk == 0 && FIRST) mfma0(acc[m][n], fw0[n], fx0[m]);
       else if constexpr (kk == 0) mfma(acc[m][n], fw0[n], fx0[m]);
       else mfma(acc[m][n], fw1[n], fx1[m]);
@@ -256,19 +279,19 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
   ss_issue(tm);
   // prologue: K-tiles 0 and 1 (the row-scale loads are older: retired with K-tile 0)
 #pragma unroll
-  for (int q = 0; q < 32; ++q) {
-    set_m0(piece_m0(q >> 4, q & 15));
+  for (int q = 0; q < 2 * NP; ++q) {
+    set_m0(piece_m0(q / NP, q % NP));
     asm volatile("s_nop 0");
-    dma(q >> 4, q & 15);
+    dma(q / NP, q % NP);
   }
   set_m0(piece_m0(2, 0));
-  wait_vm<16>();
+  wait_vm<NP>();
   barrier_raw();
   if constexpr (SC) {
 #pragma unroll
     for (int p = 0; p < SCP; ++p) ssum += ssp[p];
   }
-  unroll<16>([&](auto j_t) { rd(bx[0], bw[0], j_t, fx0, fw0); });
+  unroll<NR>([&](auto j_t) { rd(bx[0], bw[0], j_t, fx0, fw0); });
   ktile(T{}, T{}, T{}, 0);
   int t = 1;
   for (; t + 2 < nk; ++t) ktile(F{}, T{}, T{}, t);
@@ -281,15 +304,15 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
     // lane holds row tm*256 + wr*128 + 16m + r; fragment pair (2p, 2p+1) the 8 consecutive
     // columns 32p + 8g .. +7 of the wave's 128 (SwiGLU: gate pairs 0, 1 and up pairs 2, 3 of
     // each 64-row half ... the wave's 64 output columns)
-    float scm[8];
+    float scm[MB];
 #pragma unroll
-    for (int m = 0; m < 8; ++m) scm[m] = 1.f;
+    for (int m = 0; m < MB; ++m) scm[m] = 1.f;
     if constexpr (SC) {
       scl[tid] = rsqrtf(ssum * ea.inv_h + ea.eps);
       lgkm0();
       barrier_raw();
 #pragma unroll
-      for (int m = 0; m < 8; ++m) scm[m] = scl[wr * 128 + m * 16 + r];
+      for (int m = 0; m < MB; ++m) scm[m] = scl[wr * WM + m * 16 + r];
     }
     auto pk8 = [](const float (&y)[8]) {
       return u32x4_t{pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3]), pack_bf2(y[4], y[5]), pack_bf2(y[6], y[7])};
@@ -298,8 +321,8 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
       float* part = reinterpret_cast<float*>(out) + (long)kz * M * ldo;
       const auto ps = __builtin_amdgcn_make_buffer_rsrc(part, 0, (int)min((long)M * ldo * 4, 0x7FFFFFF0L), 0x00020000);
 #pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const unsigned rb = (unsigned)(((long)tm * kBM + wr * 128 + m * 16 + r) * ldo + tn * kBN + wc * 128) * 4;
+      for (int m = 0; m < MB; ++m) {
+        const unsigned rb = (unsigned)(((long)tm * BM + wr * WM + m * 16 + r) * ldo + tn * kBN + wc * 128) * 4;
 #pragma unroll
         for (int n = 0; n < 8; ++n)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[m][n]), ps,
@@ -308,8 +331,8 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
     } else if constexpr (EPI == E_SWIGLU) {
       const auto os = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)min((long)M * ldo * 2, 0x7FFFFFF0L), 0x00020000);
 #pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const unsigned rb = (unsigned)(((long)tm * kBM + wr * 128 + m * 16 + r) * ldo + tn * 128 + wc * 64 + 8 * g) * 2;
+      for (int m = 0; m < MB; ++m) {
+        const unsigned rb = (unsigned)(((long)tm * BM + wr * WM + m * 16 + r) * ldo + tn * 128 + wc * 64 + 8 * g) * 2;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
           float y[8];
@@ -325,10 +348,10 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
       // r = bf16(r + bf16(acc)) in place, then the partial sum of squares of the new r over the
       // tile's 256 columns (lanes g, then the two wc waves through LDS) into ss_out[tn][row]
       const auto rrs = __builtin_amdgcn_make_buffer_rsrc(ea.resid, 0, (int)min((long)M * ea.ldr * 2, 0x7FFFFFF0L), 0x00020000);
-      float ssm[8];
+      float ssm[MB];
 #pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const long row = (long)tm * kBM + wr * 128 + m * 16 + r;
+      for (int m = 0; m < MB; ++m) {
+        const long row = (long)tm * BM + wr * WM + m * 16 + r;
         const unsigned rb = (unsigned)((row * ea.ldr + (long)tn * kBN + wc * 128 + 8 * g) * 2);
         u32x4_t rv[4];
 #pragma unroll
@@ -353,22 +376,22 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
         ss += __shfl_xor(ss, 32, 64);
         ssm[m] = ss;
       }
-      float* red = reinterpret_cast<float*>(smem + kLdsStages + 1024);  // [2 wc][256 tile rows]
+      float* red = reinterpret_cast<float*>(smem + kLdsStages + 1024);  // [2 wc][BM tile rows]
       if (g == 0) {
 #pragma unroll
-        for (int m = 0; m < 8; ++m) red[wc * 256 + wr * 128 + m * 16 + r] = ssm[m];
+        for (int m = 0; m < MB; ++m) red[wc * BM + wr * WM + m * 16 + r] = ssm[m];
       }
       lgkm0();
       barrier_raw();
-      const int row = tm * kBM + tid;
-      if (row < M) ea.ss_out[(long)tn * ea.ss_out_ld + row] = red[tid] + red[256 + tid];
+      const int row = tm * BM + tid;
+      if (tid < BM && row < M) ea.ss_out[(long)tn * ea.ss_out_ld + row] = red[tid] + red[BM + tid];
     } else if constexpr (EPI == E_QKV) {
       // RoPE (interleaved pairs) on the q / k heads + the paged-KV scatter, on the bf16-rounded
       // (row-scaled) projection: the values "GEMM -> rope_kv_" would leave
       const int qcols = ea.hq * ea.hd, kcols = ea.hkv * ea.hd, half = ea.hd >> 1;
 #pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const int row = tm * kBM + wr * 128 + m * 16 + r;
+      for (int m = 0; m < MB; ++m) {
+        const int row = tm * BM + wr * WM + m * 16 + r;
         if (row >= M) continue;
         const float sc = scm[m];
         const int pos = ea.pos[row];
@@ -433,8 +456,8 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
         return e;
       };
 #pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const unsigned rb = (unsigned)(((long)tm * kBM + wr * 128 + m * 16 + r) * ldo + tn * kBN + wc * 128 + 8 * g) * 2;
+      for (int m = 0; m < MB; ++m) {
+        const unsigned rb = (unsigned)(((long)tm * BM + wr * WM + m * 16 + r) * ldo + tn * kBN + wc * 128 + 8 * g) * 2;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
           float y[8];
@@ -503,34 +526,44 @@ int group1w() {  // row tiles per XCD group of the tile order (LK_GEMM_GROUP_M, 
   return g;
 }
 
-template <int EPI, int SCP>
+template <int EPI, int SCP, int BM>
 void launch1w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
-              long ldo, int TM, int TN, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
+              long ldo, int TN, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
+  constexpr int lds = Tile<BM>::kLds;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm1w_kernel<EPI, SCP>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm1w_kernel<EPI, SCP, BM>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  gemm1w_kernel<EPI, SCP><<<dim3(TM * TN, ks), 256, kLds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN,
-                                                            group_m > 0 ? group_m : group1w(), ea);
+  const int TM = (M + BM - 1) / BM;
+  gemm1w_kernel<EPI, SCP, BM><<<dim3(TM * TN, ks), 256, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN,
+                                                                 group_m > 0 ? group_m : group1w(), ea);
+}
+template <int EPI, int SCP>
+void launch1w_bm(int bm, const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I,
+                 bf16_t* out, long ldo, int TN, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
+  if (bm == 192) launch1w<EPI, SCP, 192>(x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
+  else if (bm == 128) launch1w<EPI, SCP, 128>(x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
+  else launch1w<EPI, SCP, 256>(x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
 }
 template <int EPI>
-void launch1w_sc(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
-                 long ldo, int TM, int TN, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
+void launch1w_sc(int bm, const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I,
+                 bf16_t* out, long ldo, int TN, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
   if constexpr (scalable(EPI)) {
     if (ea.ss_in != nullptr) {
-      if (ea.ss_nt <= 16) launch1w<EPI, 16>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, group_m, st, ea);
-      else launch1w<EPI, 32>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, group_m, st, ea);
+      if (ea.ss_nt <= 16) launch1w_bm<EPI, 16>(bm, x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
+      else launch1w_bm<EPI, 32>(bm, x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
       return;
     }
   }
-  launch1w<EPI, 0>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN, ks, group_m, st, ea);
+  launch1w_bm<EPI, 0>(bm, x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
 }
 
 }  // namespace
 
-int lk_gemm1w_supported(int M, int N, int K, int epi, int ks) {
+int lk_gemm1w_supported(int M, int N, int K, int epi, int ks, int bm) {
+  if (bm != 256 && bm != 192 && bm != 128) return 0;
   if (M < 1 || K % kBK || ks < 1 || ks > 8 || K / kBK < 3 * ks) return 0;  // >= 3 K-tiles per split
   if (ks > 1 && (epi == E_SWIGLU || epi == E_QKV || N % 256)) return 0;
   if (epi == E_SWIGLU) return N % 2 == 0 && (N / 2) % 128 == 0;
@@ -538,42 +571,41 @@ int lk_gemm1w_supported(int M, int N, int K, int epi, int ks) {
   return epi >= E_NONE && epi <= E_BIAS_RELU && N % kBN == 0;
 }
 
-// out = epi(X W^T (+ bias)): the contract of lk_gemm with a fixed 256 x 256 tile (ea: the fused
-// chain arguments, see kernels.h).  group_m <= 0: LK_GEMM_GROUP_M / 4.
+// out = epi(X W^T (+ bias)): the contract of lk_gemm with a bm x 256 tile, bm = 256 / 192 / 128
+// (ea: the fused chain arguments, see kernels.h).  group_m <= 0: LK_GEMM_GROUP_M / 4.
 int lk_gemm1w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi,
-              bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, const LkEpi* ea_, int group_m) {
+              bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, const LkEpi* ea_, int group_m, int bm) {
   LkEpi ea = ea_ ? *ea_ : LkEpi{};
   if (ea.ss_in && (ea.ss_nt < 1 || ea.ss_nt > 32 || ea.ss_ld < M || ea.inv_h <= 0.f || ks > 1)) return -1;
   if (epi == E_RESID && (!ea.resid || !ea.ss_out || ea.ldr % 8 || ea.ss_out_ld < M)) return -1;
   if (epi == E_QKV && (!ea.pos || !ea.cos_sin || ea.hd % 16 || ea.hd <= 0 || N != (ea.hq + 2 * ea.hkv) * ea.hd ||
                        ((ea.kc || ea.vc) && (!ea.slots || ea.bs < 1))))
     return -1;
-  if (!lk_gemm1w_supported(M, N, K, epi, ks) || ldx % 8 || ldo % 8 || reinterpret_cast<uintptr_t>(out) % 16 ||
+  if (!lk_gemm1w_supported(M, N, K, epi, ks, bm) || ldx % 8 || ldo % 8 || reinterpret_cast<uintptr_t>(out) % 16 ||
       (bias != nullptr && reinterpret_cast<uintptr_t>(bias) % 16))
     return -1;
   if (epi >= E_BIAS && epi <= E_BIAS_RELU && bias == nullptr) return -1;
   if ((long)N * K * 2 >= 0x7FFFFFF0L) return -1;
   // 32-bit buffer offsets: X, the output (fp32 partials for split-K) and the residual in row chunks
-  const int TMall = (M + kBM - 1) / kBM;
-  const long rows_pad = (long)TMall * kBM;
+  const int TMall = (M + bm - 1) / bm;
+  const long rows_pad = (long)TMall * bm;
   const long xb = rows_pad * ldx * 2, ob = rows_pad * ldo * (ks > 1 ? 4 * ks : 2), rb = epi == E_RESID ? rows_pad * ea.ldr * 2 : 0;
   if (xb >= 0x7FFFFFF0L || ob >= 0x7FFFFFF0L || rb >= 0x7FFFFFF0L) {
     if (ea_ || ks > 1) return -1;  // (the fused chain indexes whole-M side buffers)
     const long per = max(ldx, ldo) * 2;
-    const long max_rows = (0x7FFFFFF0L / per) / kBM * kBM - kBM;
-    if (max_rows < kBM) return -1;
+    const long max_rows = (0x7FFFFFF0L / per) / bm * bm - bm;
+    if (max_rows < bm) return -1;
     for (long m0 = 0; m0 < M; m0 += max_rows) {
       const int mc = (int)min((long)M - m0, max_rows);
       const int rc = lk_gemm1w(x + m0 * ldx, ldx, w, bias, mc, N, K, epi, out + m0 * ldo, ldo, st, 1, nullptr, nullptr,
-                               group_m);
+                               group_m, bm);
       if (rc) return rc;
     }
     return 0;
   }
-  const int TM = TMall;
   if (ks > 1) {  // fp32 partials of ks K-ranges into ws [ks, M, N], then the reduce applies the epilogue
     if (ws == nullptr) return -1;
-    launch1w_sc<E_PARTIAL>(x, ldx, w, nullptr, M, K, 0, reinterpret_cast<bf16_t*>(ws), N, TM, N / kBN, ks, group_m, st,
+    launch1w_sc<E_PARTIAL>(bm, x, ldx, w, nullptr, M, K, 0, reinterpret_cast<bf16_t*>(ws), N, N / kBN, ks, group_m, st,
                            ea);
     if (epi == E_RESID) {
       reduce1w_resid_kernel<<<dim3(N / 256, M), 64, 0, st>>>(ws, ks, M, N, ea);
@@ -592,13 +624,13 @@ int lk_gemm1w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, in
     return 0;
   }
   switch (epi) {
-    case E_NONE: launch1w_sc<E_NONE>(x, ldx, w, bias, M, K, 0, out, ldo, TM, N / kBN, 1, group_m, st, ea); break;
-    case E_SWIGLU: launch1w_sc<E_SWIGLU>(x, ldx, w, bias, M, K, N / 2, out, ldo, TM, N / 256, 1, group_m, st, ea); break;
-    case E_BIAS: launch1w<E_BIAS, 0>(x, ldx, w, bias, M, K, 0, out, ldo, TM, N / kBN, 1, group_m, st, ea); break;
-    case E_BIAS_GELU: launch1w<E_BIAS_GELU, 0>(x, ldx, w, bias, M, K, 0, out, ldo, TM, N / kBN, 1, group_m, st, ea); break;
-    case E_BIAS_RELU: launch1w<E_BIAS_RELU, 0>(x, ldx, w, bias, M, K, 0, out, ldo, TM, N / kBN, 1, group_m, st, ea); break;
-    case E_RESID: launch1w<E_RESID, 0>(x, ldx, w, nullptr, M, K, 0, out, ldo, TM, N / kBN, 1, group_m, st, ea); break;
-    case E_QKV: launch1w_sc<E_QKV>(x, ldx, w, nullptr, M, K, 0, out, ldo, TM, N / kBN, 1, group_m, st, ea); break;
+    case E_NONE: launch1w_sc<E_NONE>(bm, x, ldx, w, bias, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
+    case E_SWIGLU: launch1w_sc<E_SWIGLU>(bm, x, ldx, w, bias, M, K, N / 2, out, ldo, N / 256, 1, group_m, st, ea); break;
+    case E_BIAS: launch1w_bm<E_BIAS, 0>(bm, x, ldx, w, bias, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
+    case E_BIAS_GELU: launch1w_bm<E_BIAS_GELU, 0>(bm, x, ldx, w, bias, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
+    case E_BIAS_RELU: launch1w_bm<E_BIAS_RELU, 0>(bm, x, ldx, w, bias, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
+    case E_RESID: launch1w_bm<E_RESID, 0>(bm, x, ldx, w, nullptr, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
+    case E_QKV: launch1w_sc<E_QKV>(bm, x, ldx, w, nullptr, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
     default: return -1;
   }
   LK_CHECK_LAUNCH();
@@ -607,7 +639,7 @@ int lk_gemm1w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, in
 
 // probes (benchmarks/gemm1w_probe.py): plain / SwiGLU / bias epilogues through ctypes
 extern "C" int lk_gemm1w_c(const void* x, long ldx, const void* w, const void* bias, int M, int N, int K, int epi,
-                           void* out, long ldo, void* stream, int group_m) {
+                           void* out, long ldo, void* stream, int group_m, int bm) {
   return lk_gemm1w((const bf16_t*)x, ldx, (const bf16_t*)w, (const bf16_t*)bias, M, N, K, epi, (bf16_t*)out, ldo,
-                   (hipStream_t)stream, 1, nullptr, nullptr, group_m);
+                   (hipStream_t)stream, 1, nullptr, nullptr, group_m, bm);
 }

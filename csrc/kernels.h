@@ -96,12 +96,14 @@ int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int 
             int variant, bf16_t* out, long ldo, hipStream_t st, int ks = 1, float* ws = nullptr,
             const LkEpi* ea = nullptr);
 
-// gemm1w.hip: the one-wave-per-SIMD 256 x 256 prefill GEMM (hipBLASLt's gfx950 K-loop schedule,
-// every lk_gemm epilogue); lk_gemm routes variant 3 here.  Needs K % 64 == 0 and >= 3 K-tiles per
-// split, N % 256 == 0 (SwiGLU: N/2 % 128).  group_m <= 0: LK_GEMM_GROUP_M (4).
-int lk_gemm1w_supported(int M, int N, int K, int epi, int ks);
+// gemm1w.hip: the one-wave-per-SIMD bm x 256 prefill GEMM (hipBLASLt's gfx950 K-loop schedule,
+// every lk_gemm epilogue); lk_gemm routes variants 3 / 4 / 5 here (row tile bm = 256 / 192 / 128).
+// Needs K % 64 == 0 and >= 3 K-tiles per split, N % 256 == 0 (SwiGLU: N/2 % 128).
+// group_m <= 0: LK_GEMM_GROUP_M (4).
+inline int lk_gemm1w_bm(int variant) { return variant == 3 ? 256 : variant == 4 ? 192 : variant == 5 ? 128 : 0; }
+int lk_gemm1w_supported(int M, int N, int K, int epi, int ks, int bm = 256);
 int lk_gemm1w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi,
-              bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, const LkEpi* ea, int group_m);
+              bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, const LkEpi* ea, int group_m, int bm = 256);
 
 // rope_kv.hip
 int lk_rope_kv(bf16_t* qkv, long qs, const int* positions, const float* cos_sin, long T, int Hq,

@@ -381,35 +381,62 @@ def _gemm_sched(K: int) -> int:
     return 2 if K >= 4096 else 0
 _GEMM_TABLE: dict = {}
 LIBRARY_FALLBACKS: dict = {}
+# measured (variant, bn, splits) per (M bucket, N, K, epilogue) for the shipped models' projections
+# (benchmarks/gemm_table.py on an MI355X; LK_GEMM_STATIC=0 ignores it)
+GEMM_TABLE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_table_mi355x.json")
+_STATIC: Optional[dict] = None
+
+
+def _static_table() -> dict:
+    global _STATIC
+    if _STATIC is None:
+        _STATIC = {}
+        if os.environ.get("LK_GEMM_STATIC", "1") != "0" and os.path.exists(GEMM_TABLE_FILE):
+            import json
+
+            with open(GEMM_TABLE_FILE) as f:
+                for mb, n, k, epi, v, bn, ks in json.load(f)["entries"]:
+                    _STATIC[(mb, n, k, epi)] = (v, bn, ks)
+    return _STATIC
 
 
 def _gemm_key(M: int, N: int, K: int, epi: int):
     return ((M + 255) // 256, N, K, epi)
 
 
-# Variant 3 = csrc/gemm1w.hip, the one-wave-per-SIMD 256 x 256 kernel on hipBLASLt's gfx950
-# K-loop schedule: 1.04-1.09x gemm.hip and 0.95-1.10x hipBLASLt on the Llama-3-8B projections
-# (profiles/r5_gemm1w/).  The default for 256-wide tiles once they fill at least one wave of CUs;
-# gemm.hip keeps the 192-wide tiles (QKV at M 4096: 512 tiles = 2 whole waves, where 256-wide
-# tiles leave half a wave idle) and the split-K shapes.  LK_GEMM1W=0 restores round 4's choice.
+# Variants 3 / 4 / 5 = csrc/gemm1w.hip, the one-wave-per-SIMD kernel on hipBLASLt's gfx950 K-loop
+# schedule, 256-wide column tiles and 256 / 192 / 128-row tiles: 1.04-1.09x gemm.hip and
+# 0.95-1.10x hipBLASLt on the Llama-3-8B projections at 256 rows (profiles/r5_gemm1w/).  The
+# smaller row tiles fill the 256 CUs where 256-row tiles leave most of a wave idle: at the
+# serving bench's mixed-step sizes (prefill chunk + ~105 decode rows) they are 1.2-1.4x the
+# round-4 dispatch (M 2664: QKV on 128-row tiles 109.5 vs 151.6 us, O / down on 192-row tiles
+# 66.7 / 220.8 vs 82.3 / 295.5 us; benchmarks/gemm_tiles.py, profiles/r5_gemm_tiles/).
+# Which tile wins depends on M through the wave quantisation AND the chip's clocks (a partly
+# filled wave runs at a higher clock), so the choice is MEASURED: ``tune_gemm`` times every
+# candidate per 256-row M bucket, and a table of those measurements for the shipped models
+# (gemm_table_mi355x.json, written by benchmarks/gemm_table.py on an MI355X) is the default;
+# ``_gemm_default`` below is the fallback for shapes the table does not hold.
+# LK_GEMM1W=0 restores round 4's gemm.hip-only choice.
 GEMM1W = os.environ.get("LK_GEMM1W", "1") != "0"
 GEMM1W_MIN_TILES = 256
+GEMM1W_BM = {3: 256, 4: 192, 5: 128}
 
 
 def _gemm_configs(N: int, epi: int):
-    """(schedule, column tile) candidates the kernels support for this N / epilogue."""
+    """(schedule / variant, column tile) candidates the kernels support for this N / epilogue."""
     bns = [256] if epi == 1 else [bn for bn in (256, 192) if N % bn == 0]
     cfgs = [(sched, bn) for bn in bns for sched in (0, 1, 2)]
-    if 256 in bns:
-        cfgs.append((3, 256))
+    if 256 in bns and GEMM1W:
+        cfgs += [(v, 256) for v in GEMM1W_BM]
     return cfgs
 
 
 def _gemm_default(M: int, N: int, K: int, epi: int):
-    """Fewest tile-columns x waves: cost(bn) = ceil(tiles / 256 CUs) * bn (ties -> 256); 256-wide
-    tiles on gemm1w.hip (variant 3) when they fill a wave, else gemm.hip's 4-phase schedule
-    (fastest of its schedules on the serving shapes with weights streamed from HBM:
-    profiles/r2_gemm.md)."""
+    """Fallback policy for shapes without a measured entry.  gemm.hip: fewest tile-columns x
+    waves, cost(bn) = ceil(tiles / 256 CUs) * bn (ties -> 256), 4-phase schedule (fastest of its
+    schedules with weights streamed from HBM: profiles/r2_gemm.md).  gemm1w.hip (256-row tiles)
+    instead once its tiles fill a wave, and its 192-row tiles where 256-row tiles would leave
+    over a third of a single wave idle while 192-row ones still fit in one."""
     tm = (M + 255) // 256
     best = None
     for _, bn in _gemm_configs(N, epi):
@@ -422,8 +449,12 @@ def _gemm_default(M: int, N: int, K: int, epi: int):
     bn = best[1]
     ks = _gemm_splits(M, N, K, epi, bn)
     tiles = tm * (N // 2 // 128 if epi == 1 else N // bn)
-    if GEMM1W and bn == 256 and ks == 1 and tiles >= GEMM1W_MIN_TILES and K // 64 >= 3:
-        return (3, 256, 1)
+    if GEMM1W and bn == 256 and ks == 1 and K // 64 >= 3:
+        if tiles >= GEMM1W_MIN_TILES:
+            return (3, 256, 1)
+        tiles192 = -(-M // 192) * (N // 2 // 128 if epi == 1 else N // 256)
+        if tiles < 0.7 * 256 and tiles192 <= 256:
+            return (4, 256, 1)
     return (_gemm_sched(K), bn, ks)
 
 
@@ -461,12 +492,9 @@ def gemm(x, w, b=None, epi: int = 0, out=None):
         return None
     if out is not None and (out.data_ptr() % 16 or out.stride(0) % 8 or out.stride(1) != 1):
         return None
-    key = _gemm_key(M, N, K, epi)
-    cfg = _GEMM_TABLE.get(key)
-    if cfg is None:
-        cfg = _gemm_default(M, N, K, epi)
-        if cfg is None or not lib().gemm_supported(M, N, K, epi, cfg[1], cfg[2], cfg[0]):
-            return None
+    cfg = _cfg_of(M, N, K, epi)
+    if cfg is None or not lib().gemm_supported(M, N, K, epi, cfg[1], cfg[2], cfg[0]):
+        return None
     return lib().gemm(x, w, b, epi, cfg[1], out, cfg[0], cfg[2])
 
 
@@ -480,13 +508,16 @@ def _library(x, w, b, act, key):
     return y
 
 
-def tune_gemm(weights, max_m: int, min_m: int = 512, iters: int = 6, cold_bytes: int = 600 << 20) -> dict:
-    """Time every (schedule, column tile) of the kernel for each 256-row M bucket in
-    [min_m, max_m] and each (weight, epilogue) pair; keep the fastest.  As in serving, the
-    weights arrive from HBM: each launch reads the next of enough weight copies to overflow
-    the 256 MB MALL (a warm-weight tuning picks the 2-phase schedule for the SwiGLU
-    projection, which is 3 % slower in situ).  Candidates are timed round-robin so clock drift
-    hits all alike.  ``weights``: [(w [N, K] bf16 CUDA tensor, epi)].  Returns {key: {cfg: us}}."""
+def tune_gemm(weights, max_m: int, min_m: int = 512, iters: int = 6, cold_bytes: int = 600 << 20,
+              ms: Optional[list] = None) -> dict:
+    """Time every (schedule / variant, column tile) of the prefill kernels for each 256-row M
+    bucket in [min_m, max_m] (or the row counts ``ms``) and each (weight, epilogue) pair; keep
+    the fastest.  gemm.hip candidates run with the split-K the policy gives them, gemm1w.hip
+    unsplit.  As in serving, the weights arrive from HBM: each launch reads the next of enough
+    weight copies to overflow the 256 MB MALL (a warm-weight tuning picks the 2-phase schedule for
+    the SwiGLU projection, which is 3 % slower in situ).  Candidates are timed round-robin so
+    clock drift hits all alike.  ``weights``: [(w [N, K] bf16 CUDA tensor, epi)].  Returns
+    {key: {cfg: us}} and fills the tuned table."""
     import statistics
 
     L = lib()
@@ -500,11 +531,9 @@ def tune_gemm(weights, max_m: int, min_m: int = 512, iters: int = 6, cold_bytes:
         b.synchronize()
         return a.elapsed_time(b) * 1e3
 
+    rows = ms if ms is not None else [mb * 256 for mb in range(max(min_m, 256) // 256, max_m // 256 + 1)]
     for w, epi in weights:
         N, K = w.shape
-        cfgs = [c for c in _gemm_configs(N, epi) if L.gemm_supported(max_m, N, K, epi, c[1], 1, c[0])]
-        if not cfgs:
-            continue
         copies = [w] + [w.clone() for _ in range(max(0, -(-cold_bytes // (N * K * 2)) - 1))]
         rot = [0]
 
@@ -513,10 +542,19 @@ def tune_gemm(weights, max_m: int, min_m: int = 512, iters: int = 6, cold_bytes:
             return copies[rot[0]]
 
         bias = torch.zeros(N, device=w.device, dtype=torch.bfloat16) if epi >= 2 else None
-        xmax = torch.randn(max_m, K, device=w.device, dtype=torch.bfloat16)
-        for mb in range(max(min_m, 256) // 256, max_m // 256 + 1):
-            x = xmax[: mb * 256]
-            fns = {c: (lambda c=c: L.gemm(x, wn(), bias, epi, c[1], None, c[0])) for c in cfgs}
+        xmax = torch.randn(max(rows), K, device=w.device, dtype=torch.bfloat16)
+        for M in rows:
+            x = xmax[:M]
+            cfgs = []
+            for v, bn in _gemm_configs(N, epi):
+                ks = 1 if v in GEMM1W_BM else _gemm_splits(M, N, K, epi, bn)
+                if not L.gemm_supported(M, N, K, epi, bn, ks, v):
+                    ks = 1
+                if L.gemm_supported(M, N, K, epi, bn, ks, v):
+                    cfgs.append((v, bn, ks))
+            if not cfgs:
+                continue
+            fns = {c: (lambda c=c: L.gemm(x, wn(), bias, epi, c[1], None, c[0], c[2])) for c in cfgs}
             for f in fns.values():
                 f()
             ts = {c: [] for c in cfgs}
@@ -524,13 +562,9 @@ def tune_gemm(weights, max_m: int, min_m: int = 512, iters: int = 6, cold_bytes:
                 for c, f in fns.items():
                     ts[c].append(once(f))
             med = {c: statistics.median(v) for c, v in ts.items()}
-            key = _gemm_key(mb * 256, N, K, epi)
-            sched, bn = min(med, key=med.get)
-            # keep the default policy's split-K for the winning tile (a 2-tuple
-            # entry silently dropped it on the low-tile-count O / down shapes)
-            ks = _gemm_splits(mb * 256, N, K, epi, bn)
-            _GEMM_TABLE[key] = (sched, bn, ks if L.gemm_supported(mb * 256, N, K, epi, bn, ks, sched) else 1)
-            out[key] = {f"s{c[0]}/{c[1]}": round(t, 1) for c, t in med.items()}
+            key = _gemm_key(M, N, K, epi)
+            _GEMM_TABLE[key] = min(med, key=med.get)
+            out[key] = {f"v{c[0]}/{c[1]}/k{c[2]}": round(t, 1) for c, t in med.items()}
         del copies
     return out
 
@@ -717,14 +751,23 @@ EPI_RESID, EPI_QKV = 6, 7
 
 
 def _cfg_of(M: int, N: int, K: int, epi: int):
-    """(schedule, bn, splits) of the prefill GEMM for this shape (tuned table, else default)."""
-    cfg = _GEMM_TABLE.get(_gemm_key(M, N, K, epi))
+    """(schedule / variant, bn, splits) of the prefill GEMM for this shape: the start-up tuned
+    table (LK_GEMM_TUNE=1), else the shipped measurements (gemm_table_mi355x.json), else the
+    fallback policy."""
+    key = _gemm_key(M, N, K, epi)
+    cfg = _GEMM_TABLE.get(key)
+    if cfg is None:
+        cfg = _static_table().get(key)
+        if cfg is not None and (not GEMM1W and cfg[0] in GEMM1W_BM):
+            cfg = None
     return cfg if cfg is not None else _gemm_default(M, N, K, epi)
 
 
 def _resid_cfg(M: int, N: int, K: int):
-    sched = _cfg_of(M, N, K, 0)
-    sched = sched[0] if sched is not None else _gemm_sched(K)
+    c = _cfg_of(M, N, K, 0)
+    if c is not None and c[0] in GEMM1W_BM:
+        return c  # (variant, 256, 1)
+    sched = c[0] if c is not None else _gemm_sched(K)
     return sched, 256, _gemm_splits(M, N, K, 0, 256)
 
 

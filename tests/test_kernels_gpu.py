@@ -419,8 +419,9 @@ def test_ws_swiglu(hip, M, IK):
     _close(hip.ws_linear(x, w, True, 64, 2), a_ref, 0.03, 0.01, "ws swiglu bn64 S2")
 
 
-# (schedule, column tile): gemm.hip schedules 0-2, and variant 3 = csrc/gemm1w.hip (256-wide only)
-GEMM_CFGS = [(0, 256), (1, 256), (2, 256), (0, 192), (1, 192), (2, 192), (3, 256)]
+# (schedule, column tile): gemm.hip schedules 0-2, and variants 3 / 4 / 5 = csrc/gemm1w.hip (256-wide
+# column tiles, 256 / 192 / 128-row tiles)
+GEMM_CFGS = [(0, 256), (1, 256), (2, 256), (0, 192), (1, 192), (2, 192), (3, 256), (4, 256), (5, 256)]
 
 
 @pytest.mark.parametrize("M", [1, 257, 1000, 3584])
@@ -459,7 +460,7 @@ def test_gemm_splitk(hip, MNK, splits, epi):
         y = torch.nn.functional.gelu(y)
     elif epi == 4:
         y = torch.relu(y)
-    for sched in (0, 1, 3):
+    for sched in (0, 1, 3, 4, 5):
         for bn in (256, 192):
             if hip.gemm_supported(M, N, K, epi, bn, splits, sched):
                 _close(hip.gemm(x, w, b, epi, bn, None, sched, splits), y, 0.03, 0.01,
@@ -541,7 +542,7 @@ def test_gemm_asymmetric_layout(hip):
     M = N = K = 256
     x = torch.eye(M, K, device=DEV, dtype=torch.bfloat16)
     w = (torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K) % 97 - 48).to(torch.bfloat16)
-    for sched, bn in [(0, 256), (1, 256), (3, 256)]:
+    for sched, bn in [(0, 256), (1, 256), (3, 256), (4, 256), (5, 256)]:
         y = hip.gemm(x, w, None, 0, bn, None, sched)
         assert torch.equal(y.float().cpu(), w.float().t().cpu()), f"s{sched}/{bn}"
 
@@ -554,7 +555,7 @@ def test_gemm_swiglu_matches_unfused(hip, M, IK):
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(2 * I, K, device=DEV, dtype=torch.bfloat16) * 0.05
     a_ref = ref.silu_mul((x.float() @ w.float().t()).to(torch.bfloat16))
-    for sched in (0, 1, 3):
+    for sched in (0, 1, 3, 4, 5):
         _close(hip.gemm(x, w, None, 1, 256, None, sched), a_ref, 0.03, 0.01, f"gemm s{sched} swiglu M{M} I{I}")
 
 
@@ -802,8 +803,8 @@ def _qkv_setup(M, Hq=32, Hkv=8, D=128, H=4096, nb=600, bs=16, seed=0):
 
 
 @pytest.mark.parametrize("M,N,K,splits", [(300, 1024, 512, 1), (1000, 4096, 1024, 1), (2304, 4096, 14336, 3),
-                                          (777, 2048, 4096, 2), (4352, 4096, 4096, 1)])
-@pytest.mark.parametrize("variant", [2, 3])
+                                          (777, 2048, 4096, 2), (4352, 4096, 4096, 1), (2664, 4096, 4096, 1)])
+@pytest.mark.parametrize("variant", [2, 3, 4, 5])
 def test_gemm_resid_epilogue(hip, M, N, K, splits, variant):
     """RESID (producer side of the folded norm): r = bf16(r + bf16(x W^T)) in place and the
     per-256-column partial sums of squares of the new r, in-kernel and through the split-K
@@ -827,7 +828,7 @@ def test_gemm_resid_epilogue(hip, M, N, K, splits, variant):
 
 @pytest.mark.parametrize("M", [300, 2048, 4352])
 @pytest.mark.parametrize("scaled", [False, True])
-@pytest.mark.parametrize("variant,H", [(2, 4096), (3, 4096), (3, 8192)])
+@pytest.mark.parametrize("variant,H", [(2, 4096), (3, 4096), (3, 8192), (4, 4096), (5, 8192)])
 def test_gemm_swiglu_row_scale(hip, M, scaled, variant, H):
     """SwiGLU epilogue with the folded post-norm's row scale s = rsqrt(sum(ss) / H + eps) (H 8192:
     32 partial planes, the 70B width)."""
@@ -842,7 +843,8 @@ def test_gemm_swiglu_row_scale(hip, M, scaled, variant, H):
 
 
 @pytest.mark.parametrize("M,bn,variant", [(300, 192, 2), (1111, 256, 2), (4352, 192, 2), (2560, 256, 2),
-                                          (300, 256, 3), (1111, 256, 3), (4352, 256, 3)])
+                                          (300, 256, 3), (1111, 256, 3), (4352, 256, 3), (2664, 256, 4),
+                                          (300, 256, 4), (2664, 256, 5), (1111, 256, 5)])
 @pytest.mark.parametrize("scaled", [False, True])
 def test_gemm_qkv_epilogue(hip, M, bn, variant, scaled):
     """QKV epilogue: row scale, interleaved-pair RoPE on q / k, K / V into the paged cache at
@@ -874,7 +876,7 @@ def test_gemm_qkv_epilogue_layout(hip):
     slots = torch.arange(M, device=DEV, dtype=torch.int32)
     kc = torch.zeros(M // 16, Hkv, 16, D, device=DEV, dtype=torch.bfloat16)
     vc, kc2, vc2 = kc.clone(), kc.clone(), kc.clone()
-    for variant in (2, 3):
+    for variant in (2, 3, 4, 5):
         kc.zero_(), vc.zero_(), kc2.zero_(), vc2.zero_()
         out = hip.gemm_fused(x, w, 7, 256, None, variant, 1, positions=pos, cos_sin=cs, slots=slots, k_cache=kc,
                              v_cache=vc, hq=Hq, hkv=Hkv, hd=D)

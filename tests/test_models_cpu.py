@@ -309,9 +309,11 @@ def test_gemm_split_k_policy():
 
 
 def test_gemm1w_default_policy(monkeypatch):
-    """256-wide prefill tiles go to the one-wave-per-SIMD kernel (variant 3, csrc/gemm1w.hip) once
-    they fill a wave of 256 CUs; QKV at M 4096 keeps gemm.hip's 192-wide tiles (2 whole waves),
-    split-K shapes stay on gemm.hip; LK_GEMM1W=0 turns it off."""
+    """Fallback policy (shapes without a measured entry): 256-wide prefill tiles go to the
+    one-wave-per-SIMD kernel (variant 3, csrc/gemm1w.hip) once they fill a wave of 256 CUs, its
+    192-row tiles (variant 4) where 256-row tiles would leave over a third of one wave idle; QKV
+    at M 4096 keeps gemm.hip's 192-wide tiles (2 whole waves), split-K shapes stay on gemm.hip;
+    LK_GEMM1W=0 turns it off."""
     from llm_kubernetes_minikube_sharp4dev_amd import ops
 
     monkeypatch.setattr(ops, "GEMM1W", True)
@@ -320,11 +322,40 @@ def test_gemm1w_default_policy(monkeypatch):
     assert ops._gemm_default(4096, 28672, 4096, 1) == (3, 256, 1)     # gate_up + SwiGLU
     assert ops._gemm_default(4096, 6144, 4096, 7)[:2] == (ops._gemm_sched(4096), 192)  # QKV: 2 whole waves
     assert ops._gemm_default(8192, 6144, 4096, 0) == (3, 256, 1)      # tie on waves -> 256
-    assert ops._gemm_default(1024, 4096, 4096, 0)[0] != 3             # 64 tiles: split-K on gemm.hip
-    assert (3, 256) in ops._gemm_configs(4096, 0) and (3, 256) in ops._gemm_configs(28672, 1)
-    assert all(c[0] != 3 for c in ops._gemm_configs(1152, 0))         # no 256-wide tile
+    assert ops._gemm_default(2664, 4096, 4096, 0) == (4, 256, 1)      # 176 tiles -> 224 of 192 rows
+    assert ops._gemm_default(1024, 4096, 4096, 0)[0] not in ops.GEMM1W_BM  # 64 tiles: split-K on gemm.hip
+    assert {(3, 256), (4, 256), (5, 256)} <= set(ops._gemm_configs(4096, 0))
+    assert (3, 256) in ops._gemm_configs(28672, 1)
+    assert all(c[0] not in ops.GEMM1W_BM for c in ops._gemm_configs(1152, 0))  # no 256-wide tile
     monkeypatch.setattr(ops, "GEMM1W", False)
     assert ops._gemm_default(4096, 4096, 4096, 0)[0] == ops._gemm_sched(4096)
+    assert all(c[0] not in ops.GEMM1W_BM for c in ops._gemm_configs(4096, 0))
+
+
+def test_static_gemm_table_is_well_formed(monkeypatch):
+    """The shipped measured dispatch table (benchmarks/gemm_table.py on an MI355X): every entry a
+    kernel / tile / split the dispatch knows, looked up by _cfg_of before the fallback policy,
+    and ignored under LK_GEMM1W=0 where it names a gemm1w variant."""
+    import json
+    import os
+
+    from llm_kubernetes_minikube_sharp4dev_amd import ops
+
+    if not os.path.exists(ops.GEMM_TABLE_FILE):
+        pytest.skip("no measured table shipped")
+    doc = json.load(open(ops.GEMM_TABLE_FILE))
+    assert doc["arch"] == "gfx950" and doc["entries"]
+    for mb, n, k, epi, v, bn, ks in doc["entries"]:
+        assert v in (0, 1, 2, 3, 4, 5) and bn in (192, 256) and 1 <= ks <= 4 and epi in (0, 1)
+        assert bn == 256 or v not in ops.GEMM1W_BM
+        assert ks == 1 or v not in ops.GEMM1W_BM
+        assert k % 64 == 0 and n % bn == 0
+    mb, n, k, epi, v, bn, ks = doc["entries"][0]
+    monkeypatch.setattr(ops, "_GEMM_TABLE", {})
+    monkeypatch.setattr(ops, "GEMM1W", True)
+    assert ops._cfg_of(mb * 256, n, k, epi) == (v, bn, ks)
+    monkeypatch.setattr(ops, "GEMM1W", False)
+    assert ops._cfg_of(mb * 256, n, k, epi)[0] not in ops.GEMM1W_BM
 
 
 def test_lib_path_ab_knob_loads_the_named_build():
