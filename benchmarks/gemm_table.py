@@ -21,10 +21,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from llm_kubernetes_minikube_sharp4dev_amd import ops  # noqa: E402
-from llm_kubernetes_minikube_sharp4dev_amd.models.configs import DECODERS  # noqa: E402
+from llm_kubernetes_minikube_sharp4dev_amd.models.configs import DECODERS, ENCODERS  # noqa: E402
 
 
 def shapes(name: str):
+    if name in ENCODERS:  # bias epilogues; M = the encoder's token-budget batches
+        c = ENCODERS[name]
+        return [(3 * c.hidden, c.hidden, 2), (c.hidden, c.hidden, 2), (c.intermediate, c.hidden, 3),
+                (c.hidden, c.intermediate, 2)]
     base, _, tp = name.partition("/tp")
     c = DECODERS[base]
     t = int(tp) if tp else 1
@@ -41,6 +45,8 @@ def main():
     ap.add_argument("--min-m", type=int, default=512)
     ap.add_argument("--max-m", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=7)
+    ap.add_argument("--encoders", default="bge-base", help="encoder presets, measured at --encoder-ms rows")
+    ap.add_argument("--encoder-ms", default="16384,65536,131072")
     a = ap.parse_args()
     torch.manual_seed(0)
     t0 = time.time()
@@ -58,6 +64,16 @@ def main():
                 timings[",".join(map(str, key))] = arms
                 best = ops._GEMM_TABLE[key]
                 print(f"{m:16s} M{key[0] * 256:5d} N{N:5d} K{K:5d} e{epi}: v{best[0]}/{best[1]}/k{best[2]} "
+                      f"{arms[f'v{best[0]}/{best[1]}/k{best[2]}']:.1f} us  ({len(arms)} candidates)", flush=True)
+            del w
+    for m in [e for e in a.encoders.split(",") if e]:
+        for N, K, epi in shapes(m):
+            w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
+            res = ops.tune_gemm([(w, epi)], 0, iters=3, ms=[int(v) for v in a.encoder_ms.split(",")])
+            for key, arms in res.items():
+                timings[",".join(map(str, key))] = arms
+                best = ops._GEMM_TABLE[key]
+                print(f"{m:16s} M{key[0] * 256:6d} N{N:5d} K{K:5d} e{epi}: v{best[0]}/{best[1]}/k{best[2]} "
                       f"{arms[f'v{best[0]}/{best[1]}/k{best[2]}']:.1f} us  ({len(arms)} candidates)", flush=True)
             del w
     entries = sorted([list(k) + list(v) for k, v in ops._GEMM_TABLE.items()])

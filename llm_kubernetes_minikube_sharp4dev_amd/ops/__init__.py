@@ -385,6 +385,7 @@ LIBRARY_FALLBACKS: dict = {}
 # (benchmarks/gemm_table.py on an MI355X; LK_GEMM_STATIC=0 ignores it)
 GEMM_TABLE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_table_mi355x.json")
 _STATIC: Optional[dict] = None
+_STATIC_TOP: dict = {}  # (N, K, epi) -> largest measured M bucket
 
 
 def _static_table() -> dict:
@@ -397,7 +398,21 @@ def _static_table() -> dict:
             with open(GEMM_TABLE_FILE) as f:
                 for mb, n, k, epi, v, bn, ks in json.load(f)["entries"]:
                     _STATIC[(mb, n, k, epi)] = (v, bn, ks)
+                    _STATIC_TOP[(n, k, epi)] = max(mb, _STATIC_TOP.get((n, k, epi), 0))
     return _STATIC
+
+
+def _static_cfg(key):
+    """The measured entry of an M bucket; past the largest measured bucket of the shape (the
+    encoder's 100k-row batches: many whole waves, where the choice no longer moves with M) the
+    largest one's."""
+    t = _static_table()
+    cfg = t.get(key)
+    if cfg is None:
+        top = _STATIC_TOP.get(key[1:])
+        if top is not None and key[0] > top:
+            cfg = t.get((top,) + key[1:])
+    return cfg
 
 
 def _gemm_key(M: int, N: int, K: int, epi: int):
@@ -757,7 +772,7 @@ def _cfg_of(M: int, N: int, K: int, epi: int):
     key = _gemm_key(M, N, K, epi)
     cfg = _GEMM_TABLE.get(key)
     if cfg is None:
-        cfg = _static_table().get(key)
+        cfg = _static_cfg(key)
         if cfg is not None and (not GEMM1W and cfg[0] in GEMM1W_BM):
             cfg = None
     return cfg if cfg is not None else _gemm_default(M, N, K, epi)

@@ -6,6 +6,8 @@ timeout -k 10 300 python benchmarks/index_build.py > gpurun_out/ib/plain.log 2>&
 grep '"docs"' gpurun_out/ib/plain.log
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/ib/prof -o run --output-format csv -- python3 benchmarks/index_build.py > gpurun_out/ib/prof.log 2>&1 || { tail -5 gpurun_out/ib/prof.log; exit 3; }
 grep '"docs"' gpurun_out/ib/prof.log
+t=$(find gpurun_out/ib/prof -name "*kernel_trace.csv" | head -1)
+SUMMARY_BY_GRID=1 SUMMARY_TOP=40 python3 scripts/summarize_trace.py $t 60 > gpurun_out/ib/by_grid.md && rm -f $t
 f=$(find gpurun_out/ib/prof -name "*kernel_stats.csv" | head -1)
 python -c "
 import csv

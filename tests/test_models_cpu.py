@@ -346,7 +346,7 @@ def test_static_gemm_table_is_well_formed(monkeypatch):
     doc = json.load(open(ops.GEMM_TABLE_FILE))
     assert doc["arch"] == "gfx950" and doc["entries"]
     for mb, n, k, epi, v, bn, ks in doc["entries"]:
-        assert v in (0, 1, 2, 3, 4, 5) and bn in (192, 256) and 1 <= ks <= 4 and epi in (0, 1)
+        assert v in (0, 1, 2, 3, 4, 5) and bn in (192, 256) and 1 <= ks <= 4 and epi in (0, 1, 2, 3, 4)
         assert bn == 256 or v not in ops.GEMM1W_BM
         assert ks == 1 or v not in ops.GEMM1W_BM
         assert k % 64 == 0 and n % bn == 0
