@@ -116,9 +116,18 @@ LK_DEVICE u32x4_t srd(const void* p, long bytes) {  // buffer descriptor words, 
   return u32x4_t{rfl((unsigned)a), rfl((unsigned)(a >> 32)), (unsigned)min(bytes, 0x7FFFFFF0L), 0x00020000u};
 }
 
+// vector-memory operations per lane of the plain / bias epilogues (bias loads, then stores): the
+// persistent walk's counted wait for the next tile's first K-tile skips them
+template <int EPI, int MB>
+constexpr int epi_vm_ops() { return (EPI == E_NONE ? 0 : 4) + 4 * MB; }
+constexpr bool persistable(int e) { return e == E_NONE || e == E_BIAS || e == E_BIAS_GELU || e == E_BIAS_RELU; }
+
 // SCP: partial-sum planes of the folded-RMSNorm row scale loaded per row (0: no row scale; 16 covers
-// a 4096-wide producer, 32 an 8192-wide one)
-template <int EPI, int SCP, int BM>
+// a 4096-wide producer, 32 an 8192-wide one).  PERSIST: one workgroup per CU walks the tiles
+// blockIdx.x, + gridDim.x, ...; the next tile's first two K-tiles are DMA'd during the current
+// tile's last two, so its load ramp hides behind the current epilogue (short-K shapes: the
+// encoder's K = 768 projections, 12 K-tiles per tile)
+template <int EPI, int SCP, int BM, bool PERSIST = false>
 __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict__ X, long ldx,
                                                         const bf16_t* __restrict__ W,
                                                         const bf16_t* __restrict__ bias, int M, int K, int I,
@@ -126,6 +135,7 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
                                                         int group_m, LkEpi ea) {
   constexpr bool SC = SCP > 0;
   static_assert(!SC || scalable(EPI), "row scale");
+  static_assert(!PERSIST || (persistable(EPI) && !SC), "persistent walk: plain / bias epilogues");
   using TL = Tile<BM>;
   constexpr int MB = TL::MB, NM = TL::NM, NR = TL::NR, PX = TL::PX, NP = TL::NP, WM = BM / 2;
   constexpr int kOpX = TL::kOpX, kStage = TL::kStage, kLdsStages = TL::kLdsStages;
@@ -156,14 +166,15 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
   // 64 w + 8 (i - PX) + (lane >> 3) of W, 16-B chunk lane & 7 (source chunk swizzled); per-lane
   // row offsets of the tile
   const int lr8 = lane >> 3, lc8 = lane & 7;
-  unsigned xo[PX], wo[8];
+  unsigned xo[PX], wo[8], xo2[PX], wo2[8];  // this tile's / (PERSIST) the next tile's
+  int par = 0;  // stage of tile-relative K-tile t: (t + par) & 1 (a persistent walk carries it on)
   // (32-bit: the host keeps every operand under 2^31 bytes).  Closed forms with the piece index
   // i in immediates only -- per-i lane constants held across the tile loop spill:
   //   row = BM/4 w + 8 i + lr8;  swz(row) = (lr8 >> 1) ^ 4 (i & 1)  (BM/8 w is a multiple of 8);
   //   W row = lane part + 32 (i >> 2) + 16 (i & 1) + 4 ((i >> 1) & 1)   (pair_col of row & 31)
   const unsigned ldxb = (unsigned)ldx * 2, kb = (unsigned)K * 2;
   const unsigned ch0 = (unsigned)((lc8 ^ (lr8 >> 1)) << 4);
-  auto offsets = [&](int tm, int tn) {
+  auto offsets = [&](int tm, int tn, unsigned (&xo)[PX], unsigned (&wo)[8]) {
     const unsigned xb = (unsigned)(tm * BM + (BM / 4) * w + lr8) * ldxb;
     const int lanew = 8 * (lr8 >> 2) + (lr8 & 3);
     const unsigned wl = EPI == E_SWIGLU ? (unsigned)((w & 1) * I + tn * 128 + (w >> 1) * 64 + lanew)
@@ -176,14 +187,16 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
       wo[i] = wb + (unsigned)(32 * (i >> 2) + 16 * (i & 1) + 4 * ((i >> 1) & 1)) * kb + (ch0 ^ (unsigned)((i & 1) << 6));
   };
   auto piece_m0 = [&](int t, int i) -> unsigned {  // LDS base of piece i of (tile-relative) K-tile t
-    return i < PX ? ldsx + (unsigned)((t & 1) * kStage + 8 * i * kRowB)
-                  : ldsw + (unsigned)((t & 1) * kStage + 8 * (i - PX) * kRowB);
+    return i < PX ? ldsx + (unsigned)(((t + par) & 1) * kStage + 8 * i * kRowB)
+                  : ldsw + (unsigned)(((t + par) & 1) * kStage + 8 * (i - PX) * kRowB);
   };
-  // issue piece i of K-tile t (M0 already holds its LDS base)
-  auto dma = [&](int t, int i) {
-    const unsigned so = rfl((unsigned)(kt0 + t) * (kBK * 2));
-    if (i < PX) asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(xo[i]), "s"(xsrd), "s"(so) : "memory");
-    else asm volatile("buffer_load_dwordx4 %0, %1, %2 offen sc0 sc1 lds" ::"v"(wo[i - PX]), "s"(wsrd), "s"(so) : "memory");
+  // issue piece i of K-tile t (M0 already holds its LDS base); NEXT: K-tile t - nk of the next tile
+  auto dma = [&](bool NEXT, int t, int i) {  // (NEXT is a constant at every call: folded when inlined)
+    const unsigned so = rfl((unsigned)(NEXT ? t - nk : kt0 + t) * (kBK * 2));
+    const unsigned xv = NEXT ? xo2[i < PX ? i : 0] : xo[i < PX ? i : 0];
+    const unsigned wv = NEXT ? wo2[i < PX ? 0 : i - PX] : wo[i < PX ? 0 : i - PX];
+    if (i < PX) asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(xv), "s"(xsrd), "s"(so) : "memory");
+    else asm volatile("buffer_load_dwordx4 %0, %1, %2 offen sc0 sc1 lds" ::"v"(wv), "s"(wsrd), "s"(so) : "memory");
   };
 
   // ---- fragments: lane reads stage row (16-row base + r), 16-B chunk 4 kk + g, from per-(kk,
@@ -229,12 +242,12 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
   };
 
   // K-tile t: NM MFMAs (kk 0 set: n-major 0..NM/2-1, kk 1 set: the rest) with the reads / DMA /
-  // barriers of the file comment (positions: Tile<BM>).  FIRST: C = 0.  DMA: K-tile t+2 exists.  NXT: K-tile t+1
-  // exists.  LAST: the final K-tile.
-  auto ktile = [&](auto first_t, auto dma_t, auto nxt_t, int t) {
+  // barriers of the file comment (positions: Tile<BM>).  FIRST: C = 0.  DMA: K-tile t+2 exists
+  // (NEXT: it is K-tile t+2-nk of the next tile of a persistent walk).  NXT: K-tile t+1 exists.
+  auto ktile = [&](auto first_t, auto dma_t, auto nxt_t, auto next_t, int t) {
     constexpr bool FIRST = decltype(first_t)::value, DMA = decltype(dma_t)::value;
     constexpr bool NXT = decltype(nxt_t)::value;
-    const unsigned so = (unsigned)(t & 1) * kStage, sn = (unsigned)kStage - so;  // this / next stage
+    const unsigned so = (unsigned)((t + par) & 1) * kStage, sn = (unsigned)kStage - so;  // this / next stage
     unroll<NM>([&](auto i_t) {
       constexpr int i = decltype(i_t)::value;
       constexpr int B1 = TL::B1, D0 = TL::D0, DS = TL::DS, LAG = TL::LAG, B2 = TL::B2;
@@ -246,7 +259,7 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
       }
       if constexpr (DMA && i >= D0 && i < D0 + DS * NP && (i - D0) % DS == 0) {
         fence();
-        dma(t + 2, (i - D0) / DS);
+        dma(decltype(next_t)::value, t + 2, (i - D0) / DS);
         fence();
       }
       if constexpr (DMA && i >= D0 + LAG && i < D0 + LAG + DS * NP && (i - D0 - LAG) % DS == 0) {
@@ -269,36 +282,62 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
     });
   };
 
-  // ---- one tile per workgroup (a persistent walk with the next tile's first K-tiles DMA'd during
-  // the last one measured 1-3 % slower: the hardware already starts the next workgroup on a CU
-  // while the finished one's stores drain -- profiles/r5_gemm1w/)
-  const int tile = blockIdx.x;
+  // ---- one tile per workgroup by default (for long K a persistent walk measured 1-3 % slower: the
+  // hardware already starts the next workgroup on a CU while the finished one's stores drain --
+  // profiles/r5_gemm1w/); PERSIST for short K, where the load ramp is a third of a tile
+  int tile = blockIdx.x;
   int tm, tn;
   coords(tile, tm, tn);
-  offsets(tm, tn);
+  offsets(tm, tn, xo, wo);
   ss_issue(tm);
   // prologue: K-tiles 0 and 1 (the row-scale loads are older: retired with K-tile 0)
 #pragma unroll
   for (int q = 0; q < 2 * NP; ++q) {
     set_m0(piece_m0(q / NP, q % NP));
     asm volatile("s_nop 0");
-    dma(q / NP, q % NP);
+    dma(false, q / NP, q % NP);
   }
   set_m0(piece_m0(2, 0));
   wait_vm<NP>();
-  barrier_raw();
-  if constexpr (SC) {
+  for (;;) {
+    int nxt = 0, tm2 = 0, tn2 = 0;
+    bool has_next = false;
+    if constexpr (PERSIST) {
+      // opaque per tile: keeps hipcc from hoisting the unrolled K-tiles' per-piece / per-fragment
+      // addresses out of the tile loop into hundreds of live registers (it spills them otherwise)
+      asm volatile("" : "+v"(bx[0]), "+v"(bx[1]), "+v"(bw[0]), "+v"(bw[1]));
 #pragma unroll
-    for (int p = 0; p < SCP; ++p) ssum += ssp[p];
-  }
-  unroll<NR>([&](auto j_t) { rd(bx[0], bw[0], j_t, fx0, fw0); });
-  ktile(T{}, T{}, T{}, 0);
-  int t = 1;
-  for (; t + 2 < nk; ++t) ktile(F{}, T{}, T{}, t);
-  ktile(F{}, F{}, T{}, t);
-  ktile(F{}, F{}, F{}, t + 1);
-  // the asm MFMAs are invisible to hipcc's hazard recognizer: wait out MFMA -> accumulator read
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+      for (int i = 0; i < PX; ++i) asm volatile("" : "+v"(xo[i]));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(wo[i]));
+      nxt = tile + (int)gridDim.x;
+      has_next = nxt < nwg;
+      // the last tile of the walk DMAs its own first K-tiles again (harmless, never read): one
+      // straight-line tail instead of two
+      coords(has_next ? nxt : tile, tm2, tn2);
+      offsets(tm2, tn2, xo2, wo2);
+    }
+    barrier_raw();
+    if constexpr (SC) {
+#pragma unroll
+      for (int p = 0; p < SCP; ++p) ssum += ssp[p];
+    }
+    {
+      const unsigned s0 = (unsigned)(par & 1) * kStage;
+      unroll<NR>([&](auto j_t) { rd(bx[0] + s0, bw[0] + s0, j_t, fx0, fw0); });
+    }
+    ktile(T{}, T{}, T{}, F{}, 0);
+    int t = 1;
+    for (; t + 2 < nk; ++t) ktile(F{}, T{}, T{}, F{}, t);
+    if constexpr (PERSIST) {  // the next tile's K-tiles 0 and 1 into the stages these two free
+      ktile(F{}, T{}, T{}, T{}, t);
+      ktile(F{}, T{}, F{}, T{}, t + 1);
+    } else {
+      ktile(F{}, F{}, T{}, F{}, t);
+      ktile(F{}, F{}, F{}, F{}, t + 1);
+    }
+    // the asm MFMAs are invisible to hipcc's hazard recognizer: wait out MFMA -> accumulator read
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
 
     // ================= epilogue of tile (tm, tn)
     // lane holds row tm*256 + wr*128 + 16m + r; fragment pair (2p, 2p+1) the 8 consecutive
@@ -469,6 +508,26 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
         }
       }
     }
+    if constexpr (!PERSIST) {
+      break;
+    } else {
+      if (!has_next) {
+        wait_vm<0>();  // the walk's last (unread) DMAs land before the workgroup's LDS is released
+        break;
+      }
+      tile = nxt;
+      tm = tm2;
+      tn = tn2;
+#pragma unroll
+      for (int i = 0; i < PX; ++i) xo[i] = xo2[i];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) wo[i] = wo2[i];
+      par ^= nk & 1;
+      // the next tile's K-tile 0 has landed: younger than it are K-tile 1's NP pieces and the
+      // epilogue's bias loads and stores (the counter retires in issue order)
+      wait_vm<NP + epi_vm_ops<EPI, MB>()>();
+    }
+  }
 }
 
 // split-K reduction: out[r, c..c+3] = epi(sum_z part[z, r, c..c+3] (+ bias)), rounded like the
@@ -526,19 +585,50 @@ int group1w() {  // row tiles per XCD group of the tile order (LK_GEMM_GROUP_M, 
   return g;
 }
 
-template <int EPI, int SCP, int BM>
-void launch1w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
-              long ldo, int TN, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
+int cu_count() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    return hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+  }();
+  return n;
+}
+
+// persistent walk for short K (LK_GEMM1W_PERSIST_KT: the most K-tiles of 64 it is used for; 0: off)
+int persist_kt() {
+  static const int v = [] {
+    const char* e = getenv("LK_GEMM1W_PERSIST_KT");
+    return e ? atoi(e) : 16;
+  }();
+  return v;
+}
+
+template <int EPI, int SCP, int BM, bool PERSIST = false>
+void launch1w_p(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
+                long ldo, int TN, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
   constexpr int lds = Tile<BM>::kLds;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm1w_kernel<EPI, SCP, BM>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm1w_kernel<EPI, SCP, BM, PERSIST>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
   const int TM = (M + BM - 1) / BM;
-  gemm1w_kernel<EPI, SCP, BM><<<dim3(TM * TN, ks), 256, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN,
-                                                                 group_m > 0 ? group_m : group1w(), ea);
+  const int grid = PERSIST ? min(TM * TN, cu_count()) : TM * TN;
+  gemm1w_kernel<EPI, SCP, BM, PERSIST><<<dim3(grid, ks), 256, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN,
+                                                                       group_m > 0 ? group_m : group1w(), ea);
+}
+template <int EPI, int SCP, int BM>
+void launch1w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
+              long ldo, int TN, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
+  if constexpr (persistable(EPI) && SCP == 0 && BM == 256) {
+    const int tiles = ((M + BM - 1) / BM) * TN;
+    if (ks == 1 && K / kBK <= persist_kt() && tiles > 2 * cu_count()) {
+      launch1w_p<EPI, SCP, BM, true>(x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
+      return;
+    }
+  }
+  launch1w_p<EPI, SCP, BM, false>(x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
 }
 template <int EPI, int SCP>
 void launch1w_bm(int bm, const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I,

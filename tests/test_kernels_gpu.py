@@ -442,6 +442,27 @@ def test_gemm(hip, M, NK):
     assert ran >= 2
 
 
+@pytest.mark.parametrize("M,N,K", [(50001, 3072, 768), (40000, 2304, 768), (33000, 768, 1024)])
+@pytest.mark.parametrize("epi", [0, 2, 3, 4])
+def test_gemm1w_persistent_walk(hip, M, N, K, epi):
+    """Short-K shapes with many tiles run gemm1w's persistent walk (one workgroup per CU, the next
+    tile's first K-tiles DMA'd during the current tile's last two): every tile, M tails and the
+    bias / GELU / ReLU epilogues vs fp32 (the encoder's K = 768 projections)."""
+    torch.manual_seed(M + N + epi)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16) if epi else None
+    y = x.float() @ w.float().t()
+    if epi:
+        y = (y + b.float()).to(torch.bfloat16).float()
+    if epi == 3:
+        y = torch.nn.functional.gelu(y)
+    elif epi == 4:
+        y = torch.relu(y)
+    assert hip.gemm_supported(M, N, K, epi, 256, 1, 3)
+    _close(hip.gemm(x, w, b, epi, 256, None, 3, 1), y, 0.03, 0.01, f"persistent epi{epi} M{M} N{N} K{K}")
+
+
 @pytest.mark.parametrize("MNK", [(2048, 4096, 4096), (300, 1280, 8192), (1000, 768, 3072), (4096, 1280, 8192)])
 @pytest.mark.parametrize("splits", [2, 3, 4])
 @pytest.mark.parametrize("epi", [0, 2, 3, 4])
