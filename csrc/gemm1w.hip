@@ -336,8 +336,14 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
       ktile(F{}, F{}, T{}, F{}, t);
       ktile(F{}, F{}, F{}, F{}, t + 1);
     }
-    // the asm MFMAs are invisible to hipcc's hazard recognizer: wait out MFMA -> accumulator read
+    // the asm MFMAs are invisible to hipcc's hazard recognizer: wait out MFMA -> accumulator read,
+    // and pin every accumulator behind that wait (hipcc otherwise schedules some v_accvgpr_read of
+    // the final K-tile's results right after their MFMA is issued, before it has written them)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+      for (int n = 0; n < 8; ++n) asm volatile("" : "+a"(acc[m][n]));
 
     // ================= epilogue of tile (tm, tn)
     // lane holds row tm*256 + wr*128 + 16m + r; fragment pair (2p, 2p+1) the 8 consecutive
