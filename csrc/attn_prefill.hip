@@ -72,6 +72,7 @@ struct PrefillParams {
   // context parallelism: position of sequence b's first query relative to its FIRST KEY (may be
   // negative or past the keys: this rank holds only a shard of the keys); null = ctx - q_len
   const int* q_past;
+  int xcd;  // XCD-aware workgroup order (prefill_xcd())
 };
 
 // NW waves per workgroup (4 or 8): WH of them share a row group (one head each), and
@@ -94,12 +95,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int G = p.Hq / p.Hkv;
-  const int head = blockIdx.y * WH + (w % WH);
+  // XCD-aware order: the hardware deals workgroups round-robin over the 8 XCDs (each with its own
+  // L2); remapped, every XCD walks a contiguous range of (head group, query tile) -- the query
+  // tiles of the same KV head and sequence, which read the same K / V tiles, share one L2
+  // (LK_PREFILL_XCD=0: the plain order)
+  const int nx = gridDim.x;
+  const int lin = p.xcd ? xcd_remap(blockIdx.y * nx + blockIdx.x, nx * gridDim.y) : blockIdx.y * nx + blockIdx.x;
+  const int bx = lin % nx, by = lin / nx;
+  const int head = by * WH + (w % WH);
   const int kvh = head / G;
   const int rg = w / WH;
 
-  const int b = p.tile_seq[blockIdx.x];
-  const int q0 = p.tile_q0[blockIdx.x];
+  const int b = p.tile_seq[bx];
+  const int q0 = p.tile_q0[bx];
   const int qbeg = p.cu_q[b];
   const int qlen = p.cu_q[b + 1] - qbeg;
   const int ctx = p.ctx_lens ? p.ctx_lens[b] : qlen;
@@ -115,7 +123,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
   // scalar base per chunk, the lane part (row within block, 16-byte chunk) a constant.
   // Rows past the context re-read the last valid key (block clamped here, slot by the
   // clamped key): never a stale slot, whose bytes could be NaN under a zero P.
-  const int kvh_u = blockIdx.y * WH / G;  // == head / G for every wave of the workgroup
+  const int kvh_u = by * WH / G;  // == head / G for every wave of the workgroup
   auto paged_base = [&](int kt, int row) __attribute__((always_inline)) -> long {
     const int last = (ctx - 1) >> p.bs_shift;
     const int bi = __builtin_amdgcn_readfirstlane(min((kt + row) >> p.bs_shift, last));
@@ -461,6 +469,14 @@ static bool prefill_pipe() {
   return env;
 }
 
+static int prefill_xcd() {
+  static const int env = [] {
+    const char* e = getenv("LK_PREFILL_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  return env;
+}
+
 static float prefill_defer() {
   static const float env = [] {
     const char* e = getenv("LK_PREFILL_DEFER");
@@ -490,7 +506,7 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
   while ((1 << bs_shift) < BS) ++bs_shift;
   PrefillParams pr{q, qs, k, v, ks, vs, block_tables, bt_stride, cu_q, ctx_lens, tile_seq,
                    tile_q0, out, os, Hq, Hkv, BS, bs_shift, scale * 1.4426950408889634f, part_o, part_ml,
-                   part_o ? 0.f : prefill_defer(), q_past};
+                   part_o ? 0.f : prefill_defer(), q_past, prefill_xcd()};
   const int WH = G >= 4 ? 4 : G;
   const int NW = prefill_waves(G, D);
   dim3 grid(ntiles, Hq / WH);
