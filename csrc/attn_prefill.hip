@@ -97,8 +97,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
   const int G = p.Hq / p.Hkv;
   // XCD-aware order: the hardware deals workgroups round-robin over the 8 XCDs (each with its own
   // L2); remapped, every XCD walks a contiguous range of (head group, query tile) -- the query
-  // tiles of the same KV head and sequence, which read the same K / V tiles, share one L2
-  // (LK_PREFILL_XCD=0: the plain order)
+  // tiles of the same KV head and sequence, which read the same K / V tiles, share one L2, and
+  // each XCD takes its tiles heaviest first (LK_PREFILL_XCD=0: the plain order)
   const int nx = gridDim.x;
   const int lin = p.xcd ? xcd_remap(blockIdx.y * nx + blockIdx.x, nx * gridDim.y) : blockIdx.y * nx + blockIdx.x;
   const int bx = lin % nx, by = lin / nx;
@@ -506,10 +506,14 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
   while ((1 << bs_shift) < BS) ++bs_shift;
   PrefillParams pr{q, qs, k, v, ks, vs, block_tables, bt_stride, cu_q, ctx_lens, tile_seq,
                    tile_q0, out, os, Hq, Hkv, BS, bs_shift, scale * 1.4426950408889634f, part_o, part_ml,
-                   part_o ? 0.f : prefill_defer(), q_past, prefill_xcd()};
+                   part_o ? 0.f : prefill_defer(), q_past, 0};
   const int WH = G >= 4 ? 4 : G;
   const int NW = prefill_waves(G, D);
   dim3 grid(ntiles, Hq / WH);
+  // XCD-aware order on grids of at most ~2 workgroups per CU slot (the serving chunk, B6 q643 over
+  // 930 keys: 69.5 / 68.4 vs 75.5 / 76.1 us); the long-prefill grids of 8192 workgroups run
+  // 2-6 % faster in the plain order (profiles/r5_flash_xcd/)
+  pr.xcd = prefill_xcd() && (long)ntiles * (Hq / WH) <= 2048;
   const bool pipe = causal && prefill_pipe();
 #define L(DD, C, PG, W, N)                                                        \
   if (pipe) flash_prefill_kernel<DD, C, PG, W, N, true><<<grid, 64 * N, 0, st>>>(pr); \
