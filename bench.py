@@ -425,6 +425,7 @@ def main():
             tp_barrier(engine)
         sync()
         engine.step_trace = []
+        kv_keys0 = engine.runner.decode_kv_keys
         load_host0 = dict(load.host_s) if load is not None else {}
         chars0 = (rag.planned_chars, rag.planned_tokens, rag.planned_requests, rag.planned_evidence)
         ctrl0 = (engine.tp_ctrl.seconds, engine.tp_ctrl.messages) if args.tp > 1 else None
@@ -455,6 +456,9 @@ def main():
             prof.disable()
             prof.dump_stats(f"{os.environ['LK_PROFILE_TIMED']}.rank{rank}")
         trace, engine.step_trace = engine.step_trace, None
+        # K / V bytes the decode attention read in the timed window (this rank's shard): over the
+        # paged-decode kernel time of a timed-window trace, its in-situ bandwidth
+        decode_kv_bytes = (engine.runner.decode_kv_keys - kv_keys0) * llm.kv_bytes_per_token()
         if ctrl0 is not None:  # driver -> TP worker control hop inside the timed window
             tp_ctrl = {"tp_ctrl_s": round(engine.tp_ctrl.seconds - ctrl0[0], 4),
                        "tp_ctrl_us_per_msg": round((engine.tp_ctrl.seconds - ctrl0[0]) * 1e6
@@ -522,6 +526,7 @@ def main():
             "gpu_step_busy_frac": round(sum(t[7] for t in trace) / elapsed, 3) if trace and elapsed else None,
             "avg_prefill_tokens_mixed": round(statistics.mean(t[0] for t in mixed), 1) if mixed else 0,
             "avg_decode_rows": round(statistics.mean(t[1] for t in trace), 1) if trace else 0,
+            "decode_attention_kv_gb": round(decode_kv_bytes / 1e9, 2),
             # device idle between a step's ids copy and the next step's start marker, i.e. the
             # host reached the launch after the device ran dry; by what the host did just before
             "idle_before_launch": _idle_summary(trace),

@@ -130,6 +130,7 @@ class ModelRunner:
         self._stager = (_PinnedStager(self.device) if self.device.type == "cuda"
                         and os.environ.get("LK_PINNED_STAGE", "1") != "0" else None)
         self.gemm_tuning = {}
+        self.decode_kv_keys = 0  # sum over steps of the decode rows' context lengths (prepare())
         if self.device.type == "cuda" and hasattr(model, "gemm_shapes") and self._gemm_tune_on(model):
             # opt-in (LK_GEMM_TUNE=1): pick the prefill GEMM's column tile / K-loop schedule per
             # 256-row M bucket by a cold-weight micro-benchmark at load (< 1 s for Llama-3-8B).
@@ -293,6 +294,8 @@ class ModelRunner:
         the step returns token ids (distributed argmax under TP) instead of logits."""
         si, rows = self._prepare(items)
         si.greedy = bool(greedy)
+        if si.num_decode:  # keys the decode attention reads this step (in-situ bandwidth accounting)
+            self.decode_kv_keys += int(np.asarray(si.ctx_d[: si.num_decode], dtype=np.int64).sum())
         return si, rows
 
     @staticmethod
