@@ -67,11 +67,19 @@ __global__ __launch_bounds__(256) void act_kernel(bf16_t* __restrict__ x,
 #pragma unroll
       for (int j = 0; j < 8; ++j) e[j] = bf2f(f2bf(e[j] + b[j]));
     }
+    if constexpr (KIND == 0) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if constexpr (KIND == 0) e[j] = gelu_erf(e[j]);
-      else if constexpr (KIND == 1) e[j] = gelu_tanh(e[j]);
-      else e[j] = fmaxf(e[j], 0.f);
+      for (int j = 0; j < 4; ++j) {  // pairs: packed fp32 math around the transcendentals
+        const lk_f2 gv = lk_gelu_erf2(lk_f2{e[2 * j], e[2 * j + 1]});
+        e[2 * j] = gv.x;
+        e[2 * j + 1] = gv.y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if constexpr (KIND == 1) e[j] = gelu_tanh(e[j]);
+        else e[j] = fmaxf(e[j], 0.f);
+      }
     }
     store8(x + r * xs + c, e);
   }

@@ -94,6 +94,26 @@ LK_DEVICE float lk_fast_erf(float x) {
   return copysignf(y, x);
 }
 LK_DEVICE float lk_gelu_erf(float x) { return 0.5f * x * (1.f + lk_fast_erf(x * 0.70710678118654752f)); }
+// The same GELU on two values: the polynomial and the products as packed fp32 ops (v_pk_fma_f32 /
+// v_pk_mul_f32, two values per issue) around the two scalar transcendentals -- the epilogue of the
+// encoder's bias + GELU projection was VALU-bound (+19 % over the bias epilogue at K 768:
+// benchmarks/epi_cost.py)
+typedef float lk_f2 __attribute__((ext_vector_type(2)));
+LK_DEVICE lk_f2 lk_gelu_erf2(lk_f2 x) {
+  const lk_f2 z = x * 0.70710678118654752f;
+  const lk_f2 a = __builtin_elementwise_abs(z);
+  const lk_f2 d = __builtin_elementwise_fma(a, (lk_f2){0.3275911f, 0.3275911f}, (lk_f2){1.f, 1.f});
+  const lk_f2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  lk_f2 p = __builtin_elementwise_fma((lk_f2){1.061405429f, 1.061405429f}, t, (lk_f2){-1.453152027f, -1.453152027f});
+  p = __builtin_elementwise_fma(p, t, (lk_f2){1.421413741f, 1.421413741f});
+  p = __builtin_elementwise_fma(p, t, (lk_f2){-0.284496736f, -0.284496736f});
+  p = __builtin_elementwise_fma(p, t, (lk_f2){0.254829592f, 0.254829592f});
+  const lk_f2 na = -(a * a);
+  const lk_f2 e = {__expf(na.x), __expf(na.y)};
+  const lk_f2 y = 1.f - p * t * e;
+  const lk_f2 erf = {copysignf(y.x, z.x), copysignf(y.y, z.y)};
+  return 0.5f * x * (1.f + erf);
+}
 
 // Bijective XCD-aware remap of a flat workgroup id (8 XCDs, round-robin dispatch):
 // consecutive logical tiles land on the same XCD so they share its L2.

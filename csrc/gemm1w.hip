@@ -494,9 +494,8 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
           }
         }
       }
-      auto act = [&](float e, float b) {
+      auto act = [&](float e, float b) {  // (GELU: applied pairwise below)
         if constexpr (EPI != E_NONE) e = rbf(e + b);
-        if constexpr (EPI == E_BIAS_GELU) e = lk_gelu_erf(e);
         if constexpr (EPI == E_BIAS_RELU) e = fmaxf(e, 0.f);
         return e;
       };
@@ -510,6 +509,14 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
           for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int v = 0; v < 4; ++v) y[4 * h + v] = act(acc[m][2 * p + h][v] * scm[m], bv[2 * p + h][v]);
+          if constexpr (EPI == E_BIAS_GELU) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const lk_f2 gv = lk_gelu_erf2(lk_f2{y[2 * j], y[2 * j + 1]});
+              y[2 * j] = gv.x;
+              y[2 * j + 1] = gv.y;
+            }
+          }
           __builtin_amdgcn_raw_buffer_store_b128(pk8(y), os, rb + 64 * p, 0, 0);
         }
       }
