@@ -73,6 +73,7 @@ struct PrefillParams {
   // negative or past the keys: this rank holds only a shard of the keys); null = ctx - q_len
   const int* q_past;
   int xcd;  // XCD-aware workgroup order (prefill_xcd())
+  int btv;  // block-table entries preloaded per lane (LK_PREFILL_BTV, default 1)
 };
 
 // NW waves per workgroup (4 or 8): WH of them share a row group (one head each), and
@@ -124,10 +125,26 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_prefill_kernel(PrefillP
   // Rows past the context re-read the last valid key (block clamped here, slot by the
   // clamped key): never a stale slot, whose bytes could be NaN under a zero P.
   const int kvh_u = by * WH / G;  // == head / G for every wave of the workgroup
+  // The sequence's first 64 NBV block-table entries, one per lane, read once: a chunk's block
+  // lookup is then a v_readlane instead of a scalar load whose lgkmcnt wait also drained the
+  // wave's LDS reads (blocks past them: the scalar load)
+  constexpr int NBV = 2;
+  int btv[NBV];
+  if (PAGED && p.btv) {
+    const int nblk = (ctx + p.BS - 1) >> p.bs_shift;
+#pragma unroll
+    for (int j = 0; j < NBV; ++j) {
+      const int bi = lane + 64 * j;
+      btv[j] = bi < nblk ? p.block_tables[(long)b * p.bt_stride + bi] : 0;
+    }
+  }
   auto paged_base = [&](int kt, int row) __attribute__((always_inline)) -> long {
     const int last = (ctx - 1) >> p.bs_shift;
     const int bi = __builtin_amdgcn_readfirstlane(min((kt + row) >> p.bs_shift, last));
-    const long blk = p.block_tables[(long)b * p.bt_stride + bi];
+    long blk;
+    if (p.btv && bi < 64) blk = __builtin_amdgcn_readlane(btv[0], bi);
+    else if (p.btv && bi < 128) blk = __builtin_amdgcn_readlane(btv[1], bi - 64);
+    else blk = p.block_tables[(long)b * p.bt_stride + bi];
     return ((blk * p.Hkv + kvh_u) << p.bs_shift) * D;
   };
 
@@ -469,6 +486,14 @@ static bool prefill_pipe() {
   return env;
 }
 
+static int prefill_btv() {
+  static const int env = [] {
+    const char* e = getenv("LK_PREFILL_BTV");
+    return e ? atoi(e) : 1;
+  }();
+  return env;
+}
+
 static int prefill_xcd() {
   static const int env = [] {
     const char* e = getenv("LK_PREFILL_XCD");
@@ -506,7 +531,7 @@ int lk_flash_prefill(const bf16_t* q, long qs, const bf16_t* k, const bf16_t* v,
   while ((1 << bs_shift) < BS) ++bs_shift;
   PrefillParams pr{q, qs, k, v, ks, vs, block_tables, bt_stride, cu_q, ctx_lens, tile_seq,
                    tile_q0, out, os, Hq, Hkv, BS, bs_shift, scale * 1.4426950408889634f, part_o, part_ml,
-                   part_o ? 0.f : prefill_defer(), q_past, 0};
+                   part_o ? 0.f : prefill_defer(), q_past, 0, prefill_btv()};
   const int WH = G >= 4 ? 4 : G;
   const int NW = prefill_waves(G, D);
   dim3 grid(ntiles, Hq / WH);

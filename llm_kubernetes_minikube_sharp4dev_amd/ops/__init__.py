@@ -741,14 +741,30 @@ def linear_add_rmsnorm(x, w, residual, norm_w, eps: float):
 
 def linear_rope_kv(x, w, positions, cos_sin, Hq: int, Hkv: int, D: int, k_cache=None, v_cache=None,
                    slots=None, neox: bool = True, write_k_inplace: bool = False):
-    """qkv = x W^T, then :func:`rope_kv_` on it (one launch fewer on split-K decode shapes)."""
+    """qkv = x W^T, then :func:`rope_kv_` on it (one launch fewer on split-K decode shapes; on
+    prefill-sized steps of a folded model -- interleaved RoPE, e.g. the tensor-parallel block,
+    where the whole fused chain does not apply -- the QKV GEMM's epilogue does the RoPE and the
+    paged-KV write)."""
     plan = _ws_split_plan(x, w)
     if plan is not None:
         return lib().ws_linear_rope_kv(x, w, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache, slots, neox,
                                        write_k_inplace, plan[0], plan[1])
+    if _qkv_epilogue_ok(x, w, neox, write_k_inplace, k_cache, slots):
+        return linear_qkv_fused(x, w, None, 1e-5, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache, slots)
     qkv = linear(x, w)
     rope_kv_(qkv, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache, slots, neox, write_k_inplace)
     return qkv
+
+
+def _qkv_epilogue_ok(x, w, neox: bool, write_k_inplace: bool, k_cache, slots) -> bool:
+    if neox or write_k_inplace or not PREFILL_CHAIN or GEMM_LIBRARY or not _gemm_ok(x, w):
+        return False
+    if x.shape[0] <= WS_MAX_M or (k_cache is not None and slots is None):
+        return False
+    M, K = x.shape
+    N = w.shape[0]
+    c = _cfg_of(M, N, K, 0)
+    return c is not None and c[2] == 1 and lib().gemm_supported(M, N, K, EPI_QKV, c[1], 1, c[0])
 
 
 # ---------------------------------------------------------------- fused prefill chain

@@ -884,6 +884,23 @@ def test_gemm_qkv_epilogue(hip, M, bn, variant, scaled):
     assert hip.gemm_streamk(-1) == 0
 
 
+@pytest.mark.parametrize("M,Hq,Hkv", [(1111, 32, 8), (2664, 32, 8)])
+def test_linear_rope_kv_epilogue_matches_unfused(hip, monkeypatch, M, Hq, Hkv):
+    """Prefill-sized QKV outside the fused chain (the TP block's path): RoPE and the paged-KV
+    write run in the QKV GEMM's epilogue (128- / 192-row gemm1w tiles at these M), matching
+    GEMM -> rope_kv_ (interleaved pairs)."""
+    x, w, pos, cs, slots, kc, vc = _qkv_setup(M, Hq=Hq, Hkv=Hkv, H=4096, seed=M)
+    kc2, vc2 = kc.clone(), vc.clone()
+    assert ops._qkv_epilogue_ok(x, w, False, False, kc, slots)
+    got = ops.linear_rope_kv(x, w, pos, cs, Hq, Hkv, 128, kc, vc, slots, neox=False)
+    monkeypatch.setattr(ops, "PREFILL_CHAIN", False)
+    want = ops.linear_rope_kv(x, w, pos, cs, Hq, Hkv, 128, kc2, vc2, slots, neox=False)
+    torch.cuda.synchronize()
+    _close(got, want, 0.02, 0.01, f"qkv epilogue vs unfused M{M}")
+    _close(kc, kc2, 0.02, 0.01, "k cache")
+    _close(vc, vc2, 0.02, 0.01, "v cache")
+
+
 def test_gemm_qkv_epilogue_layout(hip):
     """Asymmetric exact data through the QKV epilogue: x = I-rows, W rows = distinct ramps, RoPE at
     position 0 (identity): every output column / cache element lands where the reference puts it."""
