@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
                                                         const bf16_t* __restrict__ W,
                                                         const bf16_t* __restrict__ bias, int M, int K, int I,
                                                         bf16_t* __restrict__ out, long ldo, int TM, int TN,
-                                                        int group_m, LkEpi ea) {
+                                                        int tn0, int group_m, LkEpi ea) {
   constexpr bool SC = SCP > 0;
   static_assert(!SC || scalable(EPI), "row scale");
   static_assert(!PERSIST || (persistable(EPI) && !SC), "persistent walk: plain / bias epilogues");
@@ -155,10 +155,10 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
     const int first = (L / per_group) * group_m;
     const int gm = min(TM - first, group_m);
     tm = first + (L % per_group) % gm;
-    tn = (L % per_group) / gm;
+    tn = tn0 + (L % per_group) / gm;  // (tn0: a column-split launch's first column tile)
   };
   const u32x4_t xsrd = srd(X, (long)M * ldx * 2);
-  const u32x4_t wsrd = srd(W, (long)(EPI == E_SWIGLU ? 2 * I : TN * kBN) * K * 2);
+  const u32x4_t wsrd = srd(W, (long)(EPI == E_SWIGLU ? 2 * I : (tn0 + TN) * kBN) * K * 2);
   const unsigned lds0 = static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_ptr_t)smem));
   const unsigned ldsx = rfl(lds0 + (BM / 4) * w * kRowB), ldsw = rfl(lds0 + kOpX + 64 * w * kRowB);
 
@@ -432,46 +432,81 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
       if (tid < BM && row < M) ea.ss_out[(long)tn * ea.ss_out_ld + row] = red[tid] + red[BM + tid];
     } else if constexpr (EPI == E_QKV) {
       // RoPE (interleaved pairs) on the q / k heads + the paged-KV scatter, on the bf16-rounded
-      // (row-scaled) projection: the values "GEMM -> rope_kv_" would leave
+      // (row-scaled) projection: the values "GEMM -> rope_kv_" would leave.  Everything that
+      // depends only on the lane's columns is hoisted out of the row loop (no integer division
+      // per row), the rows' positions / slots are loaded in one round before any store (a u32
+      // store may alias the int metadata, so per-row loads would each wait behind the previous
+      // row's stores), and the next row's cos / sin are in flight while this row is rotated.
       const int qcols = ea.hq * ea.hd, kcols = ea.hkv * ea.hd, half = ea.hd >> 1;
+      const int cb = tn * kBN + wc * 128;
+      int i0[4], coff[4];
+      bool rot[4], kv[4], isv[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int c = cb + 32 * p + 8 * g;
+        rot[p] = c < qcols + kcols;
+        kv[p] = c >= qcols;
+        isv[p] = c >= qcols + kcols;
+        i0[p] = (c % ea.hd) >> 1;  // first rotation pair
+        const int cc = c - qcols - (isv[p] ? kcols : 0);
+        const int h = cc / ea.hd;
+        coff[p] = h * ea.bs * ea.hd + (cc - h * ea.hd);  // head h, dim d within a cache block
+      }
+      const long blk_stride = (long)ea.hkv * ea.bs * ea.hd;
+      int posv[MB], slotv[MB];
 #pragma unroll
       for (int m = 0; m < MB; ++m) {
         const int row = tm * BM + wr * WM + m * 16 + r;
-        if (row >= M) continue;
-        const float sc = scm[m];
-        const int pos = ea.pos[row];
-        const int slot = ea.slots ? ea.slots[row] : -1;
+        const int rc = min(row, M - 1);  // unconditional loads: no branch per row around them
+        posv[m] = ea.pos[rc];
+        slotv[m] = ea.slots ? ea.slots[rc] : -1;
+      }
+      floatx4 c4[4], s4[4];
+      auto load_cs = [&](int pos, floatx4 (&cv)[4], floatx4 (&sv)[4]) {
         const float* cs = ea.cos_sin + (long)pos * ea.hd;
-        bf16_t* orow = out + (long)row * ldo;
-        const int cb = tn * kBN + wc * 128;
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          const int c = cb + 32 * p + 8 * g;
-          float y[8];
+        for (int p = 0; p < 4; ++p) {  // (loaded for v columns too: in range, and branch-free)
+          cv[p] = *reinterpret_cast<const floatx4*>(cs + i0[p]);
+          sv[p] = *reinterpret_cast<const floatx4*>(cs + half + i0[p]);
+        }
+      };
+      load_cs(posv[0], c4, s4);
 #pragma unroll
-          for (int h = 0; h < 2; ++h)
+      for (int m = 0; m < MB; ++m) {
+        floatx4 c4n[4], s4n[4];
+        if (m + 1 < MB) load_cs(posv[m + 1], c4n, s4n);
+        const int row = tm * BM + wr * WM + m * 16 + r;
+        if (row < M) {
+          const float sc = scm[m];
+          const int slot = slotv[m];
+          const long kvb = slot >= 0 ? (long)(slot / ea.bs) * blk_stride + (long)(slot % ea.bs) * ea.hd : 0;
+          bf16_t* orow = out + (long)row * ldo;
 #pragma unroll
-            for (int v = 0; v < 4; ++v) y[4 * h + v] = rbf(acc[m][2 * p + h][v] * sc);
-          if (c < qcols + kcols) {
-            const int i0 = (c % ea.hd) >> 1;  // first rotation pair
-            const floatx4 c4 = *reinterpret_cast<const floatx4*>(cs + i0);
-            const floatx4 s4 = *reinterpret_cast<const floatx4*>(cs + half + i0);
+          for (int p = 0; p < 4; ++p) {
+            float y[8];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const float a = y[2 * q], b = y[2 * q + 1];
-              y[2 * q] = a * c4[q] - b * s4[q];
-              y[2 * q + 1] = b * c4[q] + a * s4[q];
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+              for (int v = 0; v < 4; ++v) y[4 * h + v] = rbf(acc[m][2 * p + h][v] * sc);
+            if (rot[p]) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const float a = y[2 * q], b = y[2 * q + 1];
+                y[2 * q] = a * c4[p][q] - b * s4[p][q];
+                y[2 * q + 1] = b * c4[p][q] + a * s4[p][q];
+              }
             }
+            const u32x4_t pk = pk8(y);
+            *reinterpret_cast<u32x4_t*>(orow + cb + 32 * p + 8 * g) = pk;
+            if (kv[p] && slot >= 0 && ea.kc != nullptr)
+              *reinterpret_cast<u32x4_t*>((isv[p] ? ea.vc : ea.kc) + kvb + coff[p]) = pk;
           }
-          const u32x4_t pk = pk8(y);
-          *reinterpret_cast<u32x4_t*>(orow + c) = pk;
-          if (c >= qcols && slot >= 0 && ea.kc != nullptr) {
-            const bool isv = c >= qcols + kcols;
-            const int cc = c - qcols - (isv ? kcols : 0);
-            const int h = cc / ea.hd, d = cc - h * ea.hd;
-            bf16_t* dst = (isv ? ea.vc : ea.kc) + (((long)(slot / ea.bs) * ea.hkv + h) * ea.bs + slot % ea.bs) * ea.hd + d;
-            *reinterpret_cast<u32x4_t*>(dst) = pk;
-          }
+        }
+        // one row of cos / sin in flight, not all MB (hoisted, they would take MB x 32 VGPRs)
+        asm volatile("" ::: "memory");
+        if (m + 1 < MB) {
+#pragma unroll
+          for (int p = 0; p < 4; ++p) c4[p] = c4n[p], s4[p] = s4n[p];
         }
       }
     } else {  // NONE / BIAS / BIAS_GELU / BIAS_RELU
@@ -482,7 +517,7 @@ __global__ __launch_bounds__(256, 1) void gemm1w_kernel(const bf16_t* __restrict
 #pragma unroll
         for (int v = 0; v < 4; ++v) bv[n][v] = 0.f;
       if constexpr (EPI != E_NONE) {
-        const auto bs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(bias), 0, TN * kBN * 2, 0x00020000);
+        const auto bs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(bias), 0, (tn0 + TN) * kBN * 2, 0x00020000);
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
           const u32x4_t b = __builtin_amdgcn_raw_buffer_load_b128(bs, (unsigned)((tn * kBN + wc * 128 + 32 * p + 8 * g) * 2), 0, 0);
@@ -618,7 +653,7 @@ int persist_kt() {
 
 template <int EPI, int SCP, int BM, bool PERSIST = false>
 void launch1w_p(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
-                long ldo, int TN, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
+                long ldo, int TN, int tn0, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
   constexpr int lds = Tile<BM>::kLds;
   static bool attr = false;
   if (!attr) {
@@ -629,44 +664,69 @@ void launch1w_p(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, 
   const int TM = (M + BM - 1) / BM;
   const int grid = PERSIST ? min(TM * TN, cu_count()) : TM * TN;
   gemm1w_kernel<EPI, SCP, BM, PERSIST><<<dim3(grid, ks), 256, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN,
-                                                                       group_m > 0 ? group_m : group1w(), ea);
+                                                                       tn0, group_m > 0 ? group_m : group1w(), ea);
 }
 template <int EPI, int SCP, int BM>
 void launch1w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
-              long ldo, int TN, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
+              long ldo, int TN, int tn0, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
   if constexpr (persistable(EPI) && SCP == 0 && BM == 256) {
     const int tiles = ((M + BM - 1) / BM) * TN;
     if (ks == 1 && K / kBK <= persist_kt() && tiles > 2 * cu_count()) {
-      launch1w_p<EPI, SCP, BM, true>(x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
+      launch1w_p<EPI, SCP, BM, true>(x, ldx, w, bias, M, K, I, out, ldo, TN, tn0, ks, group_m, st, ea);
       return;
     }
   }
-  launch1w_p<EPI, SCP, BM, false>(x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
+  launch1w_p<EPI, SCP, BM, false>(x, ldx, w, bias, M, K, I, out, ldo, TN, tn0, ks, group_m, st, ea);
 }
 template <int EPI, int SCP>
 void launch1w_bm(int bm, const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I,
-                 bf16_t* out, long ldo, int TN, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
-  if (bm == 192) launch1w<EPI, SCP, 192>(x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
-  else if (bm == 128) launch1w<EPI, SCP, 128>(x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
-  else launch1w<EPI, SCP, 256>(x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
+                 bf16_t* out, long ldo, int TN, int tn0, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
+  if (bm == 192) launch1w<EPI, SCP, 192>(x, ldx, w, bias, M, K, I, out, ldo, TN, tn0, ks, group_m, st, ea);
+  else if (bm == 128) launch1w<EPI, SCP, 128>(x, ldx, w, bias, M, K, I, out, ldo, TN, tn0, ks, group_m, st, ea);
+  else launch1w<EPI, SCP, 256>(x, ldx, w, bias, M, K, I, out, ldo, TN, tn0, ks, group_m, st, ea);
+}
+template <int EPI, int SCP>
+void launch1w_tiles(int bm, const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I,
+                    bf16_t* out, long ldo, int TN, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
+  if (bm == LK_GEMM1W_SPLIT128 || bm == LK_GEMM1W_SPLIT192) {
+    // column split: the column tiles that fill whole waves of the CUs with 256-row tiles, then
+    // the rest -- less than one wave of 256-row tiles -- on smaller row tiles that fill one.
+    // The QKV projection at M 4096 (16 x 24 tiles = 1.5 waves of 256 CUs) runs 16 x 16 256-row
+    // tiles, then 32 x 8 128-row tiles: 1 + ~0.6 tile times instead of 2.
+    const int ca = lk_gemm1w_split_cols(M, TN, cu_count());
+    if (ca > 0 && ca < TN) {
+      launch1w_bm<EPI, SCP>(256, x, ldx, w, bias, M, K, I, out, ldo, ca, 0, ks, group_m, st, ea);
+      launch1w_bm<EPI, SCP>(bm == LK_GEMM1W_SPLIT128 ? 128 : 192, x, ldx, w, bias, M, K, I, out, ldo, TN - ca, ca, ks,
+                            group_m, st, ea);
+      return;
+    }
+    bm = 256;
+  }
+  launch1w_bm<EPI, SCP>(bm, x, ldx, w, bias, M, K, I, out, ldo, TN, 0, ks, group_m, st, ea);
 }
 template <int EPI>
 void launch1w_sc(int bm, const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I,
                  bf16_t* out, long ldo, int TN, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
   if constexpr (scalable(EPI)) {
     if (ea.ss_in != nullptr) {
-      if (ea.ss_nt <= 16) launch1w_bm<EPI, 16>(bm, x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
-      else launch1w_bm<EPI, 32>(bm, x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
+      if (ea.ss_nt <= 16) launch1w_tiles<EPI, 16>(bm, x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
+      else launch1w_tiles<EPI, 32>(bm, x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
       return;
     }
   }
-  launch1w_bm<EPI, 0>(bm, x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
+  launch1w_tiles<EPI, 0>(bm, x, ldx, w, bias, M, K, I, out, ldo, TN, ks, group_m, st, ea);
 }
 
 }  // namespace
 
+int lk_gemm1w_split_cols(int M, int TN, int cus) {
+  const int tm = (M + 255) / 256;
+  const int waves = tm * TN / cus;  // whole waves of 256-row tiles
+  return min(TN, waves * cus / tm);
+}
+
 int lk_gemm1w_supported(int M, int N, int K, int epi, int ks, int bm) {
-  if (bm != 256 && bm != 192 && bm != 128) return 0;
+  if (bm != 256 && bm != 192 && bm != 128 && bm != LK_GEMM1W_SPLIT128 && bm != LK_GEMM1W_SPLIT192) return 0;
   if (M < 1 || K % kBK || ks < 1 || ks > 8 || K / kBK < 3 * ks) return 0;  // >= 3 K-tiles per split
   if (ks > 1 && (epi == E_SWIGLU || epi == E_QKV || N % 256)) return 0;
   if (epi == E_SWIGLU) return N % 2 == 0 && (N / 2) % 128 == 0;
@@ -690,14 +750,15 @@ int lk_gemm1w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, in
   if (epi >= E_BIAS && epi <= E_BIAS_RELU && bias == nullptr) return -1;
   if ((long)N * K * 2 >= 0x7FFFFFF0L) return -1;
   // 32-bit buffer offsets: X, the output (fp32 partials for split-K) and the residual in row chunks
-  const int TMall = (M + bm - 1) / bm;
-  const long rows_pad = (long)TMall * bm;
+  const int bmx = bm < 128 ? 256 : bm;  // (a column split's largest row tile)
+  const int TMall = (M + bmx - 1) / bmx;
+  const long rows_pad = (long)TMall * bmx;
   const long xb = rows_pad * ldx * 2, ob = rows_pad * ldo * (ks > 1 ? 4 * ks : 2), rb = epi == E_RESID ? rows_pad * ea.ldr * 2 : 0;
   if (xb >= 0x7FFFFFF0L || ob >= 0x7FFFFFF0L || rb >= 0x7FFFFFF0L) {
     if (ea_ || ks > 1) return -1;  // (the fused chain indexes whole-M side buffers)
     const long per = max(ldx, ldo) * 2;
-    const long max_rows = (0x7FFFFFF0L / per) / bm * bm - bm;
-    if (max_rows < bm) return -1;
+    const long max_rows = (0x7FFFFFF0L / per) / bmx * bmx - bmx;
+    if (max_rows < bmx) return -1;
     for (long m0 = 0; m0 < M; m0 += max_rows) {
       const int mc = (int)min((long)M - m0, max_rows);
       const int rc = lk_gemm1w(x + m0 * ldx, ldx, w, bias, mc, N, K, epi, out + m0 * ldo, ldo, st, 1, nullptr, nullptr,
@@ -729,10 +790,10 @@ int lk_gemm1w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, in
   switch (epi) {
     case E_NONE: launch1w_sc<E_NONE>(bm, x, ldx, w, bias, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
     case E_SWIGLU: launch1w_sc<E_SWIGLU>(bm, x, ldx, w, bias, M, K, N / 2, out, ldo, N / 256, 1, group_m, st, ea); break;
-    case E_BIAS: launch1w_bm<E_BIAS, 0>(bm, x, ldx, w, bias, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
-    case E_BIAS_GELU: launch1w_bm<E_BIAS_GELU, 0>(bm, x, ldx, w, bias, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
-    case E_BIAS_RELU: launch1w_bm<E_BIAS_RELU, 0>(bm, x, ldx, w, bias, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
-    case E_RESID: launch1w_bm<E_RESID, 0>(bm, x, ldx, w, nullptr, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
+    case E_BIAS: launch1w_tiles<E_BIAS, 0>(bm, x, ldx, w, bias, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
+    case E_BIAS_GELU: launch1w_tiles<E_BIAS_GELU, 0>(bm, x, ldx, w, bias, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
+    case E_BIAS_RELU: launch1w_tiles<E_BIAS_RELU, 0>(bm, x, ldx, w, bias, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
+    case E_RESID: launch1w_tiles<E_RESID, 0>(bm, x, ldx, w, nullptr, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
     case E_QKV: launch1w_sc<E_QKV>(bm, x, ldx, w, nullptr, M, K, 0, out, ldo, N / kBN, 1, group_m, st, ea); break;
     default: return -1;
   }

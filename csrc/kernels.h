@@ -100,7 +100,15 @@ int lk_gemm(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int 
 // every lk_gemm epilogue); lk_gemm routes variants 3 / 4 / 5 here (row tile bm = 256 / 192 / 128).
 // Needs K % 64 == 0 and >= 3 K-tiles per split, N % 256 == 0 (SwiGLU: N/2 % 128).
 // group_m <= 0: LK_GEMM_GROUP_M (4).
-inline int lk_gemm1w_bm(int variant) { return variant == 3 ? 256 : variant == 4 ? 192 : variant == 5 ? 128 : 0; }
+// Variants 6 / 7: a column split -- the column tiles that fill whole waves of the CUs on 256-row
+// tiles, the remaining (less than a wave) on 128 / 192-row tiles, as two launches.
+constexpr int LK_GEMM1W_SPLIT128 = 1, LK_GEMM1W_SPLIT192 = 2;
+inline int lk_gemm1w_bm(int variant) {
+  return variant == 3 ? 256 : variant == 4 ? 192 : variant == 5 ? 128 : variant == 6 ? LK_GEMM1W_SPLIT128
+       : variant == 7 ? LK_GEMM1W_SPLIT192 : 0;
+}
+// 256-wide column tiles of a variant 6 / 7 split that run on 256-row tiles (0 or all: no split)
+int lk_gemm1w_split_cols(int M, int TN, int cus);
 int lk_gemm1w_supported(int M, int N, int K, int epi, int ks, int bm = 256);
 int lk_gemm1w(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int N, int K, int epi,
               bf16_t* out, long ldo, hipStream_t st, int ks, float* ws, const LkEpi* ea, int group_m, int bm = 256);

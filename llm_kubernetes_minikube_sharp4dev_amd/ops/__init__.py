@@ -434,7 +434,24 @@ def _gemm_key(M: int, N: int, K: int, epi: int):
 # LK_GEMM1W=0 restores round 4's gemm.hip-only choice.
 GEMM1W = os.environ.get("LK_GEMM1W", "1") != "0"
 GEMM1W_MIN_TILES = 256
-GEMM1W_BM = {3: 256, 4: 192, 5: 128}
+GEMM1W_BM = {3: 256, 4: 192, 5: 128, 6: 256, 7: 256}
+# Variants 6 / 7: column split (csrc/gemm1w.hip launch1w_tiles) -- the column tiles that fill whole
+# waves of the CUs on 256-row tiles, the rest (under a wave) on 128 / 192-row tiles, two launches.
+# QKV at M 4096 = 16 x 24 256-row tiles = 1.5 waves: 16 x 16 tiles, then 32 x 8 128-row tiles.
+GEMM1W_SPLIT = {6: 128, 7: 192}
+SPLIT_ON = os.environ.get("LK_GEMM_SPLIT", "1") != "0"  # 0: measured 6 / 7 entries run as variant 3 (A/B)
+
+
+def gemm1w_split_cols(M: int, N: int, epi: int, cus: int = 256) -> int:
+    """Column tiles a variant 6 / 7 launch runs on 256-row tiles (mirrors lk_gemm1w_split_cols);
+    0 or all of them: no split (the launch is variant 3's)."""
+    tn = N // 256
+    tm = (M + 255) // 256
+    return min(tn, (tm * tn // cus) * cus // tm)
+
+
+def _split_applies(M: int, N: int, epi: int) -> bool:
+    return 0 < gemm1w_split_cols(M, N, epi) < N // 256
 
 
 def _gemm_configs(N: int, epi: int):
@@ -562,6 +579,8 @@ def tune_gemm(weights, max_m: int, min_m: int = 512, iters: int = 6, cold_bytes:
             x = xmax[:M]
             cfgs = []
             for v, bn in _gemm_configs(N, epi):
+                if v in GEMM1W_SPLIT and not _split_applies(M, N, epi):
+                    continue  # the same launch as variant 3
                 ks = 1 if v in GEMM1W_BM else _gemm_splits(M, N, K, epi, bn)
                 if not L.gemm_supported(M, N, K, epi, bn, ks, v):
                     ks = 1
@@ -791,6 +810,8 @@ def _cfg_of(M: int, N: int, K: int, epi: int):
         cfg = _static_cfg(key)
         if cfg is not None and (not GEMM1W and cfg[0] in GEMM1W_BM):
             cfg = None
+        elif cfg is not None and not SPLIT_ON and cfg[0] in GEMM1W_SPLIT:
+            cfg = (3, 256, 1)
     return cfg if cfg is not None else _gemm_default(M, N, K, epi)
 
 

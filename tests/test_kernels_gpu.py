@@ -825,7 +825,7 @@ def _qkv_setup(M, Hq=32, Hkv=8, D=128, H=4096, nb=600, bs=16, seed=0):
 
 @pytest.mark.parametrize("M,N,K,splits", [(300, 1024, 512, 1), (1000, 4096, 1024, 1), (2304, 4096, 14336, 3),
                                           (777, 2048, 4096, 2), (4352, 4096, 4096, 1), (2664, 4096, 4096, 1)])
-@pytest.mark.parametrize("variant", [2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [2, 3, 4, 5, 6])
 def test_gemm_resid_epilogue(hip, M, N, K, splits, variant):
     """RESID (producer side of the folded norm): r = bf16(r + bf16(x W^T)) in place and the
     per-256-column partial sums of squares of the new r, in-kernel and through the split-K
@@ -865,7 +865,8 @@ def test_gemm_swiglu_row_scale(hip, M, scaled, variant, H):
 
 @pytest.mark.parametrize("M,bn,variant", [(300, 192, 2), (1111, 256, 2), (4352, 192, 2), (2560, 256, 2),
                                           (300, 256, 3), (1111, 256, 3), (4352, 256, 3), (2664, 256, 4),
-                                          (300, 256, 4), (2664, 256, 5), (1111, 256, 5)])
+                                          (300, 256, 4), (2664, 256, 5), (1111, 256, 5), (4352, 256, 6),
+                                          (4000, 256, 7)])
 @pytest.mark.parametrize("scaled", [False, True])
 def test_gemm_qkv_epilogue(hip, M, bn, variant, scaled):
     """QKV epilogue: row scale, interleaved-pair RoPE on q / k, K / V into the paged cache at
@@ -884,6 +885,29 @@ def test_gemm_qkv_epilogue(hip, M, bn, variant, scaled):
     assert hip.gemm_streamk(-1) == 0
 
 
+@pytest.mark.parametrize("variant", [6, 7])
+@pytest.mark.parametrize("M,N,K,epi", [(4000, 6144, 512, 0), (4352, 4096, 768, 3), (600, 28672, 512, 1),
+                                       (6000, 3072, 768, 2)])
+def test_gemm1w_column_split(hip, variant, M, N, K, epi):
+    """Variants 6 / 7: the column tiles that fill whole waves on 256-row tiles, the rest on 128 /
+    192-row tiles (two launches, the second offset by tn0 column tiles) -- every column, bias and
+    SwiGLU pair lands where the one-launch kernel puts it."""
+    assert ops._split_applies(M, N, epi), "shape must engage the split"
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16) if epi >= 2 else None
+    got = hip.gemm(x, w, b, epi, 256, None, variant, 1)
+    y = x.float() @ w.float().t()
+    if epi == 1:
+        I = N // 2
+        y = torch.nn.functional.silu(y[:, :I].bfloat16().float()) * y[:, I:].bfloat16().float()
+    elif epi >= 2:
+        y = y.bfloat16().float() + b.float()
+        y = torch.nn.functional.gelu(y) if epi == 3 else y
+    _close(got, y, 0.03, 0.02, f"split v{variant} epi{epi} M{M} N{N}")
+
+
 @pytest.mark.parametrize("M,Hq,Hkv", [(1111, 32, 8), (2664, 32, 8)])
 def test_linear_rope_kv_epilogue_matches_unfused(hip, monkeypatch, M, Hq, Hkv):
     """Prefill-sized QKV outside the fused chain (the TP block's path): RoPE and the paged-KV
@@ -896,7 +920,9 @@ def test_linear_rope_kv_epilogue_matches_unfused(hip, monkeypatch, M, Hq, Hkv):
     monkeypatch.setattr(ops, "PREFILL_CHAIN", False)
     want = ops.linear_rope_kv(x, w, pos, cs, Hq, Hkv, 128, kc2, vc2, slots, neox=False)
     torch.cuda.synchronize()
-    _close(got, want, 0.02, 0.01, f"qkv epilogue vs unfused M{M}")
+    qd, kd = Hq * 128, (Hq + Hkv) * 128  # k columns of the row: rotated by the epilogue, unused (K is read from the cache)
+    _close(got[:, :qd], want[:, :qd], 0.02, 0.01, f"q: epilogue vs unfused M{M}")
+    _close(got[:, kd:], want[:, kd:], 0.02, 0.01, f"v: epilogue vs unfused M{M}")
     _close(kc, kc2, 0.02, 0.01, "k cache")
     _close(vc, vc2, 0.02, 0.01, "v cache")
 
