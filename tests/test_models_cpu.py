@@ -346,7 +346,7 @@ def test_static_gemm_table_is_well_formed(monkeypatch):
     doc = json.load(open(ops.GEMM_TABLE_FILE))
     assert doc["arch"] == "gfx950" and doc["entries"]
     for mb, n, k, epi, v, bn, ks in doc["entries"]:
-        assert v in (0, 1, 2, 3, 4, 5) and bn in (192, 256) and 1 <= ks <= 4 and epi in (0, 1, 2, 3, 4)
+        assert v in (0, 1, 2, 3, 4, 5, 6, 7) and bn in (192, 256) and 1 <= ks <= 4 and epi in (0, 1, 2, 3, 4)
         assert bn == 256 or v not in ops.GEMM1W_BM
         assert ks == 1 or v not in ops.GEMM1W_BM
         assert k % 64 == 0 and n % bn == 0
@@ -455,3 +455,16 @@ def test_fused_chain_reference_ops():
     y = R.gemm_scaled(r2, wg, ss, H, 1e-5)
     normed = r2 * torch.rsqrt(r2.pow(2).mean(-1, keepdim=True) + 1e-5)
     assert torch.allclose(y, normed @ wg.t(), atol=1e-4)
+
+
+def test_gemm1w_column_split_plan():
+    """Variants 6 / 7 split the column tiles: whole waves of 256-row tiles first (mirrors
+    lk_gemm1w_split_cols in csrc/gemm1w.hip)."""
+    from llm_kubernetes_minikube_sharp4dev_amd import ops
+
+    assert ops.gemm1w_split_cols(4096, 6144, 0) == 16  # 16 x 24 = 1.5 waves -> 16 x 16, then 8 columns
+    assert ops._split_applies(4096, 6144, 0)
+    assert not ops._split_applies(4096, 4096, 0)  # 16 x 16: exactly one wave
+    assert not ops._split_applies(8192, 6144, 0)  # 32 x 24: three waves
+    assert not ops._split_applies(1024, 4096, 0)  # under a wave: nothing to split
+    assert ops.gemm1w_split_cols(600, 28672, 1) == 85  # SwiGLU: 3 x 112 tiles
