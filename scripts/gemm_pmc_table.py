@@ -4,8 +4,9 @@ runs (scripts/gpu_gemm_power.sh):
 
     python scripts/gemm_pmc_table.py gpurun_out/pwr/<label>_<impl> ... [--md out.md]
 
-Per run: the kernel with the largest total time, dispatches after the first 5 (warm-up), means of
-  duration (kernel trace), effective clock = GRBM_GUI_ACTIVE / 8 XCDs / duration
+Per run: one call = every kernel launched as often as the one with the largest total time (a
+  column-split GEMM's two launches; the library's GEMM + silu_mul), dispatches after the first 5
+  (warm-up), per-call sums of the mean duration (kernel trace) and counters, effective clock = GRBM_GUI_ACTIVE / 8 XCDs / duration
   (MI355X_MICROARCH.md 'DVFS give-back'), MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x
   GRBM_GUI_ACTIVE / 8), barrier / wait share = SQ_WAIT_ANY / SQ_WAVE_CYCLES.
 The label carries the shape (q6144_4096_4096 = N, K, M), so TF/s is computed here."""
@@ -51,13 +52,17 @@ def load(d):
             by_kernel[names[did]].append(did)
     if not by_kernel:
         return None
-    name = max(by_kernel, key=lambda k: sum(dur[d] for d in by_kernel[k]))
-    ds = by_kernel[name][5:] or by_kernel[name]
-    mean = lambda key: statistics.fmean(ctr[d].get(key, 0.0) for d in ds)  # noqa: E731
-    us = statistics.fmean(dur[d] for d in ds)
+    # one call = every kernel launched as often as the top one (a column-split GEMM is two
+    # launches, the library's SwiGLU projection GEMM + silu_mul): durations summed per call,
+    # counters summed over the call's kernels
+    top = max(by_kernel, key=lambda k: sum(dur[d] for d in by_kernel[k]))
+    parts = [k for k in by_kernel if len(by_kernel[k]) == len(by_kernel[top])]
+    per = {k: (by_kernel[k][5:] or by_kernel[k]) for k in parts}
+    mean = lambda key: sum(statistics.fmean(ctr[d].get(key, 0.0) for d in ds) for ds in per.values())  # noqa: E731
+    us = sum(statistics.fmean(dur[d] for d in ds) for ds in per.values())
     cyc = mean("GRBM_GUI_ACTIVE") / 8
     return {
-        "kernel": name[:60], "dispatches": len(ds), "us": us,
+        "kernel": " + ".join(k[:40] for k in parts)[:90], "dispatches": len(per[top]), "us": us,
         "clock_ghz": cyc / (us * 1e3) if us else 0.0,
         "mfma_busy": mean("SQ_VALU_MFMA_BUSY_CYCLES") / (1024 * cyc) if cyc else 0.0,
         "wait_share": mean("SQ_WAIT_ANY") / max(1.0, mean("SQ_WAVE_CYCLES")),
