@@ -1,6 +1,16 @@
-# corpus ingest alone: wall vs tokenize vs encoder, then the encoder's kernel stats
+# corpus ingest alone: wall vs tokenize vs encoder, then the encoder's kernel stats.
+# IB_ARMS="VAR=a VAR=b": instead, the ingest under each arm, interleaved twice (knob A/B).
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/ib
+if [ -n "$IB_ARMS" ]; then
+  for round in 1 2; do
+    for arm in $IB_ARMS; do
+      env $arm timeout -k 10 300 python benchmarks/index_build.py > gpurun_out/ib/ab_${arm}_$round.log 2>&1 || { tail -5 gpurun_out/ib/ab_${arm}_$round.log; exit 4; }
+      echo "$arm $(grep '"docs"' gpurun_out/ib/ab_${arm}_$round.log)"
+    done
+  done
+  exit 0
+fi
 export TMPDIR=/tmp
 timeout -k 10 300 python benchmarks/index_build.py > gpurun_out/ib/plain.log 2>&1 || { tail -5 gpurun_out/ib/plain.log; exit 2; }
 grep '"docs"' gpurun_out/ib/plain.log
