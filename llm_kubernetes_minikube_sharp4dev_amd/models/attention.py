@@ -22,6 +22,10 @@ from .. import ops
 # paged decode ~84 us per layer) it read 103.38 / 103.18 vs 102.97 / 102.81 q/s with identical
 # schedules (mixed-step GPU time -0.45 %, profiles/r3_overlap/): on by default.
 OVERLAP_ATTN = os.environ.get("LK_OVERLAP_ATTN", "1") == "1"
+# Which kernel goes to the side stream.  The main stream's kernel starts right behind the QKV GEMM,
+# the side stream's only after a cross-queue event, so the main one takes the CUs first
+# (LK_ATTN_SIDE=decode: the flash kernel leads; =flash: the paged decode leads).
+ATTN_SIDE = os.environ.get("LK_ATTN_SIDE", "decode")
 _side: dict = {}
 
 
@@ -111,24 +115,28 @@ def paged_attention(qkv: torch.Tensor, k_cache, v_cache, meta: AttnMeta, Hq: int
                          meta.max_splits, meta.part_o, meta.part_ml, out=o, split=meta.decode_split,
                          k_start=meta.shared_len, prefix=prefix)
 
-    side = None
-    if (Tp and Bd and OVERLAP_ATTN and qkv.is_cuda and not torch.cuda.is_current_stream_capturing()):
-        cur = torch.cuda.current_stream(qkv.device)
-        side = _side_stream(qkv.device)
-        side.wait_stream(cur)  # Q and the freshly written K/V are ready
-        with torch.cuda.stream(side):
-            decode()
-        qkv.record_stream(side)
-        out.record_stream(side)
-    if Tp:
+    def prefill():
         meta.ensure_tiles(Hq, Hkv, qkv.device, D)
         ops.flash_prefill(qkv[:Tp, : Hq * D], k_cache, v_cache, meta.cu_q, Hq, Hkv, D, scale, True,
                           block_tables=meta.block_tables_p, ctx_lens=meta.ctx_lens_p,
                           q_lens_cpu=meta.q_lens_cpu, ctx_lens_cpu=meta.ctx_lens_cpu,
                           tiles=meta.tiles, out=out[:Tp])
-    if side is not None:
-        torch.cuda.current_stream(qkv.device).wait_stream(side)
-    elif Bd:
+
+    if (Tp and Bd and OVERLAP_ATTN and qkv.is_cuda and not torch.cuda.is_current_stream_capturing()):
+        cur = torch.cuda.current_stream(qkv.device)
+        side = _side_stream(qkv.device)
+        side.wait_stream(cur)  # Q and the freshly written K/V are ready
+        on_side, on_main = (prefill, decode) if ATTN_SIDE == "flash" else (decode, prefill)
+        with torch.cuda.stream(side):
+            on_side()
+        qkv.record_stream(side)
+        out.record_stream(side)
+        on_main()
+        cur.wait_stream(side)
+        return out
+    if Tp:
+        prefill()
+    if Bd:
         decode()
     return out
 
