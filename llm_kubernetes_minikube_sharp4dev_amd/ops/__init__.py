@@ -95,8 +95,10 @@ def kv_write(k, v, k_cache, v_cache, slots):
 
 # keys per decode workgroup once the batch alone fills the CUs (B * Hkv >= 512); LK_DECODE_SPLIT
 # overrides it (A/B knob: three 256-thread workgroups per CU make 768 slots, so ~1.1-1.5 rounds
-# of unsplit workgroups at the serving batch leave part of the last round idle)
-DECODE_SPLIT_LARGE = int(os.environ.get("LK_DECODE_SPLIT", "1024"))
+# of unsplit workgroups at the serving batch leave part of the last round idle).  2048: the RAG
+# bench's ~1k-key rows stay in one split, so no step launches the split-merge kernel (same box,
+# interleaved: mixed-step GPU time 9.21 / 9.18 vs 9.25 / 9.25 s, 108.2 / 108.3 vs 108.2 / 107.8 q/s)
+DECODE_SPLIT_LARGE = int(os.environ.get("LK_DECODE_SPLIT", "2048"))
 
 
 def decode_split_size(B: int, Hkv: int) -> int:
