@@ -91,6 +91,11 @@ class EngineConfig:
     # server path samples with Ollama's defaults (no grammar, so no jump-forward): round 2's
     # 8192 stays; the grammar-constrained bench runs 4096 (profiles/r3_mbt/)
     max_num_batched_tokens: int = 8192
+    # prefill hold-back steps (engine/scheduler.py): the in-process engine default is 4; requests
+    # that reach the server one by one through the front-ends lose more to the wait than the
+    # fuller steps gain (-1.6 % q/s at 128 sessions, profiles/r5_http/final/), so 0 here
+    # (LK_PREFILL_HOLD, when set, overrides both)
+    prefill_hold: int = 0
     max_model_len: int = 8192
     enable_prefix_caching: bool = True
     use_hip_graphs: bool = True

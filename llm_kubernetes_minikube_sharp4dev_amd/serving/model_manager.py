@@ -13,6 +13,7 @@ A TP core serves exactly one generator (its followers hold that model's shards);
 on the leader's GPU."""
 from __future__ import annotations
 
+import os
 import threading
 import time
 from dataclasses import dataclass, field
@@ -157,6 +158,8 @@ class ModelManager:
                   gpu_memory_fraction=e.gpu_memory_fraction, kv_cache_gb=e.kv_cache_gb, seed=e.seed)
         if self.device.type == "cpu":
             kw["num_blocks"] = 2048
+        if "LK_PREFILL_HOLD" not in os.environ:
+            kw["prefill_hold"] = e.prefill_hold
         kw.update(self.engine_overrides)
         runner = {k: v for k, v in kw.items() if k in self._RUNNER_KEYS}
         return runner, {k: v for k, v in kw.items() if k not in self._RUNNER_KEYS}
