@@ -104,7 +104,7 @@ def main():
     counts = [int(x) for x in a.requests.split(",")]
     p1, p2 = _port(), _port()
     env = dict(os.environ, LK_ENGINE__DEFAULT_MAX_NEW_TOKENS=str(a.max_new_tokens),
-               LK_ENGINE__KV_CACHE_GB=str(a.kv_gb), LK_ENGINE__MAX_NUM_BATCHED_TOKENS="8192",
+               LK_ENGINE__KV_CACHE_GB=str(a.kv_gb), LK_ENGINE__MAX_NUM_BATCHED_TOKENS=os.environ.get("LK_ENGINE__MAX_NUM_BATCHED_TOKENS", "8192"),
                LK_ENGINE__MAX_NUM_SEQS="256", PYTHONUNBUFFERED="1")
     mod = "llm_kubernetes_minikube_sharp4dev_amd"
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
