@@ -17,8 +17,9 @@ MI355X layout decisions:
   * tensor parallel: column-parallel QKV / gate_up, row-parallel o / down, each followed by
     one all-reduce fused with the residual add + RMSNorm -- the xGMI IPC kernel
     (csrc/xgmi_allreduce.hip, one- or two-shot) or RCCL + the norm kernel, per row bucket as
-    measured at start-up (parallel/xgmi_ar.py); vocab-parallel embedding + LM head (greedy: one
-    all-gather of packed (value, id) keys);
+    measured at start-up (parallel/xgmi_ar.py); on prefill-sized steps the QKV GEMM still runs
+    RoPE + the paged-KV write in its epilogue (``ops.linear_rope_kv``); vocab-parallel embedding +
+    LM head (greedy: one all-gather of packed (value, id) keys);
   * sequence parallel for prefill-sized steps (``sp_min_tokens``): residual stream and
     norms sharded over the T rows, reduce-scatter / all-gather instead of all-reduce.
 """
