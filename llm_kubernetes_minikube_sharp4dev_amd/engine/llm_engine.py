@@ -437,8 +437,26 @@ class AsyncLLMEngine:
         self._wake = threading.Event()
         self._stop = False
         self.watchdog = StepWatchdog("engine", stall_s=stall_s, on_stall=lambda dt: self._fail_all("stalled"))
+        # LK_STEP_TRACE=N: trace every step (LLMEngine.step_trace) and log a summary per N traced
+        # steps -- GPU time, device idle before launches, host time -- so a served engine's step
+        # loop can be checked for a starved device the way bench.py's in-process runs are
+        self._trace_every = int(os.environ.get("LK_STEP_TRACE", "0") or 0)
+        if self._trace_every > 0:
+            self.engine.step_trace = []
         self._thread = threading.Thread(target=self._loop, name="lk-engine", daemon=True)
         self._thread.start()
+
+    def _log_trace(self):
+        tr = self.engine.step_trace
+        if not tr or len(tr) < self._trace_every:
+            return
+        self.engine.step_trace = []
+        n = len(tr)
+        log.info("step trace: %d steps (%d decode-only), GPU %.1f ms, device idle before launch %.1f ms "
+                 "(%d launches found it idle), host step %.1f ms, mean prefill %d rows / decode %d rows",
+                 n, sum(1 for t in tr if t[0] == 0), 1e3 * sum(t[7] for t in tr), 1e3 * sum(t[8] for t in tr),
+                 sum(1 for t in tr if t[10]), 1e3 * sum(t[2] for t in tr), sum(t[0] for t in tr) // n,
+                 sum(t[1] for t in tr) // n)
 
     @property
     def healthy(self) -> bool:
@@ -474,6 +492,8 @@ class AsyncLLMEngine:
                 with self.watchdog.busy():
                     self.engine.step_pipelined()
                 self.watchdog.beat()
+                if self._trace_every:
+                    self._log_trace()
             except Exception:  # pragma: no cover
                 log.exception("engine step failed; aborting in-flight requests")
                 self._fail_all("engine step failed")
