@@ -81,7 +81,7 @@ class LLMEngine:
                                    token_align, token_align_wave, prefill_hold,
                                    int(os.environ.get("LK_HOLD_MIN_DECODE", "64")),
                                    float(os.environ.get("LK_HOLD_FILL", "1.0")),
-                                   _small_buckets())
+                                   _small_buckets(), int(os.environ.get("LK_HOLD_SMALL", "0")))
         self.sampler = Sampler(model.cfg.vocab_size, seed, history_len=max_model_len)
         self.max_model_len = max_model_len
         if eos_ids is None:

@@ -35,7 +35,7 @@ class Scheduler:
     def __init__(self, allocator, block_size: int, max_num_seqs: int = 256,
                  max_num_batched_tokens: int = 65536, max_model_len: int = 8192, token_align: int = 256,
                  token_align_wave: int = 0, prefill_hold: int = 0, hold_min_decode: int = 64,
-                 hold_fill: float = 1.0, small_buckets: tuple = ()):
+                 hold_fill: float = 1.0, small_buckets: tuple = (), hold_small: int = 0):
         self.alloc = allocator
         # weight-streaming steps (<= small_buckets[-1] rows): prompt prefill is trimmed so the
         # step stays in the row bucket its decode / extend rows already need (the decode GEMMs'
@@ -50,6 +50,10 @@ class Scheduler:
         self.prefill_hold = prefill_hold
         self.hold_min_decode = hold_min_decode
         self.hold_fill = hold_fill
+        # ... except that a held step may still take prompt tokens up to hold_small rows in total:
+        # it streams every weight once anyway (the weight-streaming GEMMs serve <= 256 rows), so a
+        # few hundred prompt rows ride in it for about half their cost in a full step
+        self.hold_small = hold_small
         self._held = 0  # consecutive steps that held prefill back
         # mixed steps: trim prefill chunks so the step's row count is a multiple of the
         # prefill GEMM's 256-row macro tile (a 3852-row step runs 16 row tiles, the 16th
@@ -151,9 +155,12 @@ class Scheduler:
             if seq.done_after_inflight or seq.length + seq.num_inflight >= self.max_model_len:
                 i += 1  # finishes when its in-flight token is collected
                 continue
+            cap = budget
             if hold and not self._generating(seq):
-                break  # prefill chunks sort last: all held this step
-            n = min(seq.pending, budget)
+                cap = min(budget, self.hold_small - (self.max_tokens - budget))
+                if cap <= 0:
+                    break  # prefill chunks sort last: all held this step
+            n = min(seq.pending, cap)
             if not self._ensure(seq, seq.num_computed + n):
                 victim = self.running.pop()
                 self._preempt(victim)
@@ -163,12 +170,16 @@ class Scheduler:
             batch.items.append((seq, seq.num_computed, n))
             budget -= n
             i += 1
-        while not hold and self.waiting and budget > 0 and len(self.running) < self.max_num_seqs:
+
+        def admit_cap() -> int:
+            return min(budget, self.hold_small - (self.max_tokens - budget)) if hold else budget
+
+        while self.waiting and admit_cap() > 0 and len(self.running) < self.max_num_seqs:
             seq = self.waiting[0]
             if seq.num_inflight:
                 break  # preempted with a token in flight: re-admit once it is collected
             self._admit_prefix(seq)
-            n = min(seq.pending, budget)
+            n = min(seq.pending, admit_cap())
             if not self._ensure(seq, seq.num_computed + n):
                 if not self.running and not batch.items:
                     # nothing else holds blocks: this request can never fit

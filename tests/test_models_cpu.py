@@ -229,6 +229,40 @@ def test_prefill_hold_back_same_tokens_fuller_steps(monkeypatch):
     assert part1 < part0, (part0, part1)
 
 
+def test_prefill_hold_small_fill_same_tokens(monkeypatch):
+    """LK_HOLD_SMALL: a held step still takes prompt tokens up to hold_small rows in total -- same
+    greedy tokens as the eager scheduler, no held step past hold_small rows, and prompt tokens do
+    ride in steps the plain hold-back leaves decode-only."""
+    m = build_decoder("llama-tiny", dtype=torch.float32)
+    monkeypatch.setenv("LK_HOLD_MIN_DECODE", "2")
+    prompts = [list(range(3, 3 + n)) for n in (40, 33, 25, 30, 17, 22, 35, 28)]
+
+    def run(hold, small):
+        monkeypatch.setenv("LK_HOLD_SMALL", str(small))
+        eng = _engine(m, max_num_batched_tokens=64, prefill_hold=hold, token_align=0)
+        eng.step_trace = []
+        seqs = [eng.add_request(p, SamplingParams.greedy(12)) for p in prompts[:3]]
+        it, held_sizes = 0, []
+        while eng.has_work() or len(seqs) < len(prompts):
+            if it % 3 == 2 and len(seqs) < len(prompts):
+                seqs.append(eng.add_request(prompts[len(seqs)], SamplingParams.greedy(12)))
+            held_before = eng.scheduler._held
+            eng.step()
+            if eng.scheduler._held > held_before:  # this step held prefill back
+                held_sizes.append(eng.step_trace[-1][0] + eng.step_trace[-1][1])
+            it += 1
+        return [s.output_ids for s in seqs], eng.step_trace, held_sizes
+
+    ref, _, _ = run(0, 0)
+    got0, tr0, held0 = run(4, 0)
+    got1, tr1, held1 = run(4, 8)
+    assert got0 == ref and got1 == ref
+    assert held1 and max(held1) <= 8, held1
+    small0 = sum(t[0] for t in tr0 if t[0] + t[1] <= 8)
+    small1 = sum(t[0] for t in tr1 if t[0] + t[1] <= 8)
+    assert small1 > small0, (small0, small1)
+
+
 def test_small_step_bucket_alignment_same_tokens(monkeypatch):
     """LK_SMALL_STEP_ALIGN: a weight-streaming step (<= the largest bucket in rows) with decode
     rows trims prompt prefill to the row bucket its decode rows need (the trimmed tokens lead the
