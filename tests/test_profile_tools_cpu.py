@@ -92,3 +92,44 @@ def test_gemm_pmc_table_clock_and_mfma_busy(tmp_path):
     row = md.read_text().splitlines()[2]
     # 2 * 4096^3 FLOP in 100 us = 1374 TF/s; busy x clock = 1.2
     assert "| 1374 |" in row and "| 2.00 |" in row and "60.0 %" in row and "| 1.200 |" in row
+
+
+def test_attn_phase_splits_overlap(tmp_path):
+    """scripts/attn_phase.py: a mixed step's attention phase (first attention kernel after a GEMM
+    to the next GEMM) split into both-running / flash-only / decode-only / neither."""
+    ap = _load("attn_phase")
+    us = 1000
+    rows = [
+        ("lk_window_mark_kernel", 0, 1),
+        ("void anon::gemm1w_kernel<7, 16, 256, false>(x)", 10, 100),   # QKV
+        ("void anon::flash_prefill_kernel<128, true>(x)", 100, 160),    # flash 100-160
+        ("void anon::paged_decode_kernel<128, 4>(x)", 120, 200),       # decode 120-200
+        ("void anon::gemm1w_kernel<6, 0, 256, false>(x)", 210, 300),    # O: phase ends at 210
+        ("void anon::paged_decode_kernel<128, 4>(x)", 300, 350),       # a decode-only phase
+        ("void anon::wsgemm_kernel<12, 128, false>(x)", 355, 400),
+        ("lk_window_mark_kernel", 500, 501),
+    ]
+    path = tmp_path / "run_kernel_trace.csv"
+    _write(path, ["Kernel_Name", "Start_Timestamp", "End_Timestamp"],
+           [{"Kernel_Name": n, "Start_Timestamp": s * us, "End_Timestamp": e * us} for n, s, e in rows])
+    ph = ap.phases(list(csv.DictReader(open(path))))
+    assert len(ph) == 2
+    mixed = ph[0]
+    assert mixed["next_gemm"] - mixed["start"] == 110 * us
+    f, d = ap._union(mixed["flash"]), ap._union(mixed["decode"])
+    both = ap._len(ap._inter(f, d))
+    assert both == 40 * us                       # 120-160
+    assert ap._len(f) - both == 20 * us          # flash alone 100-120
+    assert ap._len(d) - both == 40 * us          # decode alone 160-200
+    assert ph[1]["decode"] and not ph[1]["flash"]
+    buf = io.StringIO()
+    with redirect_stdout(buf):
+        import sys
+        argv = sys.argv
+        sys.argv = ["attn_phase.py", str(path)]
+        try:
+            ap.main()
+        finally:
+            sys.argv = argv
+    out = buf.getvalue()
+    assert "mixed (flash + decode): 1 phases" in out and "decode only: 1 phases" in out
