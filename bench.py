@@ -28,6 +28,12 @@ is ~20-60 tokens; default 48).
 
   python bench.py [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node 8 bench.py --gpus 8 ...
+
+``--gpus N`` decides the world: under torchrun it must equal ``WORLD_SIZE`` (a mismatch is
+refused); without a launcher (no ``WORLD_SIZE`` in the environment) and N > 1 this process
+makes no HIP call, starts N fresh rank processes itself (``parallel/launch.py`` rank env,
+one per local device) and relays rank 0's JSON line -- so ``python bench.py --gpus 8`` is a
+whole-node run either way.  Ranks must land on N distinct devices (``--one-device`` aside).
 """
 from __future__ import annotations
 
@@ -52,7 +58,9 @@ MODEL_NAMES = {"llama-3-8b": "Llama-3-8B", "llama-3-70b": "Llama-3-70B", "opt-12
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of the job; default: WORLD_SIZE under a launcher, else 1.  Without a "
+                         "launcher, N > 1 spawns the N rank processes itself")
     ap.add_argument("--steps", type=int, default=8, help="timed steps (continuous mode: a step = --batch completions per replica; 8 x 128 keeps the window-boundary noise of in-flight requests under 1%%)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=128,
@@ -153,6 +161,16 @@ def main():
             (["--frontends", str(args.frontends)] if args.frontends else []) + \
             (["--concurrency", args.http_levels, "--requests", args.http_requests] if args.http_levels else [])
         raise SystemExit(subprocess.call(cmd))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus is not None and args.gpus > 1:
+            raise SystemExit(_launch_ranks(args.gpus))  # no HIP call in this process
+        args.gpus = 1
+    elif args.gpus is None:
+        args.gpus = int(env_world)
+    elif int(env_world) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks; "
+                         f"refusing to report a {env_world}-rank run as {args.gpus} GPUs")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -219,6 +237,15 @@ def main():
                 dist.init_process_group("gloo")
             else:
                 dist.init_process_group("nccl", device_id=dev)
+                # one rank per GPU: N ranks on fewer than N devices would time shared GPUs
+                import socket
+
+                where = [None] * world
+                dist.all_gather_object(where, (socket.gethostname(), torch.cuda.current_device()))
+                if len(set(where)) != world:
+                    raise SystemExit(f"bench.py: {world} ranks landed on {len(set(where))} distinct devices "
+                                     f"{sorted(set(where))}; --gpus {args.gpus} needs one device per rank "
+                                     f"(--one-device shares one GPU on purpose)")
     else:
         dev = torch.device("cpu")
         if world > 1:
@@ -681,6 +708,63 @@ def main():
                 f.write(line + "\n")
     if world > 1:
         dist.destroy_process_group()
+
+
+def _launch_ranks(n: int) -> int:
+    """``python bench.py --gpus N`` without a launcher: start N fresh rank processes (this
+    process has made no HIP call, so nothing GPU-initialised forks or execs), rank r on local
+    device r with the torchrun environment of ``parallel/launch.py:rank_env``.  Rank 0's stdout
+    (the one JSON line) is relayed to this stdout; the other ranks' stdout goes to stderr.  The
+    first rank to fail ends the job: the others are terminated and its exit code returned."""
+    import signal
+    import subprocess
+    import threading
+
+    from llm_kubernetes_minikube_sharp4dev_amd.parallel.launch import free_port, rank_env
+
+    port = int(os.environ.get("MASTER_PORT") or free_port())
+    argv = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    for r in range(n):
+        procs.append(subprocess.Popen(argv, env=rank_env(r, n, r, port),
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(), text=True))
+    print(f"[bench] launched {n} ranks (pids {[p.pid for p in procs]}, master 127.0.0.1:{port})",
+          file=sys.stderr, flush=True)
+
+    def relay():
+        for line in procs[0].stdout:
+            (sys.stdout if line.startswith("{") else sys.stderr).write(line)
+            sys.stdout.flush()
+
+    th = threading.Thread(target=relay, daemon=True)
+    th.start()
+
+    def stop_all(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+
+    signal.signal(signal.SIGTERM, lambda *a: (stop_all(), sys.exit(143)))
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p for p in procs if p.poll() not in (None, 0)]
+        if bad:
+            rc = bad[0].returncode
+            print(f"[bench] rank {procs.index(bad[0])} exited with {rc}: stopping the other ranks",
+                  file=sys.stderr, flush=True)
+            stop_all()
+            break
+        time.sleep(0.2)
+    for p in procs:
+        try:
+            p.wait(timeout=60)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    th.join(timeout=10)
+    if rc == 0:
+        rc = next((p.returncode for p in procs if p.returncode), 0)
+    return rc if rc >= 0 else 128 - rc
 
 
 def _idle_summary(trace) -> dict:

@@ -4,7 +4,15 @@ serving GEMM (csrc/gemm.hip through ops.linear) vs hipBLASLt (F.linear), Llama-3
 cold weights (rotated copies past the 256 MB MALL), interleaved rounds in one process, medians;
 plus a numerics check of the new kernel against an fp32 torch matmul.
 
-    python benchmarks/gemm1w_probe.py --so benchmarks/probes/bin/libgemm1w.so [--ms 4096,8192]
+    python benchmarks/gemm1w_probe.py --build [--ms 4096,8192]
+
+``--build`` compiles the probe library from the tracked ``csrc/gemm1w.hip`` (its ``extern "C"
+lk_gemm1w_c`` entry) into ``benchmarks/probes/bin/libgemm1w.so`` with hipcc first -- the
+library is a build product (git-ignored), the source is the serving kernel itself.  The
+schedule-sweep arms of ``profiles/r5_gemm1w/`` (``libgemm1w_c7`` / ``_n2``...) were builds of
+intermediate versions of that file; the kept schedule is the one in its history
+(``git log -- csrc/gemm1w.hip``), so rebuilding a sweep arm means checking out that commit's
+``csrc/gemm1w.hip`` and passing ``--build --so <name>``.
 """
 from __future__ import annotations
 
@@ -23,6 +31,18 @@ SHAPES = [("QKV", 6144, 4096, 0), ("O", 4096, 4096, 0), ("gate_up+SwiGLU", 28672
           ("down", 4096, 14336, 0), ("enc_ffn_up", 3072, 768, 0), ("enc_ffn_dn", 768, 3072, 0)]
 
 
+def build_probe(out: str) -> str:
+    """hipcc the serving kernel source into a standalone shared library (no torch, no bindings)."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-ffp-contract=fast",
+           "-Wno-inline-asm", "-I", os.path.join(root, "csrc"), os.path.join(root, "csrc", "gemm1w.hip"), "-o", out]
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--so", default="benchmarks/probes/bin/libgemm1w.so")
@@ -33,7 +53,11 @@ def main():
     ap.add_argument("--no-cur", action="store_true", help="skip the gemm.hip arm")
     ap.add_argument("--shapes", default="")
     ap.add_argument("--extra", default="", help="extra shapes name:N:K[:swiglu],...")
+    ap.add_argument("--build", action="store_true",
+                    help="compile csrc/gemm1w.hip into the --so path (hipcc, gfx950) before probing")
     a = ap.parse_args()
+    if a.build:
+        build_probe(a.so.split(",")[0].partition(":")[0])
     fns = {}
     for spec in a.so.split(","):  # path[:group] -> one arm per entry
         path, _, grp = spec.partition(":")

@@ -17,7 +17,18 @@ hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 #define CHECK_F32(x) TORCH_CHECK((x).scalar_type() == at::kFloat, #x " must be float32")
 #define CHECK_LASTDIM(x) TORCH_CHECK((x).stride(-1) == 1, #x " must be contiguous in its last dim")
 #define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
-#define CHECK_RC(rc, name) TORCH_CHECK((rc) == 0, name ": unsupported shape/config (code ", rc, ")")
+// Every launcher's return code AND the HIP launch state are checked after each op: a rejected
+// launch raises here instead of returning an uninitialised output (common.h LK_CHECK_LAUNCH).
+void check_rc(int rc, const char* name) {
+  const hipError_t e = hipGetLastError();  // launchers that do not check their own launches
+  if (rc <= kLkAttrError && rc > kLkAttrError - 1000)
+    TORCH_CHECK(false, name, ": kernel dynamic-LDS attribute refused: ", hipGetErrorString((hipError_t)(kLkAttrError - rc)));
+  if (rc <= kLkLaunchError && rc > kLkLaunchError - 1000)
+    TORCH_CHECK(false, name, ": kernel launch failed: ", hipGetErrorString((hipError_t)(kLkLaunchError - rc)));
+  TORCH_CHECK(rc == 0, name, ": unsupported shape/config (code ", rc, ")");
+  TORCH_CHECK(e == hipSuccess, name, ": kernel launch failed: ", hipGetErrorString(e));
+}
+#define CHECK_RC(rc, name) check_rc((rc), (name))
 
 inline bf16_t* bp(const at::Tensor& t) { return reinterpret_cast<bf16_t*>(t.data_ptr()); }
 inline bf16_t* bpo(const c10::optional<at::Tensor>& t) { return t ? bp(*t) : nullptr; }
@@ -855,6 +866,7 @@ extern "C" const char lk_source_stamp[];
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("window_mark", [](int64_t id) { CHECK_RC(lk_window_mark((int)id, cur_stream()), "window_mark"); });
+  m.def("debug_invalid_launch", []() { CHECK_RC(lk_debug_invalid_launch(cur_stream()), "debug_invalid_launch"); });
   // a HIP stream restricted to the CUs of a bit mask (32 CUs per word): two kernels that
   // would each fill the chip (a mixed step's flash prefill and paged decode) run side by side
   // on disjoint CU sets.  Returned as an integer handle for torch.cuda.ExternalStream; the

@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "kernels.h"
+
 #define LK_DEVICE __device__ __forceinline__
 
 typedef unsigned short bf16_t;  // raw bf16 bits
@@ -123,7 +125,30 @@ LK_DEVICE int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-#define LK_CHECK_LAUNCH() (void)hipGetLastError()
+// Launch failures are loud: a rejected launch (bad grid / block / LDS request) returns a
+// distinct code that the bindings turn into a Python exception (bindings.cpp CHECK_RC), never
+// a "successful" op over an uninitialised output.
+// (the codes kLkLaunchError / kLkAttrError are in kernels.h, shared with the bindings)
+// first refused kernel attribute of the process (sticky: the kernel it belongs to cannot run)
+inline hipError_t& lk_attr_error() {
+  static hipError_t e = hipSuccess;
+  return e;
+}
+#define LK_CHECK_LAUNCH()                                                           \
+  do {                                                                              \
+    const hipError_t lk_e_ = hipGetLastError();                                     \
+    if (lk_attr_error() != hipSuccess) return kLkAttrError - (int)lk_attr_error(); \
+    if (lk_e_ != hipSuccess) return kLkLaunchError - (int)lk_e_;                    \
+  } while (0)
+// One-time dynamic-LDS opt-in of a kernel, its result kept: a refusal is reported by the
+// launch's LK_CHECK_LAUNCH instead of surfacing as an unexplained launch failure.
+#define LK_SET_MAX_LDS(kern, bytes)                                                                     \
+  do {                                                                                                  \
+    static const hipError_t lk_attr_ = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),        \
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                                           (int)(bytes));                              \
+    if (lk_attr_ != hipSuccess) lk_attr_error() = lk_attr_;                                             \
+  } while (0)
 
 // Device-side bounds checks for debug builds (`python csrc/build.py --debug`, objects
 // under build/csrc-debug): a failing check traps the wave with the kernel's file/line

@@ -948,12 +948,7 @@ template <int NF, int EPI, int PH, int PRIO, bool SC>
 void launch_sc(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
                long ldo, int TM, int TN, int ks, hipStream_t st, const LkEpi& ea) {
   constexpr int lds = 2 * Geo<NF>::BUF;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_kernel<NF, EPI, PH, PRIO, SC>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr = true;
-  }
+  LK_SET_MAX_LDS((gemm_kernel<NF, EPI, PH, PRIO, SC>), lds);
   SkArgs sk{0, 0, nullptr, nullptr, nullptr, 0};
   int grid = gemm_grid(TM * TN);
   if (ks == 1 && EPI != EPI_PARTIAL) sk_plan(M, TM * TN, K / kBK, 64 * NF, st, &sk, &grid);

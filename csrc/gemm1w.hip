@@ -655,12 +655,7 @@ template <int EPI, int SCP, int BM, bool PERSIST = false>
 void launch1w_p(const bf16_t* x, long ldx, const bf16_t* w, const bf16_t* bias, int M, int K, int I, bf16_t* out,
                 long ldo, int TN, int tn0, int ks, int group_m, hipStream_t st, const LkEpi& ea) {
   constexpr int lds = Tile<BM>::kLds;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm1w_kernel<EPI, SCP, BM, PERSIST>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr = true;
-  }
+  LK_SET_MAX_LDS((gemm1w_kernel<EPI, SCP, BM, PERSIST>), lds);
   const int TM = (M + BM - 1) / BM;
   const int grid = PERSIST ? min(TM * TN, cu_count()) : TM * TN;
   gemm1w_kernel<EPI, SCP, BM, PERSIST><<<dim3(grid, ks), 256, lds, st>>>(x, ldx, w, bias, M, K, I, out, ldo, TM, TN,

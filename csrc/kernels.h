@@ -7,6 +7,11 @@
 
 typedef unsigned short bf16_t;
 
+// Launch-failure return codes (common.h LK_CHECK_LAUNCH / LK_SET_MAX_LDS): the bindings raise
+// with the HIP error string instead of handing back an uninitialised output.
+constexpr int kLkLaunchError = -1000;  // rc = kLkLaunchError - hipError_t
+constexpr int kLkAttrError = -2000;    // rc = kLkAttrError - hipError_t (dynamic-LDS opt-in refused)
+
 // norm.hip
 int lk_rmsnorm(bf16_t* out, bf16_t* residual, const bf16_t* x, const bf16_t* w, long rows, int H,
                float eps, long xs, long os, long rs, hipStream_t st);
@@ -178,6 +183,8 @@ int lk_sample(float* logits, long ls, int B, int V, const int* prm, int* hist, i
 
 // csrc/marker.hip: a one-wave marker kernel bounding a timed window in kernel traces
 int lk_window_mark(int id, hipStream_t st);
+// a launch the runtime rejects (2048 threads): returns the LK_CHECK_LAUNCH code, runs nothing
+int lk_debug_invalid_launch(hipStream_t st);
 
 // csrc/step_ops.hip: the forward's small per-step gathers (no framework kernels in a step)
 int lk_embed_rows(bf16_t* out, const bf16_t* table, const int* ids, long T, int H, long lo, long n_local,

@@ -17,3 +17,11 @@ int lk_window_mark(int id, hipStream_t st) {
   lk_window_mark_kernel<<<1, 64, 0, st>>>(id, g_sink);
   return 0;
 }
+
+// Loud-failure probe (tests/test_kernels_gpu.py): a launch the runtime must reject before any
+// wave runs (2048 threads per workgroup, above the 1024 limit), checked like every launcher.
+int lk_debug_invalid_launch(hipStream_t st) {
+  lk_window_mark_kernel<<<1, 2048, 0, st>>>(0, nullptr);
+  LK_CHECK_LAUNCH();
+  return 0;
+}

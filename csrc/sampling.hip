@@ -471,12 +471,7 @@ int lk_sample(float* logits, long ls, int B, int V, const int* prm, int* hist, i
   const size_t seen_bytes = (size_t)((V + 31) >> 5) * 4;
   if (seen_bytes > 160 * 1024) return -1;  // the LDS "seen" bitmap: V <= 1.3M
   if (seen_bytes > 64 * 1024) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(sample_penalty_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr = true;
-    }
+    LK_SET_MAX_LDS(sample_penalty_kernel, 160 * 1024);
   }
   sample_penalty_kernel<<<B, 256, seen_bytes, st>>>(logits, ls, V, prm, hist, hist_len, W);
   sample_topkp_kernel<<<B, kSampThreads, 0, st>>>(logits, ls, V, prm, hist, hist_len, W, seed, out);

@@ -636,12 +636,7 @@ void launch_ws(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks,
                bf16_t* out, long ldo, float* part, long part_ld, long n_rows, hipStream_t st) {
   constexpr size_t lds = (size_t)ws_stages(MT, BN) * (16 * MT * 128 + BN * 128);
   auto kern = wsgemm_kernel<MT, BN, SWIGLU>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    attr = true;
-  }
+  LK_SET_MAX_LDS(kern, (int)lds);
   const int rot_mul = g_ws_rot_mul >= 0 ? g_ws_rot_mul : (S == 1 ? 5 : 0);
   kern<<<n_tiles * S, 256, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows, rot_mul);
 }
@@ -651,12 +646,7 @@ void launch_ws_lw(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int 
                   bf16_t* out, long ldo, float* part, long part_ld, long n_rows, hipStream_t st) {
   constexpr size_t lds = (size_t)lw_nsx(MT) * 16 * MT * 128 + (size_t)lw_nsw(MT, BN) * BN * 128;
   auto kern = wsgemm_lw_kernel<MT, BN, SWIGLU>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    attr = true;
-  }
+  LK_SET_MAX_LDS(kern, (int)lds);
   const int rot_mul = g_ws_rot_mul >= 0 ? g_ws_rot_mul : (S == 1 ? 5 : 0);
   kern<<<n_tiles * S, 384, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows, rot_mul);
 }
@@ -683,12 +673,7 @@ void launch_skinny(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int
                    int I, bf16_t* out, long ldo, float* part, long part_ld, hipStream_t st) {
   const size_t lds = sizeof(float) * kSkW * 16 * MT * (16 * NTW + 4);
   auto kern = skinny_gemm_kernel<MT, NTW, SWIGLU>;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)lds);
-    attr = true;
-  }
+  LK_SET_MAX_LDS(kern, (int)lds);
   kern<<<n_tiles * S, 256, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld);
 }
 

@@ -125,9 +125,19 @@ class XgmiAllReduce:
         pad = (-flat.numel()) % 8
         work = torch.nn.functional.pad(flat, (0, pad)) if pad else flat.clone()
         step = self.max_bytes // 2 // 8 * 8
+        # the chunks are staging-sized: no row bucket applies, so an algorithm the self-check
+        # vetoed in ANY bucket is not used
+        vetoed = set().union(*self.bad.values()) if self.bad else set()
+        algo = next((a for a in ("ipc1", "ipc2") if a not in vetoed), None)
+        if algo is None:
+            raise RuntimeError("IPC all-reduce: every IPC algorithm failed the start-up self-check")
         for s in range(0, work.numel(), step):
             piece = work[s:s + step]
-            self.state.all_reduce(piece, piece)
+            if algo == "ipc2":
+                v = piece.view(-1, 8)
+                self.state.all_reduce2(v, v)
+            else:
+                self.state.all_reduce(piece, piece)
         t.copy_(work[: flat.numel()].view_as(t))
         return t
 
@@ -309,7 +319,11 @@ class XgmiAllReduce:
                   "reasons_on_rank": why}
         vetoed = sorted(T for T, s in self.bad.items() if s)
         report["vetoed_buckets"] = vetoed
-        report["ipc_disabled"] = bool(flags[-1]) or (not self.gather_ok)
+        # buckets where BOTH IPC forms failed: without an RCCL communicator to route them to,
+        # the group's all-reduce is known to be wrong there -> the group is unusable
+        unusable = sorted(T for T, s in self.bad.items() if set(algos) <= s)
+        report["unusable_buckets"] = unusable
+        report["ipc_disabled"] = bool(flags[-1]) or (not self.gather_ok) or (bool(unusable) and not self.rccl)
         if self.table:  # re-route an already-tuned table
             self.table = route_table(self.timings, self.bad, self.rccl)
         self.check = report
@@ -322,14 +336,18 @@ class XgmiAllReduce:
 
 def route_table(timings: dict, bad: dict, rccl: bool) -> dict:
     """Per row bucket the fastest algorithm the self-check did not veto; a bucket where every
-    IPC form failed goes to RCCL (or, without a communicator, keeps its fastest IPC form --
-    ``XgmiAllReduce.check`` then says the group is unusable)."""
+    IPC form failed goes to RCCL.  Without a communicator such a bucket is an error: the
+    self-check reports it (``unusable_buckets``, ``ipc_disabled``) and ``tune_collectives``
+    raises before any table is built; called anyway, this raises too."""
     table = {}
     for T, v in timings.items():
         veto = bad.get(T) or bad.get(int(T)) or set()
         ok = {a: t for a, t in v.items() if a not in veto and (a != "rccl" or rccl)}
         if not ok:
-            ok = {"rccl": 0.0} if rccl else dict(v)
+            if not rccl:
+                raise RuntimeError(f"all-reduce bucket <= {T} rows: every IPC algorithm failed the self-check "
+                                   f"and the group has no RCCL communicator")
+            ok = {"rccl": 0.0}
         table[T] = min(ok, key=ok.get)
     return table
 

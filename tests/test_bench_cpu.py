@@ -22,11 +22,13 @@ def _port():
     return p
 
 
-def _run(extra, nproc=1, timeout=600):
+def _run(extra, nproc=1, timeout=600, self_launch=False):
     args = ["--device", "cpu", "--model", "llama-tiny", "--embedder", "bert-tiny", "--docs", "8", "--batch", "2",
             "--steps", "1", "--warmup", "1", "--max-new-tokens", "3", *extra]
-    if nproc == 1:
+    if nproc == 1 or self_launch:
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), *args]
+        if self_launch:
+            cmd += ["--gpus", str(nproc)]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
@@ -59,6 +61,33 @@ def test_bench_four_rank_dp():
     d = _run([], nproc=4)
     assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "dp4" and d["config"]["global_batch"] == 8
     assert d["value"] > 0 and d["ms_per_step"] > 0
+
+
+def test_bench_self_launch_two_ranks():
+    """The driver's plain ``python bench.py --gpus 2`` (no torchrun): bench.py starts both rank
+    processes itself, and the single JSON line is the 2-replica whole-job aggregate."""
+    d = _run([], nproc=2, self_launch=True)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 4
+    dist = d["config"]["distributed"]
+    assert dist["world_size"] == 2 and len(dist["per_replica"]) == 2
+    assert all(r["completions"] > 0 for r in dist["per_replica"])
+
+
+def test_bench_refuses_gpus_world_mismatch():
+    """--gpus 2 inside a launcher that started WORLD_SIZE=1 is refused before any work."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "2"],
+                       capture_output=True, text=True, timeout=120, cwd="/tmp",
+                       env=dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr and not r.stdout.strip()
+
+
+def test_bench_self_launch_propagates_rank_failure():
+    """A rank that fails ends the self-launched job with a non-zero exit and no JSON line."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "2",
+                        "--model", "no-such-model", "--embedder", "bert-tiny", "--docs", "8"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp", env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
 
 
 def test_bench_two_rank_tp():

@@ -1025,3 +1025,13 @@ def test_ws_loader_wave_variant_bit_identical(hip, M, NK, swiglu):
         _close(outs[1], y, 0.03, 0.02, f"lw M{M} N{N} K{K}")
     finally:
         hip.ws_set_variant(M, N, K, swiglu, -1)
+
+
+def test_invalid_launch_raises(hip):
+    """A launch the runtime rejects (2048 threads per workgroup) raises with the HIP error
+    instead of returning as if it had run; the next op on the stream still works."""
+    with pytest.raises(RuntimeError, match="kernel launch failed"):
+        hip.debug_invalid_launch()
+    x = torch.randn(4, 768, device=DEV, dtype=torch.bfloat16)
+    w = torch.ones(768, device=DEV, dtype=torch.bfloat16)
+    _close(hip.rmsnorm(x, w, 1e-5, None, None), ref.rmsnorm(x, w, 1e-5, None), 0.05, 0.01, "after a failed launch")

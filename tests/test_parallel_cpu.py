@@ -624,13 +624,13 @@ class _FakeIpcState:
 
     def all_reduce(self, inp, out):
         y = self._sum(inp)
-        if self.broken == "ipc1":
+        if self.broken in ("ipc1", "both"):
             y[0, 0] += 1
         out.copy_(y.to(out.dtype))
 
     def all_reduce2(self, inp, out, residual=None, w=None, eps=None):
         y = self._sum(inp)
-        if self.broken == "ipc2":
+        if self.broken in ("ipc2", "both"):
             y.view(-1)[-1] += 2
         if residual is None:
             out.copy_(y.to(out.dtype))
@@ -642,7 +642,7 @@ class _FakeIpcState:
 
     def all_reduce_rmsnorm(self, x, residual, w, eps, out):
         y = self._sum(x)
-        if self.broken == "ipc1":
+        if self.broken in ("ipc1", "both"):
             y[0, 0] += 1
         residual.copy_((residual.float() + y).to(residual.dtype))
         from llm_kubernetes_minikube_sharp4dev_amd.ops import reference as ref
@@ -671,25 +671,44 @@ def _selfcheck_worker(rank, world, port, out_path, broken_rank, broken_algo, gat
     x.table, x.timings, x.bad, x.gather_ok, x.check = {}, {}, {}, True, {}
     x.state = _FakeIpcState(tp, broken_algo if rank == broken_rank else None, gather_broken and rank == broken_rank)
     rep = x.self_check(64, rows=(1, 4, 16))
-    table = route_table({T: {"ipc1": 1.0, "ipc2": 2.0} for T in (1, 4, 16)}, x.bad, False)
-    torch.save((rep, {T: sorted(s) for T, s in x.bad.items()}, x.gather_ok, table), f"{out_path}.{rank}")
+    try:
+        table = route_table({T: {"ipc1": 1.0, "ipc2": 2.0} for T in (1, 4, 16)}, x.bad, False)
+    except RuntimeError as e:
+        table = str(e)
+    # the staging-sized chunked all-reduce honours the vetoes too (or refuses)
+    t = torch.full((3, 8), float(rank + 1)).to(torch.bfloat16)
+    try:
+        chunked = bool(torch.equal(x._all_reduce_chunked(t), torch.full((3, 8), 3.0).to(torch.bfloat16)))
+    except RuntimeError as e:
+        chunked = str(e)
+    torch.save((rep, {T: sorted(s) for T, s in x.bad.items()}, x.gather_ok, table, chunked), f"{out_path}.{rank}")
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("broken_algo,gather_broken", [(None, False), ("ipc1", False), ("ipc2", False), (None, True)])
+@pytest.mark.parametrize("broken_algo,gather_broken", [(None, False), ("ipc1", False), ("ipc2", False), (None, True),
+                                                       ("both", False)])
 def test_ipc_self_check_agrees_and_vetoes(broken_algo, gather_broken):
     """The start-up self-check (xgmi_ar.XgmiAllReduce.self_check) on a gloo world of 2 with a
     fake IPC state: a collective that is wrong on ONE rank is vetoed on BOTH (MAX agreement),
-    the routing table then avoids it, and a broken all-gather takes the group off the IPC path."""
+    the routing table and the chunked all-reduce then avoid it, a broken all-gather takes the
+    group off the IPC path, and a group with no RCCL whose every IPC all-reduce failed is
+    reported unusable (tune_collectives raises on ``ipc_disabled``) instead of routed."""
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "sc")
         mp.spawn(_selfcheck_worker, args=(2, port, path, 1, broken_algo, gather_broken), nprocs=2, join=True)
         res = [torch.load(f"{path}.{r}", weights_only=False) for r in range(2)]
-    (rep0, bad0, g0, t0), (rep1, bad1, g1, t1) = res
-    assert bad0 == bad1 and g0 == g1 and t0 == t1  # every rank routes alike
+    (rep0, bad0, g0, t0, c0), (rep1, bad1, g1, t1, c1) = res
+    assert bad0 == bad1 and g0 == g1 and t0 == t1 and c0 == c1  # every rank routes alike
+    if broken_algo == "both":
+        assert bad0 == {T: ["ipc1", "ipc2"] for T in (1, 4, 16)}
+        assert rep0["unusable_buckets"] == [1, 4, 16] and rep0["ipc_disabled"] is True
+        assert isinstance(t0, str) and "no RCCL" in t0          # route_table refuses
+        assert isinstance(c0, str) and "self-check" in c0       # chunked all-reduce refuses
+        return
     want = {T: ([broken_algo] if broken_algo else []) for T in (1, 4, 16)}
-    assert bad0 == want
+    assert bad0 == want and rep0["unusable_buckets"] == []
+    assert c0 is True
     if broken_algo:
         other = "ipc2" if broken_algo == "ipc1" else "ipc1"
         assert set(t0.values()) == {other}
