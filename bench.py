@@ -387,7 +387,7 @@ def main():
             ss, si = tp_knn_search(engine, knn_shard, qv, 6)
             knn_info = {"mode": f"sharded over tp{args.tp} ({knn_shard.corpus.shape[0]} rows per rank)",
                         "matches_single_scan": bool(torch.equal(si.cpu().long(), ci.cpu().long()))}
-            index.set_sharded(lambda q, k: tp_knn_search(engine, knn_shard, q, k))
+            index.set_sharded(lambda q, k: tp_knn_search(engine, knn_shard, q, k), dim=corpus.shape[1])
             log(rank, f"kNN: {knn_info}")
         k8s = FakeCluster.default()
         rag = RagAgentPipeline(index, engine, tok, k8s, cfg)
@@ -483,6 +483,11 @@ def main():
             prof.disable()
             prof.dump_stats(f"{os.environ['LK_PROFILE_TIMED']}.rank{rank}")
         trace, engine.step_trace = engine.step_trace, None
+        if os.environ.get("LK_STEP_TRACE_OUT"):  # every timed step's trace tuple, for offline analysis
+            with open(os.environ["LK_STEP_TRACE_OUT"], "w") as f:
+                json.dump({"fields": ["prefill_tokens", "decode_rows", "step_s", "schedule_s", "prepare_launch_s",
+                                      "sample_sync_s", "post_s", "gpu_s", "idle_before_s", "tag", "starved", "rows"],
+                           "steps": [list(t) for t in trace]}, f)
         # K / V bytes the decode attention read in the timed window (this rank's shard): over the
         # paged-decode kernel time of a timed-window trace, its in-situ bandwidth
         decode_kv_bytes = (engine.runner.decode_kv_keys - kv_keys0) * llm.kv_bytes_per_token()

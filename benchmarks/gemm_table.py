@@ -77,7 +77,7 @@ def main():
                       f"{arms[f'v{best[0]}/{best[1]}/k{best[2]}']:.1f} us  ({len(arms)} candidates)", flush=True)
             del w
     entries = sorted([list(k) + list(v) for k, v in ops._GEMM_TABLE.items()])
-    doc = {"device": torch.cuda.get_device_name(), "arch": "gfx950", "created": time.strftime("%Y-%m-%d"),
+    doc = {"device": torch.cuda.get_device_name(), "arch": "gfx950", "cus": ops.device_cus(), "created": time.strftime("%Y-%m-%d"),
            "source": "benchmarks/gemm_table.py (ops.tune_gemm: cold weights, median of round-robin timings)",
            "key": "[M bucket = ceil(M / 256), N, K, epilogue, variant, column tile, splits]",
            "entries": entries, "timings_us": timings}

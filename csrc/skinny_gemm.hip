@@ -637,7 +637,9 @@ void launch_ws(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks,
   constexpr size_t lds = (size_t)ws_stages(MT, BN) * (16 * MT * 128 + BN * 128);
   auto kern = wsgemm_kernel<MT, BN, SWIGLU>;
   LK_SET_MAX_LDS(kern, (int)lds);
-  const int rot_mul = g_ws_rot_mul >= 0 ? g_ws_rot_mul : (S == 1 ? 5 : 0);
+  // kNN scores (n_rows given: a corpus, not a weight) walk K in one order in every tile, so
+  // equal corpus rows score bit-identically and ties keep the stable id order
+  const int rot_mul = n_rows < (1L << 40) ? 0 : g_ws_rot_mul >= 0 ? g_ws_rot_mul : (S == 1 ? 5 : 0);
   kern<<<n_tiles * S, 256, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows, rot_mul);
 }
 
@@ -647,7 +649,7 @@ void launch_ws_lw(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int 
   constexpr size_t lds = (size_t)lw_nsx(MT) * 16 * MT * 128 + (size_t)lw_nsw(MT, BN) * BN * 128;
   auto kern = wsgemm_lw_kernel<MT, BN, SWIGLU>;
   LK_SET_MAX_LDS(kern, (int)lds);
-  const int rot_mul = g_ws_rot_mul >= 0 ? g_ws_rot_mul : (S == 1 ? 5 : 0);
+  const int rot_mul = n_rows < (1L << 40) ? 0 : g_ws_rot_mul >= 0 ? g_ws_rot_mul : (S == 1 ? 5 : 0);
   kern<<<n_tiles * S, 384, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows, rot_mul);
 }
 

@@ -58,15 +58,18 @@ int lk_embed_rows(bf16_t* out, const bf16_t* table, const int* ids, long T, int 
   return 0;
 }
 
-// ids outside the table counted by strict embed_rows launches since the last call (resets)
+// ids outside the table counted by strict embed_rows launches on the CURRENT device since the
+// last call for that device.  The device counter only grows (no read-then-reset race with a
+// kernel incrementing it in between); the host keeps the last value it saw per device.
 int lk_embed_errors() {
+  static int last[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
   int v = 0;
   if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_embed_bad_ids), sizeof(int)) != hipSuccess) return -1;
-  if (v) {
-    const int zero = 0;
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_embed_bad_ids), &zero, sizeof(int));
-  }
-  return v;
+  const int d = v - last[dev];  // (wraps only after 2^31 bad ids)
+  last[dev] = v;
+  return d;
 }
 
 int lk_scatter_ids(int* ids, const long* dst, const int* prev, const long* src, int n, hipStream_t st) {

@@ -431,7 +431,7 @@ def _shard_served_index(idx, engine):
         return None
     corpus = idx._gpu[0] if idx._gpu is not None else torch.from_numpy(idx.matrix())
     shard = tp_shard_corpus(engine, corpus)
-    idx.set_sharded(lambda q, k: tp_knn_search(engine, shard, q, k))
+    idx.set_sharded(lambda q, k: tp_knn_search(engine, shard, q, k), dim=corpus.shape[1])
     print(f"[rag] {len(idx)} chunks sharded over tp{engine.tp_ctrl.tp.size} "
           f"({shard.corpus.shape[0]} rows on the leader)", flush=True)
     return shard

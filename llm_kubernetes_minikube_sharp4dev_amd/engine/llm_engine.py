@@ -278,7 +278,7 @@ class LLMEngine:
                     self.scheduler.publish_blocks(seq)
             self.steps += 1
             if self.steps % GEMM_HEALTH_EVERY == 0 and self.model.device.type == "cuda":
-                self._check_gemm_health()
+                self._check_gemm_health(self.model.device)
             if self.step_trace is not None:
                 t3 = time.perf_counter()
                 ndec = len(batch.items) - sum(1 for sq, st, n in batch.items if st < len(sq.prompt_ids))
@@ -293,10 +293,10 @@ class LLMEngine:
                     self._trace_end_ev = ev
                 # (prefill tokens, decode rows, step s, schedule s, prepare+launch s, sample+sync s, post s,
                 #  GPU s from the step's first kernel to its ids copy, device idle before it, caller tag,
-                #  device already idle when the launch began)
+                #  device already idle when the launch began, total token rows of the step)
                 self.step_trace.append((npre, ndec, t3 - t0, t0 - ts, t1 - t0,
                                         (t2 - t1) if rows else 0.0, (t3 - t2) if rows else 0.0, gpu, idle,
-                                        launched_note, starved))
+                                        launched_note, starved, batch.num_tokens))
             M.STEP_TOKENS.observe(batch.num_tokens)
             M.STEP_TIME.observe(time.perf_counter() - t0)
             M.KV_USAGE.set(self.allocator.usage())
@@ -304,7 +304,7 @@ class LLMEngine:
             return out
 
     @staticmethod
-    def _check_gemm_health():
+    def _check_gemm_health(device=None):
         """Fail loudly if a stream-K prefill GEMM gave up waiting for a partial tile since the
         last check (csrc/gemm.hip poisons such a tile with NaN; never expected: the wait is a
         bound instead of a hang), or a token id outside the vocabulary reached the embedding
@@ -316,7 +316,10 @@ class LLMEngine:
         errs = int(ops.lib().gemm_streamk(-1))
         if errs:
             raise RuntimeError(f"stream-K GEMM: {errs} partial-tile wait(s) timed out; outputs were poisoned")
-        bad = int(ops.lib().embed_errors())
+        import torch
+
+        with torch.cuda.device(device if device is not None else torch.cuda.current_device()):
+            bad = int(ops.lib().embed_errors())  # this engine's device's counter
         if bad:
             raise RuntimeError(f"embedding: {bad} token id(s) outside the vocabulary were looked up (a tokenizer / "
                                f"model vocab mismatch); their rows were zero")

@@ -5,6 +5,7 @@ Layouts are documented in :mod:`.reference`.
 """
 from __future__ import annotations
 
+import logging
 import math
 import os
 from typing import Optional, Sequence
@@ -390,6 +391,30 @@ _STATIC: Optional[dict] = None
 _STATIC_TOP: dict = {}  # (N, K, epi) -> largest measured M bucket
 
 
+_CUS: Optional[int] = None
+
+
+def device_cus() -> int:
+    """Compute units of the current device (256 on a whole MI355X; fewer on a partitioned one,
+    e.g. CPX mode): the wave size every tile-count policy below quantises against.  256 without a
+    GPU (CPU runs never dispatch GPU kernels)."""
+    global _CUS
+    if _CUS is None:
+        _CUS = 256
+        if torch.cuda.is_available():
+            _CUS = int(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count) or 256
+    return _CUS
+
+
+def _table_matches_device(doc: dict) -> bool:
+    """The shipped table was measured on one device configuration: use it only on the same arch
+    and CU count (a partitioned MI355X has different waves, so its measured picks do not apply)."""
+    if not torch.cuda.is_available():
+        return True
+    arch = getattr(torch.cuda.get_device_properties(torch.cuda.current_device()), "gcnArchName", "") or ""
+    return arch.split(":")[0] == doc.get("arch", "gfx950") and int(doc.get("cus", 256)) == device_cus()
+
+
 def _static_table() -> dict:
     global _STATIC
     if _STATIC is None:
@@ -398,9 +423,14 @@ def _static_table() -> dict:
             import json
 
             with open(GEMM_TABLE_FILE) as f:
-                for mb, n, k, epi, v, bn, ks in json.load(f)["entries"]:
-                    _STATIC[(mb, n, k, epi)] = (v, bn, ks)
-                    _STATIC_TOP[(n, k, epi)] = max(mb, _STATIC_TOP.get((n, k, epi), 0))
+                doc = json.load(f)
+            if not _table_matches_device(doc):
+                logging.getLogger("lk.ops").warning("gemm table %s was measured on %s / %s CUs; this device differs: not used",
+                            GEMM_TABLE_FILE, doc.get("arch"), doc.get("cus", 256))
+                return _STATIC
+            for mb, n, k, epi, v, bn, ks in doc["entries"]:
+                _STATIC[(mb, n, k, epi)] = (v, bn, ks)
+                _STATIC_TOP[(n, k, epi)] = max(mb, _STATIC_TOP.get((n, k, epi), 0))
     return _STATIC
 
 
@@ -444,9 +474,10 @@ GEMM1W_SPLIT = {6: 128, 7: 192}
 SPLIT_ON = os.environ.get("LK_GEMM_SPLIT", "1") != "0"  # 0: measured 6 / 7 entries run as variant 3 (A/B)
 
 
-def gemm1w_split_cols(M: int, N: int, epi: int, cus: int = 256) -> int:
-    """Column tiles a variant 6 / 7 launch runs on 256-row tiles (mirrors lk_gemm1w_split_cols);
-    0 or all of them: no split (the launch is variant 3's)."""
+def gemm1w_split_cols(M: int, N: int, epi: int, cus: Optional[int] = None) -> int:
+    """Column tiles a variant 6 / 7 launch runs on 256-row tiles (mirrors lk_gemm1w_split_cols,
+    which uses the device's CU count too); 0 or all of them: no split (the launch is variant 3's)."""
+    cus = cus or device_cus()
     tn = N // 256
     tm = (M + 255) // 256
     return min(tn, (tm * tn // cus) * cus // tm)
@@ -472,10 +503,11 @@ def _gemm_default(M: int, N: int, K: int, epi: int):
     instead once its tiles fill a wave, and its 192-row tiles where 256-row tiles would leave
     over a third of a single wave idle while 192-row ones still fit in one."""
     tm = (M + 255) // 256
+    cus = device_cus()
     best = None
     for _, bn in _gemm_configs(N, epi):
         n_cols = N // 2 // 128 if epi == 1 else N // bn
-        cost = -(-tm * n_cols // 256) * (256 if epi == 1 else bn)
+        cost = -(-tm * n_cols // cus) * (256 if epi == 1 else bn)
         if best is None or cost < best[0]:
             best = (cost, bn)
     if best is None:
@@ -487,7 +519,7 @@ def _gemm_default(M: int, N: int, K: int, epi: int):
         if tiles >= GEMM1W_MIN_TILES:
             return (3, 256, 1)
         tiles192 = -(-M // 192) * (N // 2 // 128 if epi == 1 else N // 256)
-        if tiles < 0.7 * 256 and tiles192 <= 256:
+        if tiles < 0.7 * cus and tiles192 <= cus:
             return (4, 256, 1)
     return (_gemm_sched(K), bn, ks)
 
@@ -508,7 +540,7 @@ def _gemm_splits(M: int, N: int, K: int, epi: int, bn: int) -> int:
         # long K just past half a wave: three K-ranges give ~1.7-1.9 waves of tiles
         # (M 2304 / 2560 down projection: 295 -> 278, 277 -> 255 us; from 176 tiles on, worse)
         return 3 if tiles <= 160 and K >= 8192 else 1
-    return max(1, min(4, 256 // tiles, K // 64 // 8))
+    return max(1, min(4, device_cus() // tiles, K // 64 // 8))
 
 
 def _gemm_ok(x, w) -> bool:

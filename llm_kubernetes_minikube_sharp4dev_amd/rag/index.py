@@ -145,13 +145,18 @@ class RagIndex:
         return self._mat
 
     def _use_gpu(self) -> bool:
-        if getattr(self, "_sharded", None) is not None:
-            return True
         if self.backend == "gpu":
-            return True
-        if self.backend == "exact":
-            return False
-        return self.device.type == "cuda" and len(self.chunks) >= self.gpu_threshold
+            local = True
+        elif self.backend == "exact":
+            local = False
+        else:
+            local = self.device.type == "cuda" and len(self.chunks) >= self.gpu_threshold
+        if getattr(self, "_sharded", None) is not None:
+            # the sharded scan ranks exactly like the single-GPU bf16 scan; where this process
+            # would score on the host instead (backend 'exact', or 'auto' below the threshold) and
+            # still holds the fp32 matrix, it does -- so a TP server ranks near-ties like TP=1
+            return local or not self._emb
+        return local
 
     def gpu_tensors(self):
         if self._gpu is None:
@@ -163,12 +168,14 @@ class RagIndex:
         """Attach a corpus matrix produced directly on the GPU (bulk index builds)."""
         self._gpu = (corpus_bf16.contiguous(), norms if norms is not None else ops.row_norms(corpus_bf16))
 
-    def set_sharded(self, search_fn):
+    def set_sharded(self, search_fn, dim: Optional[int] = None):
         """Route searches through a corpus-sharded kNN: ``search_fn(queries [nq, D] bf16, k) ->
         (scores f32 [nq, k], ids int32 [nq, k])`` (parallel.tp_engine.tp_knn_search: every TP
         rank scans its shard, merged in the single-scan order).  None restores the local scan.
-        With a sharded search this process keeps no device copy of the corpus."""
+        With a sharded search this process keeps no device copy of the corpus; ``dim`` (the
+        corpus width) lets a mismatched query fail here rather than inside the sharded kNN."""
         self._sharded = search_fn
+        self._sharded_dim = dim
         if search_fn is not None:
             self._gpu = None
 
@@ -186,6 +193,9 @@ class RagIndex:
         sharded = getattr(self, "_sharded", None)
         if sharded is not None:
             # the shard's dtype (bf16 on the GPU, f32 on the CPU) is applied by the search
+            dim = getattr(self, "_sharded_dim", None)
+            if dim is not None and qt.shape[-1] != dim:
+                raise ValueError(f"query width {qt.shape[-1]} != corpus width {dim}")
             s, i = sharded(qt.reshape(-1, qt.shape[-1]), min(k, 64))
         else:
             corpus, norms = self.gpu_tensors()

@@ -1035,3 +1035,53 @@ def test_invalid_launch_raises(hip):
     x = torch.randn(4, 768, device=DEV, dtype=torch.bfloat16)
     w = torch.ones(768, device=DEV, dtype=torch.bfloat16)
     _close(hip.rmsnorm(x, w, 1e-5, None, None), ref.rmsnorm(x, w, 1e-5, None), 0.05, 0.01, "after a failed launch")
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_knn_topk_config4_scale(hip, fused):
+    """BASELINE config 4's index size: 1M runbook documents -> ~4.86M chunks x 768 (7.5 GB bf16,
+    past every 32-bit byte offset and 4 GB buffer range), vs an fp32 reference computed in
+    row chunks.  Exact duplicates planted far apart (different tiles, different halves of the
+    corpus) must tie bit-identically and come back in id order; the last row (a partial tail
+    tile) must be found."""
+    N, D, K = 4_900_000, 768, 6
+    g = torch.Generator(device=DEV).manual_seed(21)
+    corpus = torch.empty(N, D, device=DEV, dtype=torch.bfloat16)
+    for a in range(0, N, 1 << 20):
+        b = min(N, a + (1 << 20))
+        corpus[a:b] = torch.randn(b - a, D, device=DEV, generator=g).to(torch.bfloat16)
+    dup = (123, 3_000_000, 4_800_000)
+    for j in dup[1:]:
+        corpus[j] = corpus[dup[0]]
+    qs = torch.randn(8, D, device=DEV, generator=g).to(torch.bfloat16)
+    qs[0] = corpus[dup[0]]
+    qs[1] = corpus[N - 1]
+    qs[2] = corpus[2_500_000] * 0.5 + qs[2] * 0.1
+    cn, qn = hip.row_norms(corpus), hip.row_norms(qs)
+    s, i = hip.knn_topk(corpus, cn, qs, qn, K, fused)
+    torch.cuda.synchronize()
+    # fp32 reference: per 1M-row chunk, the best 64 candidates, then a stable (score, id) merge
+    qf = qs.float()
+    cand_s, cand_i = [], []
+    for a in range(0, N, 1 << 20):
+        b = min(N, a + (1 << 20))
+        sc = (qf @ corpus[a:b].float().T) / (qf.norm(dim=1, keepdim=True) * corpus[a:b].float().norm(dim=1)[None] + 1e-9)
+        ts, ti = sc.topk(64, dim=1)
+        cand_s.append(ts.cpu())
+        cand_i.append((ti + a).cpu())
+    cs, ci = torch.cat(cand_s, 1), torch.cat(cand_i, 1)
+    s, i = s.cpu(), i.cpu().long()
+    for q in range(8):
+        order = sorted(range(cs.shape[1]), key=lambda j: (-float(cs[q, j]), int(ci[q, j])))[:K]
+        want_i = [int(ci[q, j]) for j in order]
+        want_s = [float(cs[q, j]) for j in order]
+        ref_of = {int(ci[q, j]): float(cs[q, j]) for j in range(cs.shape[1])}
+        assert bool((s[q, 1:] <= s[q, :-1]).all()), f"query {q}: scores not descending"
+        for j in range(K):
+            got = int(i[q, j])
+            assert abs(float(s[q, j]) - want_s[j]) < 2e-3, (q, j, float(s[q, j]), want_s[j])
+            if got != want_i[j]:  # only a near-tie may reorder
+                assert got in ref_of and abs(ref_of[got] - want_s[j]) < 2e-3, (q, j, got, want_i[j])
+    assert i[0, :3].tolist() == list(dup), i[0].tolist()
+    assert float(s[0, 0]) == float(s[0, 1]) == float(s[0, 2])
+    assert int(i[1, 0]) == N - 1 and int(i[2, 0]) == 2_500_000

@@ -302,3 +302,27 @@ def test_continuous_load_rag_agent_mixed(mode):
         assert all(r.status in (200, 400, 404, 500) for r in out)
         assert all(r.output_tokens in (0, 4) for r in out)
         assert not eng.has_work()
+
+
+def test_sharded_search_keeps_the_local_exact_policy():
+    """With a sharded kNN attached (``all --tp``), a corpus this process would score exactly on
+    the host (backend 'exact' / 'auto' under the GPU threshold) is still scored there -- the TP
+    server ranks near-ties like the TP=1 one -- and a query of the wrong width fails at the index."""
+    import torch
+
+    idx = RagIndex(HashEmbedder(64), backend="auto", device="cpu")
+    idx.build_from_folder(os.path.dirname(RUNBOOK))
+    calls = []
+
+    def fake_sharded(q, k):
+        calls.append(q.shape)
+        return torch.zeros(q.shape[0], k), torch.zeros(q.shape[0], k, dtype=torch.int32)
+
+    want = idx.query("scale the deployment", top_k=3)
+    idx.set_sharded(fake_sharded, dim=64)
+    assert [h.id for h in idx.query("scale the deployment", top_k=3)] == [h.id for h in want] and not calls
+    idx.backend = "gpu"  # the local policy would scan on the device: the sharded scan serves it
+    idx.search_vectors(np.ones((2, 64), np.float32), 3)
+    assert calls == [(2, 64)]
+    with pytest.raises(ValueError, match="query width"):
+        idx.search_vectors(np.ones((1, 32), np.float32), 3)
