@@ -218,8 +218,11 @@ def main():
         # several processes' hardware queues share the device: at 4 per process the scheduler
         # time-slices 8 ranks and every all-reduce waits for its peers' turn (0.08 vs 2.46 q/s at
         # 2 per process, profiles/r4_tp8_onedev/); read when HIP initialises, so set it first
-        if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) > 2:
-            os.environ["GPU_MAX_HW_QUEUES"] = "2"
+        # (LK_ONE_DEVICE_HW_QUEUES: another cap, e.g. 4 for a 2-rank trace whose comm stream
+        # needs a hardware queue of its own to overlap the compute stream)
+        cap = int(os.environ.get("LK_ONE_DEVICE_HW_QUEUES", "2"))
+        if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) > cap:
+            os.environ["GPU_MAX_HW_QUEUES"] = str(cap)
     if on_gpu:
         assert torch.cuda.is_available(), "bench.py needs an MI355X (or --device cpu)"
         if args.one_device:
@@ -634,9 +637,14 @@ def main():
                 # bytes at XGMI_LINK_GBPS per link (a model figure); 2 tails per layer + the
                 # vocab-parallel embedding all-reduce
                 W, Hd, n_ar = args.tp_sim, lc.hidden, 2 * lc.num_layers + 1
-                est = {"floor_source": floor["_path"], "link_GBps_model": XGMI_LINK_GBPS, "hbm_GBps_model": HBM_GBPS}
+                est = {"floor_source": floor["_path"], "link_GBps_model": XGMI_LINK_GBPS, "hbm_GBps_model": HBM_GBPS,
+                       "gemm_TFLOPs_model": GEMM_TFLOPS,
+                       # prefill-sized steps run their o / down tails in row chunks overlapped with
+                       # the next chunk's GEMM (models/llama.py _post_attn_pipelined): only the exposed part counts
+                       "overlap": "prefill-sized steps: post-attention half of each layer pipelined over row "
+                                  "chunks (compute o / mlp, comm tails); exposed = pipeline makespan - compute"}
                 for name, up in (("upper", True), ("latency_floor_plus_bytes", False)):
-                    per_step = [n_ar * _per_call_us(floor, t[0] + t[1], Hd, W, up) for t in trace]
+                    per_step = [_exposed_step_us(floor, t[0] + t[1], lc, W, up) for t in trace]
                     tot_s = sum(per_step) / 1e6
                     est[name] = {
                         "ms_per_step": round(1e3 * tot_s / max(1, len(trace)), 3),
@@ -835,6 +843,49 @@ def _floor_us(floor: dict, rows: int, algo: str) -> float:
 
 
 HBM_GBPS = 5000.0  # streaming rate of one MI355X's HBM3E under these kernels (model figure)
+GEMM_TFLOPS = 1300.0  # in-situ prefill GEMM rate (profiles/r5_prof_window: ~1.3-1.5 PF/s; model figure)
+
+
+def _exposed_step_us(floor: dict, rows: int, lc, world: int, upper: bool = True) -> float:
+    """Collective time one TP step exposes: the vocab-parallel embedding all-reduce, then per
+    layer the o and down tails -- whole (decode-sized steps), or, for steps models/llama.py
+    chunks, the makespan of its pipeline (compute stream o(c) | mlp(c-1) | ..., communication
+    stream tail_o(c), tail_down(c-1), ...; GEMMs at their shard FLOPs / GEMM_TFLOPS) minus
+    the compute it contains."""
+    from llm_kubernetes_minikube_sharp4dev_amd.models.llama import overlap_chunks
+
+    H = lc.hidden
+    total = _per_call_us(floor, rows, H, world, upper)  # embedding all-reduce (not chunked)
+    chunks = overlap_chunks(rows)
+    if chunks is None:
+        return total + lc.num_layers * 2 * _per_call_us(floor, rows, H, world, upper)
+    k_o, inter = lc.num_heads * lc.head_dim // world, lc.intermediate // world
+    rate = GEMM_TFLOPS * 1e6  # flop per us
+    t_main = t_comm = busy = 0.0
+    ev_o, prev = {}, None
+
+    def tail(c):
+        nonlocal t_comm
+        t_comm = max(t_comm, t_main) + _per_call_us(floor, c[1] - c[0], H, world, upper)
+        return t_comm
+
+    def mlp(c):
+        nonlocal t_main, busy
+        g = 2.0 * (c[1] - c[0]) * H * 3 * inter / rate  # gate_up (2 I / W) + down (I / W)
+        t_main = max(t_main, ev_o[c]) + g
+        busy += g
+        tail(c)
+
+    for c in chunks:
+        g = 2.0 * (c[1] - c[0]) * k_o * H / rate
+        t_main += g
+        busy += g
+        ev_o[c] = tail(c)
+        if prev is not None:
+            mlp(prev)
+        prev = c
+    mlp(prev)
+    return total + lc.num_layers * (max(t_main, t_comm) - busy)
 
 
 def _per_call_us(floor: dict, rows: int, hidden: int, world: int, upper: bool = True) -> float:

@@ -151,7 +151,13 @@ def main():
             spans.update(httpx.get(f"http://127.0.0.1:{p1}/debug/spans", params={"since": since}, timeout=30).json())
             res[str(c)]["app_spans_ms"] = {k.split(".", 1)[1]: {"mean": round(v["mean_s"] * 1e3, 1),
                                                                   "p50": round(v["p50_s"] * 1e3, 1)}
-                                           for k, v in spans.items()}
+                                           for k, v in spans.items() if "mean_s" in v}
+            # the served engine's per-request accounting (prompt / cached-prefix / uncached tokens,
+            # preemptions, engine steps queued and run): compare with bench.py's in-process JSON
+            # (split server: the engine core's own counters, "core.*"; else the server's)
+            src = "core." if any(k.startswith("core.req_") for k in spans) else "server."
+            res[str(c)]["server_accounting"] = {k.split(".", 1)[1]: round(v["mean"], 2)
+                                                for k, v in spans.items() if "mean" in v and k.startswith(src)}
             print(f"[http_bench] concurrency {c}: {res[str(c)]}", file=sys.stderr, flush=True)
         top = res[str(levels[-1])]
         out = {"metric": f"RAG queries/sec via HTTP (/agent_rag -> /api/embeddings + /api/generate), "

@@ -99,6 +99,7 @@ class LLMEngine:
         # optional per-step trace: (prefill tokens, decode rows, wall seconds) -- bench.py
         self.step_trace: Optional[list] = None
         self._trace_end_ev = None  # the last traced step's ids-copy event (device idle before the next)
+        self._trace_lazy = None    # (trace index, start, end) of a rowless step timed at the next one
         self._last_ids_ev = None   # the most recently recorded ids-copy event (starvation check)
         self.trace_note = ""       # caller's tag for the host work before the next launch (bench)
 
@@ -248,6 +249,11 @@ class LLMEngine:
                     s.num_inflight, s.inflight_row = 1, i
             self.runner.prev_ids = ids
             self.runner.prev_sampled_rows = 0 if greedy else len(rows)
+        elif ev0 is not None:
+            # a step with no sampled rows (a prompt chunk that does not end its prompt): its end
+            # still bounds the traced GPU time, so the next step's idle is not charged with it
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
         return (batch, rows, host, ev, ts, t0, t1, time.perf_counter(), ev0n)
 
     def _collect(self, pending) -> list:
@@ -283,11 +289,24 @@ class LLMEngine:
                 t3 = time.perf_counter()
                 ndec = len(batch.items) - sum(1 for sq, st, n in batch.items if st < len(sq.prompt_ids))
                 npre = sum(n for sq, st, n in batch.items if st < len(sq.prompt_ids))
-                gpu = ev0.elapsed_time(ev) / 1e3 if (ev0 is not None and ev is not None) else 0.0
+                # (a rowless step's end event is not waited for: its GPU time is filled in at the
+                # next traced step, whose own wait has completed it)
+                done = bool(rows) and ev is not None  # this step's end was waited for
+                if self._trace_lazy is not None and done:
+                    k, e0, e1, pe = self._trace_lazy
+                    if k < len(self.step_trace):
+                        t = self.step_trace[k]
+                        idl = max(0.0, pe.elapsed_time(e0) / 1e3) if pe is not None else 0.0
+                        self.step_trace[k] = t[:7] + (e0.elapsed_time(e1) / 1e3, idl) + t[9:]
+                    self._trace_lazy = None
+                gpu = ev0.elapsed_time(ev) / 1e3 if (ev0 is not None and done) else 0.0
                 # device idle between the previous traced step's ids copy and this step's start
                 # marker: > 0 when the host reached this launch after the device ran dry
                 idle = 0.0
-                if ev0 is not None and self._trace_end_ev is not None:
+                if ev0 is not None and ev is not None and not rows:
+                    if self._trace_lazy is None:
+                        self._trace_lazy = (len(self.step_trace), ev0, ev, self._trace_end_ev)
+                elif ev0 is not None and self._trace_end_ev is not None and done:
                     idle = max(0.0, self._trace_end_ev.elapsed_time(ev0) / 1e3)
                 if ev is not None:
                     self._trace_end_ev = ev

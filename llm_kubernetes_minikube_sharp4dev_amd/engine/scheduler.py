@@ -10,6 +10,8 @@ is recomputed later — usually mostly from the prefix cache).
 """
 from __future__ import annotations
 
+import os
+
 import time
 from collections import deque
 from dataclasses import dataclass, field
@@ -63,6 +65,12 @@ class Scheduler:
         # 4096-row step fills the chip's 256 CUs exactly once on the N = 4096 projections
         # (o / down), a 5120-row step runs 1.25 waves of them
         self.token_align_wave = token_align_wave
+        # ... but only in steps with at least this many decode rows: they guarantee the next step
+        # runs anyway, so the trimmed tokens ride in it.  A step of (almost) only prefill -- low
+        # load, e.g. one request in flight -- would otherwise split a prompt's last chunk into a
+        # step of its own: one more weight pass on the request's critical path (batch 1: a 627-row
+        # prompt ran as 512 + 115 rows, ~4 ms of its time to first token)
+        self.align_min_decode = int(os.environ.get("LK_ALIGN_MIN_DECODE", "32"))
         self.bs = block_size
         self.max_num_seqs = max_num_seqs
         self.max_tokens = max_num_batched_tokens
@@ -230,6 +238,8 @@ class Scheduler:
         if not a:
             return
         total = batch.num_tokens
+        if sum(1 for _, _, n in batch.items if n == 1) < self.align_min_decode:
+            return
         if self.token_align_wave and total > self.token_align_wave:
             a = self.token_align_wave
         ex = total % a

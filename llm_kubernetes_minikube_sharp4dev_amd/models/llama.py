@@ -41,6 +41,33 @@ from .configs import DecoderConfig, pad_vocab
 # LK_FOLD_NORMS=0 keeps the checkpoint layout (and with it the unfused prefill path)
 FOLD_NORMS = os.environ.get("LK_FOLD_NORMS", "1") != "0"
 
+# Tensor-parallel prefill: the post-attention half of a layer (o -> all-reduce + norm -> gate_up
+# -> down -> all-reduce + norm) of a step of at least TP_OVERLAP_MIN_ROWS rows runs as
+# TP_OVERLAP_CHUNKS row chunks (multiples of TP_OVERLAP_ALIGN rows) in a software pipeline: every
+# all-reduce + residual + RMSNorm tail runs on a communication stream while the compute stream
+# runs the next chunk's GEMMs (those rows are independent once attention is done), so only the
+# last chunk's down tail is exposed (the 70B TP=8 budget: 160 tails of up to 64 MB per mixed
+# step, ~17 ms two-shot against 50.7 ms of compute when serialised, BASELINE.md).  The o tail
+# alone cannot hide behind its own GEMM (o's shard is 1/8 the FLOPs of the MLP's): the MLP of
+# the previous chunk covers it.  LK_TP_OVERLAP=0: whole-step GEMMs, then their tails.
+TP_OVERLAP = os.environ.get("LK_TP_OVERLAP", "1") != "0"
+TP_OVERLAP_MIN_ROWS = int(os.environ.get("LK_TP_OVERLAP_MIN_ROWS", "1024"))
+TP_OVERLAP_CHUNKS = int(os.environ.get("LK_TP_OVERLAP_CHUNKS", "4"))
+TP_OVERLAP_ALIGN = int(os.environ.get("LK_TP_OVERLAP_ALIGN", "256"))
+
+
+def overlap_chunks(T: int, chunks: int = None, align: int = None, min_rows: int = None) -> Optional[list]:
+    """[(r0, r1)] row chunks of a T-row row-parallel tail (None: do not chunk)."""
+    chunks = TP_OVERLAP_CHUNKS if chunks is None else chunks
+    align = TP_OVERLAP_ALIGN if align is None else align
+    min_rows = TP_OVERLAP_MIN_ROWS if min_rows is None else min_rows
+    if not TP_OVERLAP or chunks < 2 or T < max(min_rows, 2 * align):
+        return None
+    per = -(-T // chunks)
+    per = -(-per // align) * align
+    out = [(a, min(T, a + per)) for a in range(0, T, per)]
+    return out if len(out) > 1 else None
+
 
 class LlamaLayerWeights(nn.Module):
     def __init__(self, cfg: DecoderConfig, tp: TPGroup, dtype, device):
@@ -87,6 +114,8 @@ class LlamaModel(nn.Module):
         # steps of at least this many rows run sequence-parallel under TP (None: never)
         sp = os.environ.get("LK_SP_MIN_TOKENS")
         self.sp_min_tokens: Optional[int] = int(sp) if sp else None
+        self._comm_stream = None  # TP prefill: the row-parallel tails' stream (_post_attn_pipelined)
+        self.overlap_tails = 0    # layers whose post-attention half ran chunked + overlapped
         # RoPE pairs: rotate_half (i, i + D/2) as in HF checkpoints, or adjacent (2i, 2i + 1) once
         # fold_norms has permuted the q / k rows (what the fused QKV epilogue rotates)
         self.rope_neox = True
@@ -169,12 +198,65 @@ class LlamaModel(nn.Module):
                 x = ops.linear_add_rmsnorm(a, L.down, res, nxt, cfg.norm_eps)
                 continue
             # row-parallel tails: all-reduce + residual add + RMSNorm (one kernel on the xGMI path)
+            chunks = None
+            if not (attn_out.is_cuda and torch.cuda.is_current_stream_capturing()):
+                chunks = overlap_chunks(attn_out.shape[0])
+            if chunks is not None:
+                x = self._post_attn_pipelined(attn_out, L, res, nxt, cfg.norm_eps, chunks)
+                continue
             x = self.tp.all_reduce_rmsnorm(ops.linear(attn_out, L.o), res, L.post_norm, cfg.norm_eps)
             a = ops.linear_swiglu(x, L.gate_up)
             x = self.tp.all_reduce_rmsnorm(ops.linear(a, L.down), res, nxt, cfg.norm_eps)
         if meta.logits_idx is not None:
             x = ops.gather_rows(x, meta.logits_idx)
         return x
+
+    def _post_attn_pipelined(self, attn_out: torch.Tensor, L, res: torch.Tensor, nxt: torch.Tensor, eps: float,
+                             chunks: list) -> torch.Tensor:
+        """The post-attention half of a TP layer over row ``chunks``: compute stream
+        o(c) | mlp(c-1) | o(c+1) | mlp(c) ..., communication stream tail_o(c), tail_down(c-1), ...
+        (mlp = gate_up + SwiGLU + down; tail = all-reduce + residual add + RMSNorm into the rows
+        of this step's output).  ``res`` is updated in place, chunk by chunk, in the same order
+        as the unchunked path; every rank issues the same collectives in the same order.
+        Returns the next layer's normed input rows."""
+        self.overlap_tails += 1
+        tp = self.tp
+        x1 = torch.empty_like(res)   # post-attention normed rows (gate_up input)
+        out = torch.empty_like(res)  # next layer's normed input rows
+        if not attn_out.is_cuda:     # (CPU / gloo: the same chunks, one after the other)
+            for a, b in chunks:
+                tp.all_reduce_rmsnorm(ops.linear(attn_out[a:b], L.o), res[a:b], L.post_norm, eps, out=x1[a:b])
+                d = ops.linear(ops.linear_swiglu(x1[a:b], L.gate_up), L.down)
+                tp.all_reduce_rmsnorm(d, res[a:b], nxt, eps, out=out[a:b])
+            return out
+        main = torch.cuda.current_stream(attn_out.device)
+        comm = self._comm_stream
+        if comm is None or comm.device != attn_out.device:
+            comm = self._comm_stream = torch.cuda.Stream(attn_out.device)
+
+        def tail(y, a, b, w, dst):
+            comm.wait_stream(main)  # y's GEMM (and everything queued before it) is done
+            with torch.cuda.stream(comm):
+                tp.all_reduce_rmsnorm(y, res[a:b], w, eps, out=dst[a:b])
+                ev = torch.cuda.Event()
+                ev.record(comm)
+            y.record_stream(comm)
+            return ev
+
+        def mlp(a, b, ev_o):
+            main.wait_event(ev_o)  # chunk's o tail has produced its normed rows
+            d = ops.linear(ops.linear_swiglu(x1[a:b], L.gate_up), L.down)
+            tail(d, a, b, nxt, out)
+
+        prev = None
+        for a, b in chunks:
+            ev = tail(ops.linear(attn_out[a:b], L.o), a, b, L.post_norm, x1)
+            if prev is not None:
+                mlp(*prev)
+            prev = (a, b, ev)
+        mlp(*prev)
+        main.wait_stream(comm)
+        return out
 
     def _forward_chain(self, res: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
         """Prefill-sized step of a folded model: per block QKV (+ input-norm scale, RoPE, KV

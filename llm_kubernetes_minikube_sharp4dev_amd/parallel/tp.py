@@ -65,18 +65,19 @@ class TPGroup:
         return t
 
     def all_reduce_rmsnorm(self, x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
-                           eps: float) -> torch.Tensor:
+                           eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """RMSNorm(allreduce(x) + residual) * w, residual updated in place: the tail of every
         row-parallel projection.  On the IPC path ONE kernel (csrc/xgmi_allreduce.hip, one- or
-        two-shot by the measured table); otherwise RCCL all-reduce + the fused add+norm kernel."""
+        two-shot by the measured table); otherwise RCCL all-reduce + the fused add+norm kernel.
+        ``out``: write the normed rows there (a row slice of a bigger buffer)."""
         from .. import ops
 
         if self.size > 1 and self._ipc(x) and self.xgmi.eligible_rows(x, residual):
             algo = self.xgmi.algo(x.shape[0], x.numel() * 2)
             if algo != "rccl":
-                return self.xgmi.all_reduce_rmsnorm_(x, residual, w, eps, algo=algo)
+                return self.xgmi.all_reduce_rmsnorm_(x, residual, w, eps, out=out, algo=algo)
         self.all_reduce_(x)
-        return ops.rmsnorm(x, w, eps, residual=residual)
+        return ops.rmsnorm(x, w, eps, residual=residual, out=out)
 
     def reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:
         """Sum over ranks of t [size*n, ...], this rank's rows [rank*n, (rank+1)*n)."""

@@ -70,6 +70,27 @@ def sp_to_wire(sp: SamplingParams) -> dict:
     return {k: getattr(sp, k) for k in SP_FIELDS}
 
 
+def _accounting(seq) -> dict:
+    """Per-request engine accounting sent with a request's last token (front-ends report it)."""
+    q = (seq.step_first - seq.step_arrival) if getattr(seq, "step_first", None) is not None else None
+    return {"cached": seq.num_cached_prefix, "preempt": getattr(seq, "num_preemptions", 0),
+            "queued": q, "run": getattr(seq, "steps_run", None), "jumped": getattr(seq, "jumped", 0)}
+
+
+def _count_request(seq):
+    """The finished request's accounting as per-request counters in this (core) process."""
+    from ..utils import tracing
+
+    a = _accounting(seq)
+    n = len(seq.prompt_ids)
+    for name, v in (("req_prompt_tokens", n), ("req_cached_prefix_tokens", a["cached"]),
+                    ("req_uncached_prompt_tokens", n - a["cached"]), ("req_output_tokens", len(seq.output_ids)),
+                    ("req_preemptions", a["preempt"]), ("req_steps_queued", a["queued"]),
+                    ("req_steps_run", a["run"]), ("req_jumped_tokens", a["jumped"])):
+        if v is not None:
+            tracing.count("core", name, v)
+
+
 class _Conn:
     """One front-end connection: a reader thread (ops in) and a writer thread that sends the
     tokens the engine appended since the last frame as one frame."""
@@ -87,8 +108,11 @@ class _Conn:
 
     # -- engine thread side ------------------------------------------------------
     def on_token(self, rid, seq, tid, fin):
+        if fin:
+            _count_request(seq)
+        # a finished request carries its engine accounting (cached prefix, preemptions, steps)
         item = [rid, tid, fin, (seq.finish_reason or "stop") if fin else None,
-                seq.num_cached_prefix if fin else None, getattr(seq, "error", None) if tid < 0 else None]
+                _accounting(seq) if fin else None, getattr(seq, "error", None) if tid < 0 else None]
         with self.lock:
             self.pending.append(item)
         self.wake.set()
@@ -230,6 +254,10 @@ class EngineCore:
         elif op == "load":
             _, rid, model = msg
             self._pool.submit(self._load, conn, rid, model)
+        elif op == "spans":  # this process's span / counter summary (front-end /debug/spans)
+            from ..utils import tracing
+
+            conn.post(["spans", msg[1], tracing.summary(float(msg[2]) if len(msg) > 2 else 0.0)])
 
     def _embed(self, conn, rid, model, texts):
         try:

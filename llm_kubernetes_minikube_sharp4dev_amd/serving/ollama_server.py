@@ -170,6 +170,20 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
                 reason = "stop"
             if seq and seq.first_token_at:
                 M.TTFT.observe(seq.first_token_at - seq.arrival)
+            if seq is not None:  # per-request engine accounting (/debug/spans counters)
+                from ..utils import tracing
+
+                cached = seq.num_cached_prefix
+                q = getattr(seq, "steps_queued", None)
+                if q is None and getattr(seq, "step_first", None) is not None:
+                    q = seq.step_first - seq.step_arrival
+                for name, v in (("req_prompt_tokens", len(ids)), ("req_cached_prefix_tokens", cached),
+                                ("req_uncached_prompt_tokens", len(ids) - cached),
+                                ("req_output_tokens", len(seq.output_ids)),
+                                ("req_preemptions", getattr(seq, "num_preemptions", 0)),
+                                ("req_steps_queued", q), ("req_steps_run", getattr(seq, "steps_run", None))):
+                    if v is not None:
+                        tracing.count("server", name, v)
             final = mk_final(text, reason, stats, ids + (seq.output_ids if seq else []))
             yield json.dumps(final, ensure_ascii=False) + ("\n" if stream else "")
 
@@ -356,7 +370,22 @@ def create_app(manager: Optional[ModelManager] = None, cfg=None):
     async def spans(since: float = 0.0):
         from ..utils import tracing
 
-        return JSONResponse(tracing.summary(since))
+        out = tracing.summary(since)
+        pool = getattr(mgr, "pool", None)
+        if pool is not None:  # split server: the engine cores' spans and request counters too
+            for c in pool.clients:
+                try:
+                    core = (await asyncio.wait_for(c.request("spans", since), 10.0))[2]
+                except Exception:  # noqa: BLE001 - a core that does not answer is left out
+                    continue
+                for k, v in core.items():
+                    if k in out and "sum" in v and "sum" in out[k]:
+                        n = out[k]["n"] + v["n"]
+                        tot = out[k]["sum"] + v["sum"]
+                        out[k] = {"n": n, "mean": tot / n, "sum": tot}
+                    else:
+                        out.setdefault(k, v)
+        return JSONResponse(out)
 
     @app.get("/health")
     async def health():

@@ -45,6 +45,19 @@ class _SeqView:
     arrival: float = field(default_factory=time.time)
     first_token_at: Optional[float] = None
     finished: bool = False
+    num_preemptions: int = 0
+    steps_queued: Optional[int] = None
+    steps_run: Optional[int] = None
+    jumped: int = 0
+
+    def set_accounting(self, acc):
+        if isinstance(acc, dict):
+            self.num_cached_prefix = acc.get("cached") or 0
+            self.num_preemptions = acc.get("preempt") or 0
+            self.steps_queued, self.steps_run = acc.get("queued"), acc.get("run")
+            self.jumped = acc.get("jumped") or 0
+        else:  # (older cores: the cached-prefix count alone)
+            self.num_cached_prefix = acc or 0
 
 
 class CoreClient:
@@ -142,13 +155,13 @@ class CoreClient:
                     last = fin and i == len(toks) - 1
                     if last:
                         view.finished, view.finish_reason = True, reason
-                        view.num_cached_prefix = cached or 0
+                        view.set_accounting(cached)
                     yield t, last, view
                 if fin:
                     done = True
                     if err or not toks:
                         view.finished, view.finish_reason, view.error = True, reason, err
-                        view.num_cached_prefix = cached or 0
+                        view.set_accounting(cached)
                         yield -1 if err else (toks[-1] if toks else -1), True, view
                     break
         finally:

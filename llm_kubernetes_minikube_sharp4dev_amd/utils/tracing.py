@@ -89,6 +89,15 @@ def record(component: str, span: str, dur_s: float, **attrs):
     _export(rec)
 
 
+def count(component: str, name: str, value: float, **attrs):
+    """Add a per-request count (tokens, preemptions, engine steps): summarised as n / mean /
+    sum instead of a latency."""
+    rec = {"ts": time.time(), "component": component, "span": name, "value": float(value), **attrs}
+    with _lock:
+        _buffer.append(rec)
+    _export(rec)
+
+
 def recent(n: int = 100) -> list:
     with _lock:
         return list(_buffer)[-n:]
@@ -98,11 +107,17 @@ def summary(since: float = 0.0) -> dict:
     """Per-span count / mean / p50 / p99 over the buffer (spans that ended after ``since``,
     a ``time.time()`` stamp)."""
     by: dict = {}
+    counts: dict = {}
     for r in recent(len(_buffer)):
         if r["ts"] >= since:
-            by.setdefault(f"{r['component']}.{r['span']}", []).append(r["dur_s"])
+            if "value" in r:
+                counts.setdefault(f"{r['component']}.{r['span']}", []).append(r["value"])
+            else:
+                by.setdefault(f"{r['component']}.{r['span']}", []).append(r["dur_s"])
     out = {}
     for k, v in by.items():
         v = sorted(v)
         out[k] = {"n": len(v), "mean_s": sum(v) / len(v), "p50_s": v[len(v) // 2], "p99_s": v[min(len(v) - 1, int(0.99 * len(v)))]}
+    for k, v in counts.items():
+        out[k] = {"n": len(v), "mean": sum(v) / len(v), "sum": sum(v)}
     return out

@@ -118,3 +118,25 @@ def test_http_bench_cpu_plumbing():
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert set(d["config"]["levels"]) == {"1", "2"} and d["value"] > 0
     assert sum(d["config"]["levels"]["2"]["http_status_counts"].values()) == 4
+
+
+def test_tp_sim_estimate_counts_only_exposed_collectives():
+    """--tp-sim's collective estimate: a prefill-sized step's post-attention half runs as a
+    pipeline over row chunks (models/llama.py _post_attn_pipelined), so only the collective time
+    the pipeline exposes is added; decode-sized steps count every tail whole."""
+    import importlib.util
+
+    from llm_kubernetes_minikube_sharp4dev_amd.models.configs import decoder_config
+    from llm_kubernetes_minikube_sharp4dev_amd.models.llama import overlap_chunks
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    floor = b._collective_floor(None, 8192)  # the measured per-call floor (profiles/r4_tp_collectives)
+    lc = decoder_config("llama-3-70b")
+    assert overlap_chunks(64) is None and overlap_chunks(4096) == [(0, 1024), (1024, 2048), (2048, 3072), (3072, 4096)]
+    for up in (True, False):
+        serial = lambda rows: (2 * lc.num_layers + 1) * b._per_call_us(floor, rows, lc.hidden, 8, up)  # noqa: E731
+        assert abs(b._exposed_step_us(floor, 64, lc, 8, up) - serial(64)) < 1e-6
+        exposed = b._exposed_step_us(floor, 4096, lc, 8, up)
+        assert exposed < 0.6 * serial(4096), (up, exposed, serial(4096))

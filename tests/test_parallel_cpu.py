@@ -125,7 +125,14 @@ def _tp_worker(rank, world, port, arch, out_path, sp_min_tokens=None):
     tp = TPGroup(rank, world, dist.group.WORLD)
     m = build_decoder(_ours_cfg(arch), dtype=torch.float32, tp=tp)
     m.load_hf_state_dict(_hf(arch).state_dict())
-    if sp_min_tokens is not None:
+    if sp_min_tokens == "overlap":
+        # chunked row-parallel tails (models/llama.py _post_attn_pipelined) on every step of >= 2 rows:
+        # 3 chunks of any size, so odd and uneven splits occur
+        from llm_kubernetes_minikube_sharp4dev_amd.models import llama
+
+        llama.TP_OVERLAP_MIN_ROWS, llama.TP_OVERLAP_ALIGN, llama.TP_OVERLAP_CHUNKS = 2, 1, 3
+        assert llama.overlap_chunks(7) == [(0, 3), (3, 6), (6, 7)]
+    elif sp_min_tokens is not None:
         m.sp_min_tokens = sp_min_tokens
     kw = dict(block_size=16, max_model_len=512, max_num_seqs=8, num_blocks=96)
     if rank == 0:
@@ -138,10 +145,11 @@ def _tp_worker(rank, world, port, arch, out_path, sp_min_tokens=None):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("arch,sp", [("llama", None), ("opt", None), ("llama", 2)])
+@pytest.mark.parametrize("arch,sp", [("llama", None), ("opt", None), ("llama", 2), ("llama", "overlap")])
 def test_tp2_generation_matches_single_process(arch, sp):
     """TP=2 == one process; ("llama", 2): sequence parallel on every step of >= 2 rows
-    (odd row counts exercise the padding)."""
+    (odd row counts exercise the padding); ("llama", "overlap"): the chunked row-parallel
+    tails of TP prefill (each chunk's all-reduce + norm overlapping the next chunk's GEMM)."""
     from llm_kubernetes_minikube_sharp4dev_amd.engine.llm_engine import LLMEngine
     from llm_kubernetes_minikube_sharp4dev_amd.engine.sampling import SamplingParams
     from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder

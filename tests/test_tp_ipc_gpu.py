@@ -60,9 +60,13 @@ def _run(eng, pipelined: bool):
 KW = dict(block_size=16, max_model_len=512, max_num_seqs=8, num_blocks=128, use_graphs=True)
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, overlap=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LK_TP_COLLECTIVES="ipc")
+    if overlap:  # every rank: chunked row-parallel tails on the comm stream from 16-row steps up
+        from llm_kubernetes_minikube_sharp4dev_amd.models import llama
+
+        llama.TP_OVERLAP_MIN_ROWS, llama.TP_OVERLAP_ALIGN, llama.TP_OVERLAP_CHUNKS = 16, 16, 3
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     from llm_kubernetes_minikube_sharp4dev_amd.models import build_decoder
@@ -78,7 +82,7 @@ def _worker(rank, world, port, out_path):
         eng = make_tp_engine(m, tp, None, engine_kw={"eos_ids": set()}, **KW)
         tp_capture_all(eng, max_batch=16, variants=(True,))
         out = {"sync": _run(eng, False), "pipelined": _run(eng, True), "table": tp.xgmi.timings,
-               "routes": dict(tp.xgmi.table)}
+               "routes": dict(tp.xgmi.table), "overlap_tails": m.overlap_tails}
         shutdown_tp(eng)
         torch.cuda.synchronize()
         out["err"] = tp.xgmi.error()
@@ -118,14 +122,17 @@ def _same_or_near_tie(hf, got, ref):
         assert gap < 0.05 * want.abs().max().item() + 0.05, (p[:3], k, g[k], r[k], gap)
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_tp_engine_ipc_matches_tp1(reference, world):
+@pytest.mark.parametrize("world,overlap", [(2, False), (4, False), (8, False), (2, True), (4, True), (8, True)])
+def test_tp_engine_ipc_matches_tp1(reference, world, overlap):
+    """overlap: the prefill steps' row-parallel tails in 3 row chunks, each chunk's IPC all-reduce
+    + norm on the communication stream beside the next chunk's GEMM (models/llama.py _post_attn_pipelined)."""
     hf, ref = reference
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "out.pt")
-        mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), out, overlap), nprocs=world, join=True)
         got = torch.load(out, weights_only=True)
     assert got["err"] == 0
+    assert (got["overlap_tails"] > 0) == overlap, got["overlap_tails"]
     assert got["table"] and set(got["routes"].values()) <= {"ipc1", "ipc2"}, got["routes"]
     print(f"TP={world} measured collective routes: {got['routes']}")
     _same_or_near_tie(hf, got["sync"], ref)
