@@ -25,6 +25,32 @@ constexpr int kMaxSplit = 2048;  // max keys per workgroup (LDS block-table slic
 #endif
 typedef short4_t __attribute__((address_space(3))) * lds_s4_ptr;
 
+// The flash-decoding merge of one output element (seq b, query head qh, dim d) over nsplit
+// split partials (+ the cascade prefix partial): the same arithmetic as decode_reduce_kernel.
+// Partials are read past L1 / L2 (system-scope loads): other workgroups wrote them through.
+template <int D>
+LK_DEVICE void merge_splits(int b, int qh, int d, int Hq, int max_splits, int nsplit, const float* part_o,
+                            const float* part_ml, const float* pp_o, const float* pp_ml, bf16_t* out, long os) {
+  auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+  const long base = ((long)b * Hq + qh) * max_splits;
+  const long pb = (long)b * Hq + qh;
+  float M = pp_o ? pp_ml[pb * 2] : -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ld(part_ml + (base + s) * 2));
+  if (M == -INFINITY) M = 0.f;  // no keys at all (padding row)
+  float den = 0.f, num = 0.f;
+  if (pp_o) {
+    const float f = exp2f(pp_ml[pb * 2] - M);
+    den = f * pp_ml[pb * 2 + 1];
+    num = f * pp_o[pb * D + d];
+  }
+  for (int s = 0; s < nsplit; ++s) {
+    const float f = exp2f(ld(part_ml + (base + s) * 2) - M);
+    den += f * ld(part_ml + (base + s) * 2 + 1);
+    num += f * ld(part_o + (base + s) * D + d);
+  }
+  out[(long)b * os + (long)qh * D + d] = f2bf(den > 0.f ? num / den : 0.f);
+}
+
 // v3 (streaming): workgroup = (split, kv_head, seq), 4 waves; each wave walks 32-key
 // chunks (w, w+4, ...) of the split with its own online softmax, so there is no
 // workgroup barrier inside the key loop and the next chunk's K/V loads are always
@@ -42,7 +68,8 @@ __global__ __launch_bounds__(256, LK_DECODE_WG_PER_CU) void paged_decode_kernel(
     const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ctx_lens, bf16_t* __restrict__ out, long os,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int BS, int max_splits,
-    int split, float scale_log2, const int* __restrict__ k_start, int has_prefix) {
+    int split, float scale_log2, const int* __restrict__ k_start, int has_prefix,
+    const float* __restrict__ pp_o, const float* __restrict__ pp_ml, int* __restrict__ tickets) {
   constexpr int KK = D / 32;     // QK k-steps (16x16x32)
   constexpr int ND = D / 16;     // PV output tiles of 16 d
   constexpr int CPR = D / 8;     // 16-B chunks per V row
@@ -57,10 +84,16 @@ __global__ __launch_bounds__(256, LK_DECODE_WG_PER_CU) void paged_decode_kernel(
   // kernel once for all rows (its partial is merged by decode_reduce_kernel)
   const int k0 = k_start ? k_start[0] : 0;
   const int k_begin = k0 + s * split;
-  if (k_begin >= ctx) return;  // uniform for the whole workgroup
+  const int Hq = Hkv * G;
+  if (k_begin >= ctx) {  // uniform for the whole workgroup
+    // fused reduce: split 0 of a row without keys past the prefix writes its output itself
+    if (tickets != nullptr && s == 0)
+      for (int i = threadIdx.x; i < G * D; i += 256)
+        merge_splits<D>(b, kvh * G + i / D, i % D, Hq, max_splits, 0, part_o, part_ml, pp_o, pp_ml, out, os);
+    return;
+  }
   const int nkeys = min(split, ctx - k_begin);
   const int nsplit = min((ctx - k0 + split - 1) / split, max_splits);
-  const int Hq = Hkv * G;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r16 = lane & 15, h4 = lane >> 4;
 
@@ -221,6 +254,14 @@ __global__ __launch_bounds__(256, LK_DECODE_WG_PER_CU) void paged_decode_kernel(
     const int qh = kvh * G + g;
     if (nsplit == 1 && !has_prefix) {
       out[(long)b * os + (long)qh * D + d] = f2bf(O / L);
+    } else if (tickets != nullptr) {
+      // written through to memory: the workgroup that merges may sit on another XCD (own L2)
+      const long pi = ((long)b * Hq + qh) * max_splits + s;
+      __hip_atomic_store(part_o + pi * D + d, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (d == 0) {
+        __hip_atomic_store(part_ml + pi * 2, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // log2 domain
+        __hip_atomic_store(part_ml + pi * 2 + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     } else {
       const long pi = ((long)b * Hq + qh) * max_splits + s;
       part_o[pi * D + d] = O;
@@ -230,6 +271,24 @@ __global__ __launch_bounds__(256, LK_DECODE_WG_PER_CU) void paged_decode_kernel(
       }
     }
   }
+  if (tickets == nullptr || (nsplit == 1 && !has_prefix)) return;
+  // Fused reduce (flash-decoding merge) by the LAST split workgroup of this (seq, kv head) to
+  // finish: every split's partial stores are acknowledged before its ticket is taken, and the
+  // last one reads them past L1 / L2 -- no decode_reduce launch (a ~5 us kernel per layer).
+  // The ticket is reset by its last taker, ready for the next launch.
+  __builtin_amdgcn_s_waitcnt(0);  // this thread's partial stores acknowledged
+  __syncthreads();
+  __shared__ int is_last;
+  if (threadIdx.x == 0) {
+    int* tk = tickets + (long)b * Hkv + kvh;
+    const int old = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    is_last = old == nsplit - 1;
+    if (is_last) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  if (!is_last) return;
+  for (int i = threadIdx.x; i < G * D; i += 256)
+    merge_splits<D>(b, kvh * G + i / D, i % D, Hq, max_splits, nsplit, part_o, part_ml, pp_o, pp_ml, out, os);
 }
 
 // combine split partials (+ the shared-prefix partial of a cascade step): grid (Hq, B), D threads
@@ -287,7 +346,7 @@ int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc
                     const int* block_tables, int bt_stride, const int* ctx_lens, bf16_t* out,
                     long os, float* part_o, float* part_ml, int B, int Hq, int Hkv, int D, int BS,
                     int max_splits, int split, float scale, const int* k_start, const float* pp_o,
-                    const float* pp_ml, hipStream_t st) {
+                    const float* pp_ml, hipStream_t st, int* tickets) {
   if (B == 0) return 0;
   if (Hq % Hkv || BS % 16 || split % 32 || split > kMaxSplit || split % BS) return -1;
   const int G = Hq / Hkv;
@@ -297,7 +356,7 @@ int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc
   paged_decode_kernel<DD, GG><<<grid, 256, 0, st>>>(q, qs, kc, vc, block_tables, bt_stride,   \
                                                     ctx_lens, out, os, part_o, part_ml, Hkv, \
                                                     BS, max_splits, split, scale_log2, k_start, \
-                                                    pp_o != nullptr)
+                                                    pp_o != nullptr, pp_o, pp_ml, tickets)
 #define BY_G(DD)                          \
   switch (G) {                            \
     case 1: LAUNCH(DD, 1); break;         \
@@ -311,7 +370,8 @@ int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc
   else return -3;
 #undef BY_G
 #undef LAUNCH
-  if (max_splits > 1 || pp_o) {
+  LK_CHECK_LAUNCH();
+  if ((max_splits > 1 || pp_o) && tickets == nullptr) {  // (fused: the last split merges)
     if (D == 128)
       decode_reduce_kernel<128><<<dim3(Hq, B), 128, 0, st>>>(part_o, part_ml, ctx_lens, out, os, Hq,
                                                              max_splits, split, k_start, pp_o, pp_ml);
@@ -319,5 +379,6 @@ int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc
       decode_reduce_kernel<64><<<dim3(Hq, B), 64, 0, st>>>(part_o, part_ml, ctx_lens, out, os, Hq,
                                                            max_splits, split, k_start, pp_o, pp_ml);
   }
+  LK_CHECK_LAUNCH();
   return 0;
 }

@@ -461,7 +461,7 @@ at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at
                         int64_t split, double scale, const c10::optional<at::Tensor>& part_o,
                         const c10::optional<at::Tensor>& part_ml, const c10::optional<at::Tensor>& out_,
                         const c10::optional<at::Tensor>& k_start, const c10::optional<at::Tensor>& pp_o,
-                        const c10::optional<at::Tensor>& pp_ml) {
+                        const c10::optional<at::Tensor>& pp_ml, const c10::optional<at::Tensor>& tickets) {
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
   CHECK_I32(block_tables); CHECK_I32(ctx_lens); CHECK_CONTIG(ctx_lens);
   TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == q.size(2), "q must be [B, Hq, D] (row-strided)");
@@ -491,12 +491,16 @@ at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at
     TORCH_CHECK(po.numel() >= (long)B * Hq * max_splits * D && pm.numel() >= (long)B * Hq * max_splits * 2, "partials too small");
     CHECK_F32(po); CHECK_F32(pm);
   }
+  if (tickets) {  // fused split merge: one zero-initialised int32 counter per (seq, kv head)
+    CHECK_CUDA(*tickets); CHECK_I32(*tickets); CHECK_CONTIG(*tickets);
+    TORCH_CHECK(tickets->numel() >= (long)B * Hkv, "tickets: one counter per (sequence, kv head)");
+  }
   int rc = lk_paged_decode(bp(q), q.stride(0), bp(k_cache), bp(v_cache), ip(block_tables), block_tables.stride(0),
                            ip(ctx_lens), bp(out), out.stride(0), parts ? po.data_ptr<float>() : nullptr,
                            parts ? pm.data_ptr<float>() : nullptr, B, Hq, Hkv, D, BS, (int)max_splits,
                            (int)split, (float)scale, cascade ? ip(*k_start) : nullptr,
                            cascade ? pp_o->data_ptr<float>() : nullptr, cascade ? pp_ml->data_ptr<float>() : nullptr,
-                           cur_stream());
+                           cur_stream(), tickets ? tickets->data_ptr<int>() : nullptr);
   CHECK_RC(rc, "paged_decode");
   return out;
 }
@@ -941,7 +945,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("kv_write", &kv_write);
   m.def("decode_splits", &decode_splits);
   m.def("decode_split_size", &decode_split_size);
-  m.def("paged_decode", &paged_decode, "", py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("max_splits"), py::arg("split"), py::arg("scale"), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("out") = py::none(), py::arg("k_start") = py::none(), py::arg("pp_o") = py::none(), py::arg("pp_ml") = py::none());
+  m.def("paged_decode", &paged_decode, "", py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("max_splits"), py::arg("split"), py::arg("scale"), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("out") = py::none(), py::arg("k_start") = py::none(), py::arg("pp_o") = py::none(), py::arg("pp_ml") = py::none(), py::arg("tickets") = py::none());
   m.def("prefill_rows_per_tile", &prefill_rows_per_tile);
   m.def("ws_set_variant", [](int64_t M, int64_t N, int64_t K, bool swiglu, int64_t v) {
     CHECK_RC(lk_wsgemm_set_variant((int)M, (int)N, (int)K, swiglu ? 1 : 0, (int)v), "ws_set_variant");

@@ -137,7 +137,7 @@ int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc
                     const int* block_tables, int bt_stride, const int* ctx_lens, bf16_t* out,
                     long os, float* part_o, float* part_ml, int B, int Hq, int Hkv, int D, int BS,
                     int max_splits, int split, float scale, const int* k_start, const float* pp_o,
-                    const float* pp_ml, hipStream_t st);
+                    const float* pp_ml, hipStream_t st, int* tickets = nullptr);
 
 // attn_prefill.hip
 int lk_prefill_rows_per_tile(int G, int D);

@@ -113,6 +113,25 @@ def decode_splits(max_context: int, split: int) -> int:
     return max(1, (int(max_context) + split - 1) // split)
 
 
+# Split decode: the last split workgroup of each (sequence, kv head) merges the partials
+# itself (csrc/attn_decode.hip merge_splits) instead of a decode_reduce launch after the kernel
+# (~5 us per layer and step, on the batch-1 critical path; launched even when no row had more
+# than one split).  Needs one zero-initialised int32 ticket per (sequence, kv head), reset by its
+# last taker: a per-device buffer made before any graph capture.  LK_DECODE_FUSED_REDUCE=0: the
+# separate reduce kernel.
+DECODE_FUSED_REDUCE = os.environ.get("LK_DECODE_FUSED_REDUCE", "1") != "0"
+_DECODE_TICKETS: dict = {}
+
+
+def decode_tickets(device, n: int):
+    device = torch.device(device)
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    t = _DECODE_TICKETS.get(key)
+    if t is None or t.numel() < n:
+        t = _DECODE_TICKETS[key] = torch.zeros(max(n, 1 << 16), dtype=torch.int32, device=device)
+    return t
+
+
 def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_splits: Optional[int] = None,
                  part_o=None, part_ml=None, out=None, split: Optional[int] = None, k_start=None, prefix=None):
     """q [B, Hq, D] -> [B, Hq, D].  ``split`` keys per workgroup (default from
@@ -130,8 +149,9 @@ def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_
         if max_splits is None:
             max_splits = decode_splits(block_tables.shape[1] * BS, split)
         pp_o, pp_ml = prefix if prefix is not None else (None, None)
+        tickets = decode_tickets(q.device, q.shape[0] * k_cache.shape[1]) if DECODE_FUSED_REDUCE else None
         return lib().paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, max_splits, split, scale,
-                                  part_o, part_ml, out, k_start, pp_o, pp_ml)
+                                  part_o, part_ml, out, k_start, pp_o, pp_ml, tickets)
     y = ref.paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
     if out is not None:
         out.copy_(y)

@@ -37,20 +37,22 @@ def main(path):
     by = collections.defaultdict(lambda: [0, 0, 0])
     queues = collections.Counter(q for _, _, _, q, _ in ars)
     for s, e, n, q, g in ars:
-        short = n.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
-        k = (short, g)
+        short = n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+        k = (short, g, q)
         by[k][0] += 1
         by[k][1] += e - s
         by[k][2] += covered(s, e, q)
     print(f"# TP collective / GEMM overlap: {path}\n")
     print(f"{len(ars)} xGMI collective kernels on queues {dict(queues)}; {len(gemms)} GEMM kernels\n")
-    print("| collective kernel | grid | calls | total us | us beside a GEMM (other queue) | overlapped |")
-    print("|---|---|---|---|---|---|")
+    gq = collections.Counter(q for _, _, q in gemms)
+    print(f"GEMM kernels by queue: {dict(gq)}\n")
+    print("| collective kernel | grid | queue | calls | total us | us beside a GEMM (other queue) | overlapped |")
+    print("|---|---|---|---|---|---|---|")
     tot = ov = 0
-    for (n, g), (c, d, o) in sorted(by.items(), key=lambda kv: -kv[1][1]):
+    for (n, g, q), (c, d, o) in sorted(by.items(), key=lambda kv: -kv[1][1]):
         tot += d
         ov += o
-        print(f"| `{n}` | {g} | {c} | {d / 1e3:.1f} | {o / 1e3:.1f} | {100.0 * o / max(1, d):.1f} % |")
+        print(f"| `{n}` | {g} | {q} | {c} | {d / 1e3:.1f} | {o / 1e3:.1f} | {100.0 * o / max(1, d):.1f} % |")
     print(f"\nAll collectives: {tot / 1e3:.1f} us, {ov / 1e3:.1f} us of it beside a GEMM ({100.0 * ov / max(1, tot):.1f} %)")
 
 

@@ -133,10 +133,39 @@ def test_paged_decode(hip, G, D):
     cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
     scale = 1 / math.sqrt(D)
     y_ref = ref.paged_decode(q, kc, vc, bt, cl, scale)
+    tickets = torch.zeros(B * Hkv, dtype=torch.int32, device=DEV)
     for split in (128, 256, 2048):  # many partials / few partials / single pass
         max_splits = ops.decode_splits(bt.shape[1] * BS, split)
         y = hip.paged_decode(q, kc, vc, bt, cl, max_splits, split, scale, None, None, None)
         _close(y, y_ref, 0.02, 0.0, f"paged decode split={split}")
+        # fused merge (the last split workgroup of each (seq, kv head) reduces): same output, and
+        # every ticket back at 0 for the next launch
+        for _ in range(2):
+            yf = hip.paged_decode(q, kc, vc, bt, cl, max_splits, split, scale, None, None, None, None, None, None,
+                                  tickets)
+            _close(yf, y_ref, 0.02, 0.0, f"paged decode fused merge split={split}")
+            assert int(tickets.abs().sum()) == 0
+
+
+def test_paged_decode_fused_merge_empty_rows(hip):
+    """Rows without keys (graph-bucket padding, ctx 0) get zeros from split 0 when no reduce
+    kernel runs, exactly as the separate reduce kernel writes them."""
+    torch.manual_seed(16)
+    Hkv, BS, G, D = 8, 16, 4, 128
+    ctx = [0, 700, 0, 1, 3000]
+    B = len(ctx)
+    kc, vc, bt = _paged_setup(B, [max(c, 1) for c in ctx], Hkv, D, BS, seed=17)
+    q = torch.randn(B, Hkv * G, D, device=DEV, dtype=torch.bfloat16)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    tickets = torch.zeros(B * Hkv, dtype=torch.int32, device=DEV)
+    for split in (128, 512):
+        ms = ops.decode_splits(bt.shape[1] * BS, split)
+        want = hip.paged_decode(q, kc, vc, bt, cl, ms, split, 0.088, None, None, torch.full_like(q, 7.0))
+        got = hip.paged_decode(q, kc, vc, bt, cl, ms, split, 0.088, None, None, torch.full_like(q, 7.0), None, None,
+                               None, tickets)
+        assert bool((got[0] == 0).all()) and bool((got[2] == 0).all())
+        _close(got, want, 1e-3, 0.0, f"fused vs reduce kernel split={split}")
+        assert int(tickets.abs().sum()) == 0
 
 
 @pytest.mark.parametrize("G", [1, 4, 8])
