@@ -204,13 +204,23 @@ WsSplit ws_split(const at::Tensor& x, const at::Tensor& w, int64_t bn, int64_t s
 
 // out = RMSNorm(x W^T + residual) * norm_w, residual += x W^T (bf16, in place)
 at::Tensor ws_linear_rmsnorm(const at::Tensor& x, const at::Tensor& w, at::Tensor& residual,
-                             const at::Tensor& norm_w, double eps, int64_t bn, int64_t splits) {
+                             const at::Tensor& norm_w, double eps, int64_t bn, int64_t splits,
+                             const c10::optional<at::Tensor>& tickets) {
   const WsSplit p = ws_split(x, w, bn, splits, "ws_linear_rmsnorm");
   CHECK_CUDA(residual); CHECK_BF16(residual); CHECK_LASTDIM(residual); check_rows16(residual, "residual");
   TORCH_CHECK(residual.dim() == 2 && residual.size(0) == p.M && residual.size(1) == p.N, "residual shape");
   CHECK_BF16(norm_w); TORCH_CHECK(norm_w.numel() == p.N && norm_w.is_contiguous(), "norm weight shape");
   at::Tensor part = at::empty({(long)p.S * p.M * p.N}, x.options().dtype(at::kFloat));
   at::Tensor out = at::empty({p.M, p.N}, x.options());
+  if (tickets && p.M <= 4 && (p.S == 2 || p.S == 4 || p.S == 8)) {  // reduction fused into the GEMM
+    CHECK_CUDA(*tickets); CHECK_I32(*tickets); CHECK_CONTIG(*tickets);
+    TORCH_CHECK(tickets->numel() >= 1, "tickets");
+    int rc = lk_ws_rmsnorm_fused(bp(x), x.stride(0), bp(w), p.M, p.N, p.K, p.BN, p.S, part.data_ptr<float>(),
+                                 tickets->data_ptr<int>(), bp(out), out.stride(0), bp(residual), residual.stride(0),
+                                 bp(norm_w), (float)eps, cur_stream());
+    CHECK_RC(rc, "ws_linear_rmsnorm (fused)");
+    return out;
+  }
   int rc = lk_wsgemm_part(bp(x), x.stride(0), bp(w), p.M, p.N, p.K, p.BN, p.S, part.data_ptr<float>(), cur_stream());
   CHECK_RC(rc, "ws_linear_rmsnorm (gemm)");
   rc = lk_splitk_rmsnorm(bp(out), bp(residual), part.data_ptr<float>(), p.S, bp(norm_w), p.M, p.N, (float)eps,
@@ -224,7 +234,7 @@ at::Tensor ws_linear_rope_kv(const at::Tensor& x, const at::Tensor& w, const at:
                              const at::Tensor& cos_sin, int64_t Hq, int64_t Hkv, int64_t D,
                              const c10::optional<at::Tensor>& k_cache, const c10::optional<at::Tensor>& v_cache,
                              const c10::optional<at::Tensor>& slots, bool neox, bool write_k_inplace, int64_t bn,
-                             int64_t splits) {
+                             int64_t splits, const c10::optional<at::Tensor>& tickets) {
   const WsSplit p = ws_split(x, w, bn, splits, "ws_linear_rope_kv");
   TORCH_CHECK(p.N == (Hq + 2 * Hkv) * D, "w must be the fused [(Hq + 2 Hkv) * D, K] projection");
   CHECK_I32(positions); CHECK_F32(cos_sin); CHECK_CONTIG(cos_sin); CHECK_CONTIG(positions);
@@ -241,6 +251,16 @@ at::Tensor ws_linear_rope_kv(const at::Tensor& x, const at::Tensor& w, const at:
   }
   at::Tensor part = at::empty({(long)p.S * p.M * p.N}, x.options().dtype(at::kFloat));
   at::Tensor qkv = at::empty({p.M, p.N}, x.options());
+  if (tickets && p.BN == D && D == 128 && (p.S == 2 || p.S == 4 || p.S == 8)) {  // reduction fused into the GEMM
+    CHECK_CUDA(*tickets); CHECK_I32(*tickets); CHECK_CONTIG(*tickets);
+    TORCH_CHECK(tickets->numel() >= Hq + 2 * Hkv, "tickets: one per head");
+    int rc = lk_ws_rope_kv_fused(bp(x), x.stride(0), bp(w), p.M, p.K, p.BN, p.S, part.data_ptr<float>(),
+                                 tickets->data_ptr<int>(), bp(qkv), qkv.stride(0), ip(positions),
+                                 cos_sin.data_ptr<float>(), (int)Hq, (int)Hkv, (int)D, bpo(k_cache), bpo(v_cache),
+                                 ipo(slots), BS, neox ? 1 : 0, write_k_inplace ? 1 : 0, cur_stream());
+    CHECK_RC(rc, "ws_linear_rope_kv (fused)");
+    return qkv;
+  }
   int rc = lk_wsgemm_part(bp(x), x.stride(0), bp(w), p.M, p.N, p.K, p.BN, p.S, part.data_ptr<float>(), cur_stream());
   CHECK_RC(rc, "ws_linear_rope_kv (gemm)");
   rc = lk_splitk_rope_kv(part.data_ptr<float>(), p.S, bp(qkv), qkv.stride(0), ip(positions), cos_sin.data_ptr<float>(),
@@ -937,11 +957,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_kv_", &rope_kv_);
   m.def("ws_set_rot", [](int64_t r) { lk_wsgemm_set_rot((int)r); });
   m.def("ws_linear_rmsnorm", &ws_linear_rmsnorm, "", py::arg("x"), py::arg("w"), py::arg("residual"),
-        py::arg("norm_w"), py::arg("eps"), py::arg("bn") = 0, py::arg("splits") = 0);
+        py::arg("norm_w"), py::arg("eps"), py::arg("bn") = 0, py::arg("splits") = 0, py::arg("tickets") = py::none());
   m.def("ws_linear_rope_kv", &ws_linear_rope_kv, "", py::arg("x"), py::arg("w"), py::arg("positions"),
         py::arg("cos_sin"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("k_cache"), py::arg("v_cache"),
         py::arg("slots"), py::arg("neox") = true, py::arg("write_k_inplace") = false, py::arg("bn") = 0,
-        py::arg("splits") = 0);
+        py::arg("splits") = 0, py::arg("tickets") = py::none());
   m.def("kv_write", &kv_write);
   m.def("decode_splits", &decode_splits);
   m.def("decode_split_size", &decode_split_size);

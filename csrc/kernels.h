@@ -43,6 +43,15 @@ int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, i
 int lk_wsgemm_set_variant(int M, int N, int K, int swiglu, int variant);  // -1 = back to the default
 int lk_wsgemm_part(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, float* part,
                    hipStream_t st);
+// the same split-K GEMM with the reduction fused into its last workgroup(s): RoPE + paged-KV
+// write per head (BN == D == 128), or residual + RMSNorm for M <= 4 (skinny_gemm.hip WsTail)
+int lk_ws_rope_kv_fused(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int BN, int S, float* part,
+                        int* tickets, bf16_t* qkv, long qs, const int* positions, const float* cos_sin, int Hq,
+                        int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,
+                        int write_k_inplace, hipStream_t st);
+int lk_ws_rmsnorm_fused(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, float* part,
+                        int* tickets, bf16_t* out, long os, bf16_t* residual, long rs, const bf16_t* norm_w, float eps,
+                        hipStream_t st);
 
 void lk_wsgemm_set_rot(int rot_mul);  // K-step rotation per column tile (0 = off, -1 = policy)
 

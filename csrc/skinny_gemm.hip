@@ -40,6 +40,183 @@ constexpr int kSkW = 4;  // waves per block
 LK_DEVICE float silu_f(float x) { return x / (1.f + __expf(-x)); }
 LK_DEVICE float rbf(float x) { return bf2f(f2bf(x)); }
 
+constexpr int kSysCoherent = 1 | 16;  // buffer cache policy sc0 | sc1: past L1 and L2
+
+// Fused split-K tail of the weight-streaming GEMM (kind != 0).  Every split workgroup writes its
+// f32 partial through to memory and takes a ticket; the LAST one to finish reduces the slabs
+// itself, so no reduce kernel is launched after the GEMM (at decode sizes a reduce launch is a
+// ~5 us step of the critical path per projection):
+//   kind 1: RoPE + paged-KV write, one ticket per column tile = one head (BN == D): the qkv rows
+//           exactly as lk_splitk_rope_kv leaves them (q rotated, k rotated in the cache and in
+//           the row only with write_k_inplace, v copied);
+//   kind 2: residual add + RMSNorm, one ticket for the whole grid (few rows: the last workgroup
+//           normalises every row), exactly as lk_splitk_rmsnorm.
+// Tickets are zero-initialised int32 counters reset by their last taker.
+struct WsTail {
+  int kind = 0;
+  int* tickets = nullptr;
+  bf16_t* out = nullptr;  // 1: qkv rows; 2: normed rows
+  long os = 0;
+  const int* positions = nullptr;
+  const float* cos_sin = nullptr;
+  int Hq = 0, Hkv = 0, D = 0;
+  bf16_t* kc = nullptr;
+  bf16_t* vc = nullptr;
+  const int* slots = nullptr;
+  int BS = 1, neox = 0, write_k_inplace = 0;
+  bf16_t* residual = nullptr;
+  long rs = 0;
+  const bf16_t* norm_w = nullptr;
+  float eps = 0.f;
+};
+
+// 8 consecutive columns of one row: the S slabs summed in slab order, rounded to bf16 (the values
+// the unfused reduce stores); partials read past L1 / L2 (other workgroups wrote them through)
+LK_DEVICE void tail_ld8(__amdgpu_buffer_rsrc_t prs, int S, long slab, long off, float* f) {
+  floatx4 a = floatx4{0.f, 0.f, 0.f, 0.f}, b = a;
+  for (int q0 = 0; q0 < S; q0 += 4) {  // 4 slabs in flight at a time (registers: the tail shares the kernel's)
+    floatx4 pa[4], pb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q0 + q < S) {
+        const unsigned o = (unsigned)((off + (q0 + q) * slab) * 4);
+        pa[q] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(prs, o, 0, kSysCoherent));
+        pb[q] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(prs, o + 16, 0, kSysCoherent));
+      }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q0 + q < S) {
+        a += pa[q];
+        b += pb[q];
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[j] = bf2f(f2bf(a[j]));
+    f[j + 4] = bf2f(f2bf(b[j]));
+  }
+}
+
+// kind 1: head = column tile t of the fused [(Hq + 2 Hkv) * D] projection, all M rows
+LK_DEVICE void tail_rope_kv(const WsTail& tl, __amdgpu_buffer_rsrc_t prs, int S, int M, long ld, int head) {
+  const int D = tl.D, half = D >> 1;
+  const long slab = (long)M * ld;
+  const bool rot = head < tl.Hq + tl.Hkv;
+  const int ipr = rot ? (tl.neox ? (D >> 4) : (D >> 3)) : (D >> 3);
+  const bool is_k = head >= tl.Hq && rot;
+  const bool store_src = !is_k || tl.write_k_inplace;
+  for (int it = threadIdx.x; it < M * ipr; it += blockDim.x) {
+    const int row = it / ipr, v = it - row * ipr;
+    bf16_t* hp = tl.out + (long)row * tl.os + (long)head * D;
+    const long pbase = (long)row * ld + (long)head * D;
+    const int slot = tl.slots ? tl.slots[row] : -1;
+    const long blk = slot >= 0 ? slot / tl.BS : 0;
+    const int off = slot >= 0 ? slot % tl.BS : 0;
+    if (!rot) {  // V: copy into the row and the cache
+      const int c = v * 8, h = head - tl.Hq - tl.Hkv;
+      float f[8];
+      tail_ld8(prs, S, slab, pbase + c, f);
+      store8(hp + c, f);
+      if (tl.vc && slot >= 0) store8(tl.vc + ((blk * tl.Hkv + h) * tl.BS + off) * D + c, f);
+      continue;
+    }
+    const float* cs = tl.cos_sin + (long)tl.positions[row] * D;  // [cos(D/2) | sin(D/2)]
+    bf16_t* kdst = (is_k && tl.kc && slot >= 0) ? tl.kc + ((blk * tl.Hkv + (head - tl.Hq)) * tl.BS + off) * D : nullptr;
+    if (tl.neox) {
+      const int i0 = v * 8;
+      float x1[8], x2[8], y1[8], y2[8];
+      tail_ld8(prs, S, slab, pbase + i0, x1);
+      tail_ld8(prs, S, slab, pbase + half + i0, x2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float c = cs[i0 + j], sn = cs[half + i0 + j];
+        y1[j] = x1[j] * c - x2[j] * sn;
+        y2[j] = x2[j] * c + x1[j] * sn;
+      }
+      store8(hp + i0, store_src ? y1 : x1);
+      store8(hp + half + i0, store_src ? y2 : x2);
+      if (kdst) {
+        store8(kdst + i0, y1);
+        store8(kdst + half + i0, y2);
+      }
+    } else {
+      const int e0 = v * 8;  // elements e0..e0+7 = pairs e0/2 .. e0/2+3
+      float x[8], y[8];
+      tail_ld8(prs, S, slab, pbase + e0, x);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const float c = cs[(e0 >> 1) + p], sn = cs[half + (e0 >> 1) + p];
+        y[2 * p] = x[2 * p] * c - x[2 * p + 1] * sn;
+        y[2 * p + 1] = x[2 * p + 1] * c + x[2 * p] * sn;
+      }
+      store8(hp + e0, store_src ? y : x);
+      if (kdst) store8(kdst + e0, y);
+    }
+  }
+}
+
+// kind 2: rows 0..M-1 of N = ld columns: residual += bf16(sum of slabs); out = RMSNorm(residual) * w
+LK_DEVICE void tail_rmsnorm(const WsTail& tl, __amdgpu_buffer_rsrc_t prs, int S, int M, long ld, float* red) {
+  const int nvec = (int)(ld >> 3);
+  const long slab = (long)M * ld;
+  const int nw = blockDim.x >> 6, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int row = 0; row < M; ++row) {
+    float ss = 0.f;
+    for (int c = threadIdx.x; c < nvec; c += blockDim.x) {
+      float v[8], r[8];
+      tail_ld8(prs, S, slab, (long)row * ld + c * 8, v);
+      bf16_t* rr = tl.residual + (long)row * tl.rs + c * 8;
+      load8(rr, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[j] = bf2f(f2bf(v[j] + r[j]));  // the new residual stream: the bf16-rounded sum
+        ss += v[j] * v[j];
+      }
+      store8(rr, v);
+    }
+    ss = wave_sum(ss);
+    __syncthreads();  // (the previous row's reads of red are done)
+    if (lane == 0) red[wv] = ss;
+    __syncthreads();
+    float tot = 0.f;
+    for (int i = 0; i < nw; ++i) tot += red[i];
+    const float inv = rsqrtf(tot / (float)ld + tl.eps);
+    for (int c = threadIdx.x; c < nvec; c += blockDim.x) {
+      float v[8], g[8], y[8];
+      load8(tl.residual + (long)row * tl.rs + c * 8, v);  // (this thread's own stores above)
+      load8(tl.norm_w + c * 8, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = v[j] * inv * g[j];
+      store8(tl.out + (long)row * tl.os + c * 8, y);
+    }
+  }
+}
+
+// after the epilogue, by ALL threads of the workgroup (uniform control flow: it has barriers).
+// lds: the kernel's dynamic LDS, dead once the K loop is done (no static LDS here: the ring
+// already fills the 160 KB)
+__attribute__((noinline)) __device__ void ws_tail(const WsTail& tl, float* part, int M, long ld, int S, int t, int n_tiles, unsigned char* lds) {
+  int* is_last = reinterpret_cast<int*>(lds);
+  float* red = reinterpret_cast<float*>(lds + 64);
+  __builtin_amdgcn_s_waitcnt(0);  // this thread's write-through partial stores acknowledged
+  __syncthreads();                // (and every wave is done with the LDS ring)
+  if (threadIdx.x == 0) {
+    int* tk = tl.tickets + (tl.kind == 1 ? t : 0);
+    const int need = tl.kind == 1 ? S : S * n_tiles;
+    const int old = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const int last = old == need - 1;
+    if (last) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    *is_last = last;
+  }
+  __syncthreads();
+  if (!*is_last) return;
+  const long bytes = (long)S * M * ld * 4;
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)part, (short)0, (int)min(bytes, 0x7FFFFFF0L), 0x00020000);
+  if (tl.kind == 1) tail_rope_kv(tl, prs, S, M, ld, t);
+  else tail_rmsnorm(tl, prs, S, M, ld, red);
+}
+
 template <int MT, int NTW, bool SWIGLU>
 __global__ __launch_bounds__(256) void skinny_gemm_kernel(
     const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W, int M, int K, int ks,
@@ -259,12 +436,12 @@ LK_DEVICE void wait_ahead(int ahead) {  // vmcnt(ahead * L), ahead in [0, NS-2]
   }
 }
 
-template <int MT, int BN, bool SWIGLU>
+template <int MT, int BN, bool SWIGLU, bool TAIL>
 __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict__ X, long ldx,
                                                         const bf16_t* __restrict__ W, int M, int K, int ks,
                                                         int n_tiles, int swiglu_I, bf16_t* __restrict__ out,
                                                         long ldo, float* __restrict__ part, long part_ld,
-                                                        long n_rows, int rot_mul) {
+                                                        long n_rows, int rot_mul, WsTail tl) {
   // n_rows: valid W rows (the last column tile may be partial: kNN over a corpus of
   // any size); loads clamp to the last row, stores are masked
   constexpr int ROWS = 16 * MT;          // padded M
@@ -375,6 +552,9 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
   // tile columns 16n + 4g .. +3
   const bool split = part != nullptr;
   const bool part_vec = split && part_ld % 4 == 0 && reinterpret_cast<uintptr_t>(part) % 16 == 0;
+  // (fused tail: the partial slabs through a buffer resource, written past L1 / L2)
+  const __amdgpu_buffer_rsrc_t tprs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)part, (short)0, (int)min((long)(K / ks) * M * part_ld * 4, 0x7FFFFFF0L), 0x00020000);
   const bool out_vec = ldo % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 8 == 0;
 #pragma unroll
   for (int m = 0; m < MTW; ++m) {
@@ -403,7 +583,10 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
         // 4 consecutive tile rows stay inside one half of a SwiGLU tile: contiguous W rows
         const long col = wrow(16 * n + 4 * g);
         float* dst = part + (long)s * M * part_ld + (long)row * part_ld + col;
-        if (part_vec && col + 3 < n_rows) {
+        if (TAIL) {  // fused tail: through to memory (full 16-B tiles: checked on the host)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4_t, acc[m][n]), tprs,
+                                                 (unsigned)(((long)s * M + row) * part_ld + col) * 4u, 0, kSysCoherent);
+        } else if (part_vec && col + 3 < n_rows) {
           *reinterpret_cast<floatx4*>(dst) = acc[m][n];
         } else {
 #pragma unroll
@@ -429,6 +612,7 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
       }
     }
   }
+  if constexpr (TAIL) ws_tail(tl, part, M, part_ld, K / ks, t, n_tiles, smem);
 }
 
 // ---------------------------------------------------------------------------------
@@ -446,12 +630,12 @@ constexpr int lw_nsw(int MT, int BN) {
   return n > 12 ? 12 : n;
 }
 
-template <int MT, int BN, bool SWIGLU>
+template <int MT, int BN, bool SWIGLU, bool TAIL>
 __global__ __launch_bounds__(384, 1) void wsgemm_lw_kernel(const bf16_t* __restrict__ X, long ldx,
                                                            const bf16_t* __restrict__ W, int M, int K, int ks,
                                                            int n_tiles, int swiglu_I, bf16_t* __restrict__ out,
                                                            long ldo, float* __restrict__ part, long part_ld,
-                                                           long n_rows, int rot_mul) {
+                                                           long n_rows, int rot_mul, WsTail tl) {
   constexpr int ROWS = 16 * MT;
   constexpr int MTW = MT / 4;
   constexpr int NT = BN / 16;
@@ -515,8 +699,9 @@ __global__ __launch_bounds__(384, 1) void wsgemm_lw_kernel(const bf16_t* __restr
       __builtin_amdgcn_sched_barrier(0);
       if (st + NSW - 1 < nst) issue_w(st + NSW - 1);
     }
-    return;  // the epilogue is the compute waves' (no barrier after the loop)
-  }
+    // the epilogue is the compute waves' (no barrier after the loop); a fused tail needs
+    // every wave again
+  } else {
 
   const bf16_t* xsrc[LX];
 #pragma unroll
@@ -571,6 +756,9 @@ __global__ __launch_bounds__(384, 1) void wsgemm_lw_kernel(const bf16_t* __restr
   // 16n + 4g .. +3
   const bool split = part != nullptr;
   const bool part_vec = split && part_ld % 4 == 0 && reinterpret_cast<uintptr_t>(part) % 16 == 0;
+  // (fused tail: the partial slabs through a buffer resource, written past L1 / L2)
+  const __amdgpu_buffer_rsrc_t tprs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)part, (short)0, (int)min((long)(K / ks) * M * part_ld * 4, 0x7FFFFFF0L), 0x00020000);
   const bool out_vec = ldo % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 8 == 0;
 #pragma unroll
   for (int m = 0; m < MTW; ++m) {
@@ -598,7 +786,10 @@ __global__ __launch_bounds__(384, 1) void wsgemm_lw_kernel(const bf16_t* __restr
       for (int n = 0; n < NT; ++n) {
         const long col = wrow(16 * n + 4 * g);
         float* dst = part + (long)s * M * part_ld + (long)row * part_ld + col;
-        if (part_vec && col + 3 < n_rows) {
+        if (TAIL) {  // fused tail: through to memory
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4_t, acc[m][n]), tprs,
+                                                 (unsigned)(((long)s * M + row) * part_ld + col) * 4u, 0, kSysCoherent);
+        } else if (part_vec && col + 3 < n_rows) {
           *reinterpret_cast<floatx4*>(dst) = acc[m][n];
         } else {
 #pragma unroll
@@ -624,6 +815,8 @@ __global__ __launch_bounds__(384, 1) void wsgemm_lw_kernel(const bf16_t* __restr
       }
     }
   }
+  }  // (compute waves)
+  if constexpr (TAIL) ws_tail(tl, part, M, part_ld, K / ks, t, n_tiles, smem);  // every wave: it has barriers
 }
 
 // K-step rotation multiplier: -1 = policy (5 for unsplit-K grids -- the long-K gate_up
@@ -633,37 +826,40 @@ int g_ws_rot_mul = -1;
 
 template <int MT, int BN, bool SWIGLU>
 void launch_ws(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks, int S, int n_tiles, int I,
-               bf16_t* out, long ldo, float* part, long part_ld, long n_rows, hipStream_t st) {
+               bf16_t* out, long ldo, float* part, long part_ld, long n_rows, hipStream_t st, const WsTail& tl) {
   constexpr size_t lds = (size_t)ws_stages(MT, BN) * (16 * MT * 128 + BN * 128);
-  auto kern = wsgemm_kernel<MT, BN, SWIGLU>;
-  LK_SET_MAX_LDS(kern, (int)lds);
+  // (the fused-tail instantiation only where a tail runs: the plain kernel keeps its registers)
+  auto kern = tl.kind ? wsgemm_kernel<MT, BN, SWIGLU, true> : wsgemm_kernel<MT, BN, SWIGLU, false>;
+  if (tl.kind) LK_SET_MAX_LDS((wsgemm_kernel<MT, BN, SWIGLU, true>), (int)lds);
+  else LK_SET_MAX_LDS((wsgemm_kernel<MT, BN, SWIGLU, false>), (int)lds);
   // kNN scores (n_rows given: a corpus, not a weight) walk K in one order in every tile, so
   // equal corpus rows score bit-identically and ties keep the stable id order
   const int rot_mul = n_rows < (1L << 40) ? 0 : g_ws_rot_mul >= 0 ? g_ws_rot_mul : (S == 1 ? 5 : 0);
-  kern<<<n_tiles * S, 256, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows, rot_mul);
+  kern<<<n_tiles * S, 256, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows, rot_mul, tl);
 }
 
 template <int MT, int BN, bool SWIGLU>
 void launch_ws_lw(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks, int S, int n_tiles, int I,
-                  bf16_t* out, long ldo, float* part, long part_ld, long n_rows, hipStream_t st) {
+                  bf16_t* out, long ldo, float* part, long part_ld, long n_rows, hipStream_t st, const WsTail& tl) {
   constexpr size_t lds = (size_t)lw_nsx(MT) * 16 * MT * 128 + (size_t)lw_nsw(MT, BN) * BN * 128;
-  auto kern = wsgemm_lw_kernel<MT, BN, SWIGLU>;
-  LK_SET_MAX_LDS(kern, (int)lds);
+  auto kern = tl.kind ? wsgemm_lw_kernel<MT, BN, SWIGLU, true> : wsgemm_lw_kernel<MT, BN, SWIGLU, false>;
+  if (tl.kind) LK_SET_MAX_LDS((wsgemm_lw_kernel<MT, BN, SWIGLU, true>), (int)lds);
+  else LK_SET_MAX_LDS((wsgemm_lw_kernel<MT, BN, SWIGLU, false>), (int)lds);
   const int rot_mul = n_rows < (1L << 40) ? 0 : g_ws_rot_mul >= 0 ? g_ws_rot_mul : (S == 1 ? 5 : 0);
-  kern<<<n_tiles * S, 384, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows, rot_mul);
+  kern<<<n_tiles * S, 384, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows, rot_mul, tl);
 }
 
 template <bool SWIGLU>
 int dispatch_ws(int MT, int BN, const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks, int S,
                 int n_tiles, int I, bf16_t* out, long ldo, float* part, long part_ld, hipStream_t st,
-                long n_rows = 1L << 40, int variant = 0) {
-#define LK_WS(mt, bn)                                                                                      \
-  if (MT == mt && BN == bn) {                                                                              \
-    if (variant == 1)                                                                                      \
-      launch_ws_lw<mt, bn, SWIGLU>(x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, part, part_ld, n_rows, st); \
-    else                                                                                                   \
-      launch_ws<mt, bn, SWIGLU>(x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, part, part_ld, n_rows, st);    \
-    return 0;                                                                                              \
+                long n_rows = 1L << 40, int variant = 0, const WsTail& tl = WsTail{}) {
+#define LK_WS(mt, bn)                                                                                          \
+  if (MT == mt && BN == bn) {                                                                                  \
+    if (variant == 1)                                                                                          \
+      launch_ws_lw<mt, bn, SWIGLU>(x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, part, part_ld, n_rows, st, tl); \
+    else                                                                                                       \
+      launch_ws<mt, bn, SWIGLU>(x, ldx, w, M, K, ks, S, n_tiles, I, out, ldo, part, part_ld, n_rows, st, tl);    \
+    return 0;                                                                                                  \
   }
   LK_WS(4, 64) LK_WS(4, 128) LK_WS(8, 64) LK_WS(8, 128) LK_WS(12, 64) LK_WS(12, 128) LK_WS(16, 64) LK_WS(16, 128)
 #undef LK_WS
@@ -793,6 +989,62 @@ int lk_wsgemm_part(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int
   const int MT = ws_mt(M);
   const int rc = dispatch_ws<false>(MT, BN, x, ldx, w, M, K, K / S, S, N / BN, 0, nullptr, 0, part, N, st,
                                     1L << 40, ws_variant(M, N, K, 0));
+  LK_CHECK_LAUNCH();
+  return rc;
+}
+
+// split-K GEMM whose last split workgroup per head applies RoPE and writes the paged KV (WsTail
+// kind 1): the rows lk_splitk_rope_kv would leave, without its launch.  Needs one column tile per
+// head (BN == D) and S in {2, 4, 8}; tickets: >= (Hq + 2 Hkv) zeroed int32.
+int lk_ws_rope_kv_fused(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int BN, int S, float* part,
+                        int* tickets, bf16_t* qkv, long qs, const int* positions, const float* cos_sin, int Hq,
+                        int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,
+                        int write_k_inplace, hipStream_t st) {
+  const int N = (Hq + 2 * Hkv) * D;
+  if (M < 1 || M > 256 || !(S == 2 || S == 4 || S == 8) || K % (S * 64) || BN != D || BN != 128 || !part ||
+      !tickets || !qkv || qs % 8 || D % 16 || (long)S * M * N * 4 >= 0x7FFFFFF0L)
+    return -1;
+  WsTail tl;
+  tl.kind = 1;
+  tl.tickets = tickets;
+  tl.out = qkv;
+  tl.os = qs;
+  tl.positions = positions;
+  tl.cos_sin = cos_sin;
+  tl.Hq = Hq;
+  tl.Hkv = Hkv;
+  tl.D = D;
+  tl.kc = kc;
+  tl.vc = vc;
+  tl.slots = slots;
+  tl.BS = BS;
+  tl.neox = neox;
+  tl.write_k_inplace = write_k_inplace;
+  const int rc = dispatch_ws<false>(ws_mt(M), BN, x, ldx, w, M, K, K / S, S, N / BN, 0, nullptr, 0, part, N, st,
+                                    1L << 40, ws_variant(M, N, K, 0), tl);
+  LK_CHECK_LAUNCH();
+  return rc;
+}
+
+// split-K GEMM + residual add + RMSNorm by the grid's last workgroup (WsTail kind 2), for a few
+// rows (M <= 4: one workgroup normalises them all); tickets: >= 1 zeroed int32
+int lk_ws_rmsnorm_fused(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, float* part,
+                        int* tickets, bf16_t* out, long os, bf16_t* residual, long rs, const bf16_t* norm_w, float eps,
+                        hipStream_t st) {
+  if (M < 1 || M > 4 || !(S == 2 || S == 4 || S == 8) || K % (S * 64) || (BN != 64 && BN != 128) || N % BN ||
+      !part || !tickets || !out || !residual || os % 8 || rs % 8 || (long)S * M * N * 4 >= 0x7FFFFFF0L)
+    return -1;
+  WsTail tl;
+  tl.kind = 2;
+  tl.tickets = tickets;
+  tl.out = out;
+  tl.os = os;
+  tl.residual = residual;
+  tl.rs = rs;
+  tl.norm_w = norm_w;
+  tl.eps = eps;
+  const int rc = dispatch_ws<false>(ws_mt(M), BN, x, ldx, w, M, K, K / S, S, N / BN, 0, nullptr, 0, part, N, st,
+                                    1L << 40, ws_variant(M, N, K, 0), tl);
   LK_CHECK_LAUNCH();
   return rc;
 }

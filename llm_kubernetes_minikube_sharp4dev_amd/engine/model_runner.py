@@ -108,8 +108,9 @@ class ModelRunner:
         log.info("kv cache: %d blocks x %d tokens (%.1f GB)", num_blocks, block_size,
                  num_blocks * block_bytes / 2**30)
         self.use_graphs = use_graphs and self.device.type == "cuda"
-        if self.device.type == "cuda":  # the fused split-decode tickets exist before any capture
+        if self.device.type == "cuda":  # the fused split-decode / split-K tail tickets exist before any capture
             ops.decode_tickets(self.device, 2 * max_num_seqs * self.hkv)
+            ops.ws_tickets(self.device)
         # cascade decode attention over the batch's shared prompt prefix (GPU kernels; opt-in
         # LK_CASCADE=1).  Measured on MI355X at the RAG operating point (B=120, 288 of ~950
         # keys shared): 8.06 ms per decode step with vs 7.71 without -- the shared blocks

@@ -803,12 +803,32 @@ def _ws_split_plan(x, w):
     return plan if plan[1] in (2, 4, 8) else None
 
 
+# Split-K decode GEMMs whose reduction runs in their own last workgroup(s) (csrc/skinny_gemm.hip
+# WsTail): the QKV projection's RoPE + paged-KV write (one ticket per head), and for <= 4 rows the
+# o / down projections' residual + RMSNorm -- no reduce launch after them (batch-1 decode: three
+# ~5 us launches per layer).  LK_WS_FUSED_TAIL=0: the separate reduce kernels.
+WS_FUSED_TAIL = os.environ.get("LK_WS_FUSED_TAIL", "1") != "0"
+_WS_TICKETS: dict = {}
+
+
+def ws_tickets(device):
+    """Zeroed int32 tickets of the fused split-K tails (one buffer per device, made before any
+    graph capture by the model runner; every ticket is reset by its last taker)."""
+    device = torch.device(device)
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    t = _WS_TICKETS.get(key)
+    if t is None:
+        t = _WS_TICKETS[key] = torch.zeros(4096, dtype=torch.int32, device=device)
+    return t
+
+
 def linear_add_rmsnorm(x, w, residual, norm_w, eps: float):
     """RMSNorm(x W^T + residual) * norm_w, with ``residual`` updated in place to
     x W^T + residual (the pre-norm block's "o / down projection -> add -> norm")."""
     plan = _ws_split_plan(x, w)
     if plan is not None and residual.is_contiguous():
-        return lib().ws_linear_rmsnorm(x, w, residual, norm_w, eps, plan[0], plan[1])
+        tk = ws_tickets(x.device) if WS_FUSED_TAIL and x.shape[0] <= 4 else None
+        return lib().ws_linear_rmsnorm(x, w, residual, norm_w, eps, plan[0], plan[1], tk)
     return rmsnorm(linear(x, w), norm_w, eps, residual=residual)
 
 
@@ -820,8 +840,9 @@ def linear_rope_kv(x, w, positions, cos_sin, Hq: int, Hkv: int, D: int, k_cache=
     paged-KV write)."""
     plan = _ws_split_plan(x, w)
     if plan is not None:
+        tk = ws_tickets(x.device) if WS_FUSED_TAIL and plan[0] == D == 128 else None
         return lib().ws_linear_rope_kv(x, w, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache, slots, neox,
-                                       write_k_inplace, plan[0], plan[1])
+                                       write_k_inplace, plan[0], plan[1], tk)
     if _qkv_epilogue_ok(x, w, neox, write_k_inplace, k_cache, slots):
         return linear_qkv_fused(x, w, None, 1e-5, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache, slots)
     qkv = linear(x, w)
