@@ -188,7 +188,7 @@ def main():
     from llm_kubernetes_minikube_sharp4dev_amd.rag.corpus import build_chunks
 
     ncpu = os.cpu_count() or 8
-    chunks = build_chunks(args.docs, args.seed, workers=max(1, min(16, ncpu // max(1, world))),
+    chunks = build_chunks(args.docs, args.seed, workers=max(1, min(16, ncpu) // max(1, world)),  # (at most 16 workers over all ranks)
                           section_chars=1150 if args.long_evidence else 0)
     log(rank, f"corpus: {args.docs} docs -> {len(chunks)} chunks ({time.perf_counter() - t_setup:.1f}s)")
 
