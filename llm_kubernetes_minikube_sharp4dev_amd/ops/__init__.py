@@ -840,7 +840,9 @@ def linear_rope_kv(x, w, positions, cos_sin, Hq: int, Hkv: int, D: int, k_cache=
     paged-KV write)."""
     plan = _ws_split_plan(x, w)
     if plan is not None:
-        tk = ws_tickets(x.device) if WS_FUSED_TAIL and plan[0] == D == 128 else None
+        # (rows <= 64: past that the last workgroup of a head reduces >= 128 KB of partials alone,
+        # as long as the reduce kernel's whole launch)
+        tk = ws_tickets(x.device) if WS_FUSED_TAIL and plan[0] == D == 128 and x.shape[0] <= 64 else None
         return lib().ws_linear_rope_kv(x, w, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache, slots, neox,
                                        write_k_inplace, plan[0], plan[1], tk)
     if _qkv_epilogue_ok(x, w, neox, write_k_inplace, k_cache, slots):
