@@ -805,9 +805,12 @@ def _ws_split_plan(x, w):
 
 # Split-K decode GEMMs whose reduction runs in their own last workgroup(s) (csrc/skinny_gemm.hip
 # WsTail): the QKV projection's RoPE + paged-KV write (one ticket per head), and for <= 4 rows the
-# o / down projections' residual + RMSNorm -- no reduce launch after them (batch-1 decode: three
-# ~5 us launches per layer).  LK_WS_FUSED_TAIL=0: the separate reduce kernels.
-WS_FUSED_TAIL = os.environ.get("LK_WS_FUSED_TAIL", "1") != "0"
+# o / down projections' residual + RMSNorm -- no reduce launch after them.  Measured OFF: at batch 1
+# (same box, twice each, profiles/r6_ws_tail/) a decode step took 4.34 / 4.32 ms with the tails vs
+# 3.685 / 3.672 ms with the three ~5 us reduce launches per layer (p50 161.8 vs 139.4 ms): the
+# write-through partials and the one-workgroup reductions cost more than the launches they save.
+# LK_WS_FUSED_TAIL=1 turns them on (numerics: tests/test_kernels_gpu.py *fused_tail*).
+WS_FUSED_TAIL = os.environ.get("LK_WS_FUSED_TAIL", "0") == "1"
 _WS_TICKETS: dict = {}
 
 
