@@ -57,8 +57,24 @@ def create_rag_app(cfg: Optional[Config] = None, index=None, llm=None, k8s=None,
 
     from ..serving.batcher import MicroBatcher
 
-    knn_batcher = MicroBatcher(lambda qs: index.search_vectors(np.stack([np.asarray(q, dtype=np.float32) for q in qs]),
-                                                               r.agent_topk), max_items=64)
+    # the app's kNN shares the GPU with the model server's engine: its few small kernels go on a
+    # high-priority stream so they are dispatched ahead of the engine's queued step kernels
+    knn_stream = None
+    if getattr(getattr(index, "device", None), "type", "cpu") == "cuda":
+        import torch
+
+        knn_stream = torch.cuda.Stream(index.device, priority=-1)
+
+    def knn_batch(qs):
+        qa = np.stack([np.asarray(q, dtype=np.float32) for q in qs])
+        if knn_stream is None:
+            return index.search_vectors(qa, r.agent_topk)
+        import torch
+
+        with torch.cuda.stream(knn_stream):
+            return index.search_vectors(qa, r.agent_topk)
+
+    knn_batcher = MicroBatcher(knn_batch, max_items=64)
 
     @app.get("/health")
     async def health():

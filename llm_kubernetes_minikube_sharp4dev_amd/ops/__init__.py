@@ -114,12 +114,16 @@ def decode_splits(max_context: int, split: int) -> int:
 
 
 # Split decode: the last split workgroup of each (sequence, kv head) merges the partials
-# itself (csrc/attn_decode.hip merge_splits) instead of a decode_reduce launch after the kernel
-# (~5 us per layer and step, on the batch-1 critical path; launched even when no row had more
-# than one split).  Needs one zero-initialised int32 ticket per (sequence, kv head), reset by its
-# last taker: a per-device buffer made before any graph capture.  LK_DECODE_FUSED_REDUCE=0: the
-# separate reduce kernel.
-DECODE_FUSED_REDUCE = os.environ.get("LK_DECODE_FUSED_REDUCE", "1") != "0"
+# itself (csrc/attn_decode.hip merge_splits) instead of a decode_reduce launch after the kernel.
+# Needs one zero-initialised int32 ticket per (sequence, kv head), reset by its last taker: a
+# per-device buffer made before any graph capture.  Used where the batch fills the CUs unsplit
+# (B x Hkv >= 512, 2048-key workgroups): rows of <= 2048 keys write their output directly and the
+# reduce launch (which round 5 made on every layer of every step, to find nothing to merge) is
+# gone.  At small batches, where every row splits, the separate reduce kernel measured faster
+# (batch 1, same box, twice each: decode step 3.74 / 3.73 ms fused vs 3.65 / 3.61 ms,
+# profiles/r6_fused_merge/): the split workgroups' write-through partials and ticket sit on the
+# critical path.  LK_DECODE_FUSED_REDUCE=0: never, =2: always.
+DECODE_FUSED_REDUCE = int(os.environ.get("LK_DECODE_FUSED_REDUCE", "1") or 0)
 _DECODE_TICKETS: dict = {}
 
 
@@ -149,7 +153,9 @@ def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_
         if max_splits is None:
             max_splits = decode_splits(block_tables.shape[1] * BS, split)
         pp_o, pp_ml = prefix if prefix is not None else (None, None)
-        tickets = decode_tickets(q.device, q.shape[0] * k_cache.shape[1]) if DECODE_FUSED_REDUCE else None
+        bh = q.shape[0] * k_cache.shape[1]
+        fused = DECODE_FUSED_REDUCE == 2 or (DECODE_FUSED_REDUCE == 1 and bh >= 512)
+        tickets = decode_tickets(q.device, bh) if fused else None
         return lib().paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, max_splits, split, scale,
                                   part_o, part_ml, out, k_start, pp_o, pp_ml, tickets)
     y = ref.paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
