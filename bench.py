@@ -295,6 +295,11 @@ def main():
     del full, shard, mine
     sync()
     t_index = time.perf_counter() - t0
+    if on_gpu and not args.no_graphs and args.admit_chunk == 1:
+        # one query per retrieval (batch 1): its encoder pass replays a hipGraph per length
+        t_cap = time.perf_counter()
+        ncap = emb_engine.capture_queries(dtypes=(torch.bfloat16,))
+        log(rank, f"query encoder: {ncap} hipGraphs captured in {time.perf_counter() - t_cap:.1f}s")
     index = RagIndex(LocalEmbedder(emb_engine), backend="gpu", device=str(dev))
     index.chunks = [RagChunk(i, s, t) for i, s, t in chunks]
     index.set_gpu_corpus(corpus)

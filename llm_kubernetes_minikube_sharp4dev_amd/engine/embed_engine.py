@@ -41,6 +41,14 @@ if os.environ.get("LK_GEMM_LIBRARY", "0") == "1":
     BUILD_STREAMS = EMBED_STREAMS = 1
 
 
+# One query of at most QUERY_GRAPH_MAX_LEN tokens (the batch-1 serving path: a request's
+# retrieval is on its own critical path) replays a hipGraph of the whole encoder captured for its
+# length by :meth:`EmbeddingEngine.capture_queries`, instead of ~85 eager launches (~1 ms of host
+# time the device waits through).  LK_EMBED_GRAPHS=0: always eager.
+QUERY_GRAPHS = os.environ.get("LK_EMBED_GRAPHS", "1") != "0"
+QUERY_GRAPH_MAX_LEN = 64
+
+
 class EmbeddingEngine:
     def __init__(self, model, tokenizer, name: str = "encoder", max_tokens_per_batch: int = 65536,
                  max_len: Optional[int] = None):
@@ -88,6 +96,9 @@ class EmbeddingEngine:
             pos = (np.arange(b - a, dtype=np.int64) - np.repeat(starts[i:j] - a, ln)).astype(np.int32)
             cu = (starts[i:j + 1] - a).astype(np.int32)
             st = streams[k % len(streams)] if streams else None
+            if j - i == 1 and st is None and self._replay_query(flat[a:b], out[row0 + i:row0 + j]):
+                i, k = j, k + 1
+                continue
             with torch.cuda.stream(st) if st is not None else _nullctx():
                 dst = out[row0 + i:row0 + j]
                 # on the GPU the pooling kernel writes the rows of ``out`` (f32 or bf16) itself
@@ -98,6 +109,80 @@ class EmbeddingEngine:
                 if emb.data_ptr() != dst.data_ptr():
                     dst.copy_(emb)
             i, k = j, k + 1
+
+    # ------------------------------------------------------------------ query hipGraphs
+    @torch.inference_mode()
+    def capture_queries(self, max_len: int = QUERY_GRAPH_MAX_LEN, dtypes=(torch.bfloat16, torch.float32),
+                        priority: int = 0) -> int:
+        """Capture one hipGraph of the encoder per single-query length 1..max_len (and output
+        dtype), sharing one memory pool; returns the number captured.  Call once at start-up,
+        while nothing else runs on the device (capture is thread-local: other threads' launches
+        stay legal).  ``priority``: of the stream the replays run on (-1: a serving process's
+        query embeddings go ahead of the LLM engine's queued kernels, as embed_cpu's do)."""
+        if self.device.type != "cuda" or not QUERY_GRAPHS:
+            return 0
+        from .. import ops
+
+        d = self.device
+        self._qgraphs = getattr(self, "_qgraphs", {})
+        self._qpool = getattr(self, "_qpool", None) or torch.cuda.graph_pool_handle()
+        n = 0
+        with self.lock:
+            for dt in dtypes:
+                for L in range(1, max_len + 1):
+                    if (L, dt) in self._qgraphs:
+                        continue
+                    ids = torch.full((L,), 101 % self.model.cfg.vocab_size, dtype=torch.int32, device=d)
+                    cu = torch.tensor([0, L], dtype=torch.int32, device=d)
+                    pos = torch.arange(L, dtype=torch.int32, device=d)
+                    out = torch.empty((1, self.dim), dtype=dt, device=d)
+                    G = self.model.nh // self.model.nh  # (encoder attention: one kv head per head)
+                    ts, tq = ops.prefill_tiles([L], [L], G, False, self.model.D)
+                    tiles = (torch.from_numpy(ts).to(d), torch.from_numpy(tq).to(d))
+                    side = torch.cuda.Stream(d)
+                    side.wait_stream(torch.cuda.current_stream(d))
+                    with torch.cuda.stream(side):  # warm-up launch (lazy kernel attributes, allocator)
+                        self.model(ids, cu, pos, [L], out=out, tiles=tiles)
+                    torch.cuda.current_stream(d).wait_stream(side)
+                    g = torch.cuda.CUDAGraph()
+                    try:
+                        with torch.cuda.graph(g, pool=self._qpool, capture_error_mode="thread_local"):
+                            self.model(ids, cu, pos, [L], out=out, tiles=tiles)
+                    except Exception as e:  # an op that cannot be captured: stay eager (loudly)
+                        import logging
+
+                        logging.getLogger("lk.embed").warning("query encoder graph capture failed at "
+                                                              "length %d (%r): eager launches", L, e)
+                        self._qgraphs.clear()
+                        return 0
+                    self._qgraphs[(L, dt)] = (g, ids, out, tiles)
+                    n += 1
+            self._gstream = torch.cuda.Stream(d, priority=priority)
+        return n
+
+    def _replay_query(self, seq: np.ndarray, dst: torch.Tensor) -> bool:
+        """One query's encoder pass by graph replay into ``dst`` [1, D] (False: no graph).
+        Called under ``self.lock``; input copy, replay and output copy all go on one stream of
+        this engine, so concurrent callers (the server's embedding threads) never overwrite a
+        graph's buffers under a replay still in flight."""
+        graphs = getattr(self, "_qgraphs", None)
+        if not graphs or torch.cuda.is_current_stream_capturing():
+            return False
+        ent = graphs.get((len(seq), dst.dtype))
+        if ent is None:
+            return False
+        g, ids, out, _ = ent
+        host = torch.from_numpy(np.ascontiguousarray(seq, dtype=np.int32)).pin_memory()
+        cur = torch.cuda.current_stream(self.device)
+        gs = self._gstream
+        gs.wait_stream(cur)  # dst exists (and whatever the caller queued before it)
+        with torch.cuda.stream(gs):
+            ids.copy_(host, non_blocking=True)
+            g.replay()
+            dst.copy_(out)
+        dst.record_stream(gs)
+        cur.wait_stream(gs)
+        return True
 
     @torch.inference_mode()
     def embed_ids(self, seqs: list[list[int]]) -> torch.Tensor:

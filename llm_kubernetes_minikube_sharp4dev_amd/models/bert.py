@@ -80,9 +80,10 @@ class EncoderModel(nn.Module):
         return self
 
     def forward(self, ids: torch.Tensor, cu: torch.Tensor, positions: torch.Tensor,
-                lens_cpu: list, type_ids=None, pool: bool = True, out=None):
+                lens_cpu: list, type_ids=None, pool: bool = True, out=None, tiles=None):
         """ids/positions [T] int32 packed; cu [B+1] int32 -> [B, H] f32 embeddings (``out``: the
-        pooling kernel writes these rows instead, f32 or bf16)."""
+        pooling kernel writes these rows instead, f32 or bf16; ``tiles``: the attention's device
+        tile list, precomputed -- a hipGraph capture cannot upload it)."""
         cfg, nh, D, H = self.cfg, self.nh, self.D, self.cfg.hidden
         h = ops.embed_layernorm(ids, None if cfg.rotary else positions, type_ids, self.tok, self.pos,
                                 self.typ, self.emb_ln_w, self.emb_ln_b, cfg.norm_eps)
@@ -91,7 +92,7 @@ class EncoderModel(nn.Module):
             if cfg.rotary:
                 ops.rope_kv_(qkv, positions, self.cos_sin, nh, nh, D, None, None, None, True, True)
             a = ops.flash_prefill(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], cu, nh, nh, D, self.scale,
-                                  False, q_lens_cpu=lens_cpu)
+                                  False, q_lens_cpu=lens_cpu, tiles=tiles)
             o = ops.linear(a, L.o, L.o_b)
             h = ops.layernorm(o, L.ln1_w, L.ln1_b, cfg.norm_eps, residual=h)
             if cfg.activation == "swiglu":

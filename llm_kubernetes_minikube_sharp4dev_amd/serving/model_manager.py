@@ -196,8 +196,10 @@ class ModelManager:
             t0 = time.perf_counter()
             ck = self.checkpoints.get(name) or self.checkpoints.get(preset)
             enc = build_encoder(preset, device=self.device, seed=self.cfg.engine.seed, checkpoint=ck, dtype=self._dtype())
-            h = EmbedderHandle(name, preset, EmbeddingEngine(enc, load_tokenizer(ck), name=name),
-                               load_s=time.perf_counter() - t0)
+            eng = EmbeddingEngine(enc, load_tokenizer(ck), name=name)
+            if self.device.type == "cuda":  # one-query /api/embeddings calls replay hipGraphs
+                eng.capture_queries(dtypes=(torch.float32,), priority=-1)
+            h = EmbedderHandle(name, preset, eng, load_s=time.perf_counter() - t0)
             self.embedders[name] = h
             log.info("loaded embedder %s (%s) in %.1fs", name, preset, h.load_s)
             return h

@@ -73,6 +73,14 @@ def test_bench_self_launch_two_ranks():
     assert all(r["completions"] > 0 for r in dist["per_replica"])
 
 
+def test_bench_self_launch_tp2():
+    """``python bench.py --gpus 2 --tp 2`` (no launcher): one TP group of the two self-launched
+    ranks, the sharded kNN equal to the single scan."""
+    d = _run(["--tp", "2"], nproc=2, self_launch=True)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "tp2" and d["value"] > 0
+    assert d["config"]["knn"]["matches_single_scan"] is True
+
+
 def test_bench_refuses_gpus_world_mismatch():
     """--gpus 2 inside a launcher that started WORLD_SIZE=1 is refused before any work."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "2"],

@@ -369,3 +369,39 @@ def test_bulk_embedding_two_streams_bit_identical(monkeypatch):
         outs.append(eng.embed(chunks))
         torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+
+
+def test_query_encoder_graphs_equal_eager():
+    """Single-query embeddings replayed from the per-length encoder hipGraphs
+    (EmbeddingEngine.capture_queries) equal the eager encoder's, f32 and bf16 rows, also from
+    several threads at once (replays are serialised on the engine's graph stream)."""
+    import threading
+
+    from llm_kubernetes_minikube_sharp4dev_amd.engine.embed_engine import EmbeddingEngine
+    from llm_kubernetes_minikube_sharp4dev_amd.models.tokenizer import builtin_tokenizer
+
+    enc = build_encoder("bge-base", device=DEV, dtype=torch.bfloat16)
+    tok = builtin_tokenizer()
+    eager = EmbeddingEngine(enc, tok, name="e")
+    graphed = EmbeddingEngine(enc, tok, name="g")
+    assert graphed.capture_queries(max_len=24) == 48
+    texts = ["scale the api deployment in staging", "logs of pod web-1", "x", "how do I restart the worker",
+             "namespace dev replicas 3 please now quickly"]
+    for t in texts:
+        for dt in (torch.float32, torch.bfloat16):
+            want = eager.embed([t], dtype=dt)
+            got = graphed.embed([t], dtype=dt)
+            assert torch.equal(got, want), (t, dt)
+    res = {}
+
+    def worker(i):
+        res[i] = [graphed.embed_cpu([t]) for t in texts]
+
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(3)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    ref = [eager.embed_cpu([t]) for t in texts]
+    for i in range(3):
+        assert all(torch.equal(a, b) for a, b in zip(res[i], ref)), i
