@@ -4,7 +4,8 @@ chunks (compute-bound) and paged decode over its decode rows (HBM-bound) at the 
 (Llama-3-8B heads, 6 prompts x 643 new tokens over 930 keys; 128 decode rows x 1000 keys), timed
 back to back on one stream vs on two streams (both launch orders) and, with --splits, on two
 streams restricted to disjoint CU sets; cold KV (rotated copies), HIP events, medians of
-interleaved rounds.  (A flash-occupancy-cap arm -- unused LDS so a decode workgroup fits beside
+interleaved rounds.  ``unified``: one flash launch over both, the decode rows as one-token
+sequences in the same heaviest-first tile list.  (A flash-occupancy-cap arm -- unused LDS so a decode workgroup fits beside
 one flash workgroup per CU -- measured 190 us vs 178 serial and was removed.)
 
     python benchmarks/attn_overlap.py [--md out.md]
@@ -19,6 +20,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from llm_kubernetes_minikube_sharp4dev_amd import ops  # noqa: E402
@@ -57,6 +59,43 @@ def main():
     tiles = (torch.from_numpy(ts).to(DEV), torch.from_numpy(tq).to(DEV))
     out_p = torch.empty_like(qp)
     out_d = torch.empty_like(qd)
+    # unified: ONE flash launch over [prompt rows | decode rows], the decode rows as q_len-1
+    # sequences (causal with past = ctx - 1), tiles of both kinds in one heaviest-first list
+    W = bt_d.shape[1]
+    bt_u = torch.zeros(Bp + Bd, W, dtype=torch.int32, device=DEV)
+    bt_u[:Bp, :nb_p] = bt_p
+    bt_u[Bp:] = bt_d
+    q_u = torch.cat([qp, qd.view(Bd, Hq * D)])
+    cu_u = torch.cat([cu, cu[-1] + torch.arange(1, Bd + 1, dtype=torch.int32, device=DEV)])
+    cl_u = torch.cat([cl_p, cl_d])
+    tsu, tqu = ops.prefill_tiles([q] * Bp + [1] * Bd, [ctx_p] * Bp + [ctx_d] * Bd, Hq // Hkv, True)
+    tiles_u = (torch.from_numpy(tsu).to(DEV), torch.from_numpy(tqu).to(DEV))
+    # other orders of the same tile list: decode tiles (seq >= Bp) interleaved one-for-one with
+    # the prompt tiles, and prompt tiles first
+    isd = tsu >= Bp
+    dpos, ppos = np.nonzero(isd)[0], np.nonzero(~isd)[0]
+    inter = []
+    for i in range(max(len(dpos), len(ppos))):
+        if i < len(ppos):
+            inter.append(ppos[i])
+        if i < len(dpos):
+            inter.append(dpos[i])
+    orders = {"unified_inter": np.asarray(inter), "unified_pfirst": np.concatenate([ppos, dpos])}
+    for k2 in (2, 4):  # k prompt tiles per decode tile
+        o2, di = [], 0
+        for i, pi in enumerate(ppos):
+            o2.append(pi)
+            if i % k2 == k2 - 1 and di < len(dpos):
+                o2.append(dpos[di])
+                di += 1
+        o2.extend(dpos[di:])
+        orders[f"unified_p{k2}d1"] = np.asarray(o2)
+    tiles_o = {k: (torch.from_numpy(tsu[o]).to(DEV), torch.from_numpy(tqu[o]).to(DEV)) for k, o in orders.items()}
+    out_u = torch.empty_like(q_u)
+    cu_dd = torch.arange(0, Bd + 1, dtype=torch.int32, device=DEV)
+    tsd, tqd = ops.prefill_tiles([1] * Bd, [ctx_d] * Bd, Hq // Hkv, True)
+    tiles_dd = (torch.from_numpy(tsd).to(DEV), torch.from_numpy(tqd).to(DEV))
+    out_dd = torch.empty(Bd, Hq * D, device=DEV, dtype=torch.bfloat16)
     side = torch.cuda.Stream()
     sc = 1 / math.sqrt(D)
     it = [0]
@@ -68,6 +107,18 @@ def main():
     def decode(kv):
         ops.paged_decode(qd, kv[0], kv[1], bt_d, cl_d, sc, out=out_d)
 
+    def unified(kv):
+        ops.flash_prefill(q_u, kv[0], kv[1], cu_u, Hq, Hkv, D, sc, True, block_tables=bt_u, ctx_lens=cl_u,
+                          tiles=tiles_u, out=out_u)
+
+    def unified_o(kv, name):
+        ops.flash_prefill(q_u, kv[0], kv[1], cu_u, Hq, Hkv, D, sc, True, block_tables=bt_u, ctx_lens=cl_u,
+                          tiles=tiles_o[name], out=out_u)
+
+    def decode_flash(kv):
+        ops.flash_prefill(qd.view(Bd, Hq * D), kv[0], kv[1], cu_dd, Hq, Hkv, D, sc, True, block_tables=bt_d,
+                          ctx_lens=cl_d, tiles=tiles_dd, out=out_dd)
+
     def arm(name):
         if name in extra:
             return masked_arm(*extra[name])
@@ -77,6 +128,12 @@ def main():
             flash(kv)
         elif name == "decode":
             decode(kv)
+        elif name == "unified":
+            unified(kv)
+        elif name in tiles_o:
+            unified_o(kv, name)
+        elif name == "decode_flash":
+            decode_flash(kv)
         elif name == "serial":
             flash(kv)
             decode(kv)
@@ -142,7 +199,7 @@ def main():
         for e in joins:
             cur.wait_event(e)
 
-    arms = ["flash", "decode", "serial", "2s_flash_first", "2s_decode_first"]
+    arms = ["flash", "decode", "decode_flash", "serial", "2s_flash_first", "2s_decode_first", "unified", *tiles_o]
     extra = {}
     for (K, lay) in masked:
         for which in ("both", "decode", "flash"):
@@ -152,6 +209,18 @@ def main():
     for n in arms:
         arm(n)
     torch.cuda.synchronize()
+    # the unified launch equals the two kernels' outputs
+    kv = copies[0]
+    flash(kv)
+    decode(kv)
+    unified(kv)
+    decode_flash(kv)
+    torch.cuda.synchronize()
+    err_p = (out_u[: Bp * q].float() - out_p.float()).abs().max().item()
+    err_d = (out_u[Bp * q:].float() - out_d.view(Bd, -1).float()).abs().max().item()
+    err_dd = (out_dd.float() - out_d.view(Bd, -1).float()).abs().max().item()
+    print(f"unified vs separate: prefill max|d| {err_p:.3g}, decode max|d| {err_d:.3g}; decode_flash {err_dd:.3g}",
+          flush=True)
     ts_ = {n: [] for n in arms}
     for _ in range(a.rounds):
         for n in arms:

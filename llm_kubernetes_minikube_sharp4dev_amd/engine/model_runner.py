@@ -28,6 +28,7 @@ except Exception:  # pragma: no cover
     _native_rt = None
 
 from .. import ops
+from ..models import attention as _attn
 from ..models.attention import AttnMeta
 from ..utils.logging import get_logger
 
@@ -402,6 +403,21 @@ class ModelRunner:
             host.update(bt_d=si.tables_d, ctx_d=si.ctx_d)
             if si.shared_len:
                 host["shared"] = np.asarray([si.shared_len], dtype=np.int32)
+        uni = _attn.UNIFIED_ATTN and bool(si.q_lens) and si.num_decode > 0 and not si.shared_len
+        if uni:  # one attention launch for the whole step (models/attention.py UNIFIED_ATTN)
+            self.unified_attn_steps = getattr(self, "unified_attn_steps", 0) + 1
+            nd, P = si.num_decode, len(si.q_lens)
+            ql = list(si.q_lens) + [1] * nd
+            cl = list(si.ctx_lens) + np.asarray(si.ctx_d[:nd]).tolist()
+            cu_u = np.zeros(len(ql) + 1, dtype=np.int32)
+            cu_u[1:] = np.cumsum(ql)
+            wp, wd = si.tables_p.shape[1], si.tables_d.shape[1]
+            bt_u = np.zeros((len(ql), max(wp, wd)), dtype=np.int32)
+            bt_u[:P, :wp] = si.tables_p
+            bt_u[P:, :wd] = si.tables_d[:nd]
+            host.update(cu_u=cu_u, ctx_u=np.asarray(cl, dtype=np.int32), bt_u=bt_u)
+            if self.device.type == "cuda":
+                host["ts_u"], host["tq_u"] = ops.prefill_tiles(ql, cl, self.hq // self.hkv, True, self.D)
         if len(si.logits_rows):
             host["logits"] = si.logits_rows
         if si.gather is not None:
@@ -418,6 +434,10 @@ class ModelRunner:
             meta.max_splits = ops.decode_splits(si.tables_d.shape[1] * self.bs, meta.decode_split)
             if si.shared_len:
                 self._cascade_meta(meta, si.num_decode, d["shared"])
+        if uni:
+            meta.cu_u, meta.ctx_lens_u, meta.block_tables_u = d["cu_u"], d["ctx_u"], d["bt_u"]
+            if "ts_u" in d:
+                meta.tiles_u = (d["ts_u"], d["tq_u"])
         meta.logits_idx = d.get("logits")
         ids = d["ids"]
         if si.gather is not None:

@@ -26,6 +26,12 @@ OVERLAP_ATTN = os.environ.get("LK_OVERLAP_ATTN", "1") == "1"
 # the side stream's only after a cross-queue event, so the main one takes the CUs first
 # (LK_ATTN_SIDE=decode: the flash kernel leads; =flash: the paged decode leads).
 ATTN_SIDE = os.environ.get("LK_ATTN_SIDE", "decode")
+# Unified mixed-step attention: ONE flash launch over [prompt rows | decode rows], each decode
+# row a one-token sequence (causal, past = ctx - 1) in the same heaviest-first tile list, so the
+# HBM-bound decode tiles and the MFMA-bound prompt tiles share every CU instead of two kernels
+# waiting for each other's CUs (the model runner builds the combined cu / ctx / block table /
+# tile list once per step: ModelRunner._meta).
+UNIFIED_ATTN = os.environ.get("LK_UNIFIED_ATTN", "0") == "1"
 _side: dict = {}
 
 
@@ -69,6 +75,12 @@ class AttnMeta:
     pp_ml: Optional[torch.Tensor] = None
     # rows whose hidden state feeds the LM head (last token of each prefill + decode rows)
     logits_idx: Optional[torch.Tensor] = None
+    # unified mixed-step attention (UNIFIED_ATTN): sequences = the prefill chunks, then one
+    # per decode row (q_len 1); block tables padded to one width; the flash tile list
+    cu_u: Optional[torch.Tensor] = None
+    ctx_lens_u: Optional[torch.Tensor] = None
+    block_tables_u: Optional[torch.Tensor] = None
+    tiles_u: Optional[tuple] = None
     # context parallelism (paged_attention's cp_group): the block tables / ctx_lens above
     # describe THIS rank's contiguous shard of every sequence's keys, whose first key sits
     # at global position cp_key_start_{p,d}[b] (host ints); queries are replicated
@@ -101,6 +113,12 @@ def paged_attention(qkv: torch.Tensor, k_cache, v_cache, meta: AttnMeta, Hq: int
         return cp_paged_attention(qkv, k_cache, v_cache, meta, Hq, Hkv, D, scale, out, cp_group)
     Tp = meta.num_prefill_tokens
     Bd = meta.num_decode
+    if meta.cu_u is not None and Tp and Bd:
+        T = Tp + Bd
+        ops.flash_prefill(qkv[:T, : Hq * D], k_cache, v_cache, meta.cu_u, Hq, Hkv, D, scale, True,
+                          block_tables=meta.block_tables_u, ctx_lens=meta.ctx_lens_u, tiles=meta.tiles_u,
+                          out=out[:T])
+        return out
 
     def decode():
         q = qkv[Tp:Tp + Bd, : Hq * D].view(Bd, Hq, D)

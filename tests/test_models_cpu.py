@@ -109,6 +109,32 @@ def test_chunked_prefill_prefix_cache_and_preemption_consistent():
     assert sum(x.num_preemptions for x in out) > 0
 
 
+def test_unified_mixed_attention_matches_split(monkeypatch):
+    """LK_UNIFIED_ATTN: a mixed step's decode rows join the prompt chunks as one-token sequences
+    of ONE flash-attention call (combined cu / ctx / block tables built by ModelRunner._meta);
+    tokens equal the split path (flash for the chunks + paged decode for the rows), with
+    chunked prefill interleaved with decode and jump-forward-free greedy decoding."""
+    from llm_kubernetes_minikube_sharp4dev_amd.models import attention
+
+    m = build_decoder("llama-tiny", dtype=torch.float32)
+    prompts = [list(range(3, 3 + n)) for n in (70, 33, 5, 100, 17)]
+    ref = [s.output_ids for s in _engine(m, max_num_batched_tokens=24).generate(prompts, SamplingParams.greedy(12))]
+    seen = []
+    real = attention.ops.flash_prefill
+
+    def spy(q, *a, **kw):
+        seen.append(q.shape[0])
+        return real(q, *a, **kw)
+
+    monkeypatch.setattr(attention, "UNIFIED_ATTN", True)
+    monkeypatch.setattr(attention.ops, "flash_prefill", spy)
+    eng = _engine(m, max_num_batched_tokens=24)
+    out = [s.output_ids for s in eng.generate(prompts, SamplingParams.greedy(12))]
+    assert out == ref
+    # some steps were mixed and ran as one launch covering prompt and decode rows
+    assert getattr(eng.runner, "unified_attn_steps", 0) > 0 and seen and max(seen) <= 24
+
+
 def _run_pipelined(eng, prompts, params_fn, stagger: int = 0):
     """Drive eng with step_pipelined (requests i >= 2 admitted `stagger` iterations apart)."""
     seqs, pending, it = [], list(enumerate(prompts)), 0
