@@ -155,7 +155,10 @@ class EmbeddingEngine:
                                                               "length %d (%r): eager launches", L, e)
                         self._qgraphs.clear()
                         return 0
-                    self._qgraphs[(L, dt)] = (g, ids, out, tiles)
+                    # every tensor the graph reads stays referenced here: a freed ``cu`` / ``pos``
+                    # goes back to the caching allocator, and a replay would read whatever
+                    # reuses it (garbage segment bounds / positions)
+                    self._qgraphs[(L, dt)] = (g, ids, out, tiles, cu, pos)
                     n += 1
             self._gstream = torch.cuda.Stream(d, priority=priority)
         return n
@@ -171,7 +174,7 @@ class EmbeddingEngine:
         ent = graphs.get((len(seq), dst.dtype))
         if ent is None:
             return False
-        g, ids, out, _ = ent
+        g, ids, out = ent[:3]
         host = torch.from_numpy(np.ascontiguousarray(seq, dtype=np.int32)).pin_memory()
         cur = torch.cuda.current_stream(self.device)
         gs = self._gstream
