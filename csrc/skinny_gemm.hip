@@ -862,6 +862,9 @@ int dispatch_ws(int MT, int BN, const bf16_t* x, long ldx, const bf16_t* w, int 
     return 0;                                                                                                  \
   }
   LK_WS(4, 64) LK_WS(4, 128) LK_WS(8, 64) LK_WS(8, 128) LK_WS(12, 64) LK_WS(12, 128) LK_WS(16, 64) LK_WS(16, 128)
+  if constexpr (!SWIGLU) {  // 96-column tiles: projections whose N / 128 tiles leave CUs idle
+    LK_WS(4, 96) LK_WS(8, 96) LK_WS(12, 96) LK_WS(16, 96)
+  }
 #undef LK_WS
   return -2;
 }
@@ -915,12 +918,30 @@ void lk_wsgemm_plan(int M, int N, int K, int swiglu, int* bn_out, int* s_out) {
   };
   int s128 = 1, s64 = 1;
   const double o128 = plan(128, &s128), o64 = plan(64, &s64);
+  double occ;
   if (o128 >= 0.7 || (o128 >= 0 && o64 <= o128)) {
     *bn_out = 128;
     *s_out = s128;
+    occ = o128;
   } else {
     *bn_out = 64;
     *s_out = o64 >= 0 ? s64 : 1;
+    occ = o64;
+  }
+  // 96-column tiles where they fill the CUs better: the Llama-3-8B QKV projection (N 6144) is
+  // 48 x 128-column tiles x 4 K-splits = 192 blocks for 256 CUs, 64 x 96-column tiles x 4 = 256
+  // (LK_WS_BN96=0: off)
+  static const int bn96 = [] {
+    const char* e = getenv("LK_WS_BN96");
+    return e ? atoi(e) : 1;
+  }();
+  if (bn96 && !swiglu) {
+    int s96 = 1;
+    const double o96 = plan(96, &s96);
+    if (o96 > occ + 1e-9) {
+      *bn_out = 96;
+      *s_out = s96;
+    }
   }
 }
 
@@ -952,7 +973,7 @@ int lk_wsgemm_set_variant(int M, int N, int K, int swiglu, int variant) {
 
 int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, int swiglu,
               bf16_t* out, long ldo, float* part, hipStream_t st) {
-  if (M < 1 || M > 256 || S < 1 || K % (S * 64) || (BN != 64 && BN != 128)) return -1;
+  if (M < 1 || M > 256 || S < 1 || K % (S * 64) || (BN != 64 && BN != 128 && (BN != 96 || swiglu))) return -1;
   const int per = swiglu ? BN / 2 : BN;
   if (swiglu ? (N % 2 || (N / 2) % per) : N % BN) return -1;
   if (S > 1 && part == nullptr) return -1;
@@ -985,7 +1006,9 @@ void lk_wsgemm_set_rot(int rot_mul) { g_ws_rot_mul = rot_mul < 0 ? -1 : rot_mul;
 
 int lk_wsgemm_part(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, float* part,
                    hipStream_t st) {
-  if (M < 1 || M > 256 || S < 2 || K % (S * 64) || (BN != 64 && BN != 128) || N % BN || part == nullptr) return -1;
+  if (M < 1 || M > 256 || S < 2 || K % (S * 64) || (BN != 64 && BN != 96 && BN != 128) || N % BN ||
+      part == nullptr)
+    return -1;
   const int MT = ws_mt(M);
   const int rc = dispatch_ws<false>(MT, BN, x, ldx, w, M, K, K / S, S, N / BN, 0, nullptr, 0, part, N, st,
                                     1L << 40, ws_variant(M, N, K, 0));

@@ -433,9 +433,29 @@ def test_ws_linear(hip, M, NK):
     y_ref = x.float() @ w.float().t()
     _close(hip.ws_linear(x, w), y_ref, 0.02, 0.01, f"ws M{M} N{N} K{K}")
     if N <= 6144:
-        for bn, S in ((64, 1), (128, 2), (64, 4)):
+        for bn, S in ((64, 1), (128, 2), (64, 4), (96, 4)):
             if N % bn == 0 and K % (S * 64) == 0:
                 _close(hip.ws_linear(x, w, False, bn, S), y_ref, 0.02, 0.01, f"ws bn{bn} S{S}")
+
+
+@pytest.mark.parametrize("M", [1, 16, 64, 100, 129, 192, 256])
+def test_ws_bn96_plan_and_variants(hip, M):
+    """96-column weight-streaming tiles (the Llama-3-8B QKV projection: 64 tiles x 4 K-splits = 256
+    blocks instead of 192 at 128 columns), ring and loader-wave kernels, plain and with the split-K
+    partials reduced by the RoPE / KV consumer, vs an fp32 matmul."""
+    N, K = 6144, 4096
+    assert tuple(hip.ws_plan(M, N, K, False)) == (96, 4)
+    torch.manual_seed(M)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    y_ref = x.float() @ w.float().t()
+    try:
+        for v in (0, 1):
+            hip.ws_set_variant(M, N, K, False, v)
+            _close(hip.ws_linear(x, w), y_ref, 0.02, 0.01, f"ws bn96 M{M} variant {v}")
+            _close(hip.ws_linear(x, w, False, 96, 2), y_ref, 0.02, 0.01, f"ws bn96 S2 M{M} variant {v}")
+    finally:
+        hip.ws_set_variant(M, N, K, False, -1)
 
 
 @pytest.mark.parametrize("M", [1, 8, 64, 128, 150, 192, 256])
