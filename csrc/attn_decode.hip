@@ -346,7 +346,7 @@ int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc
                     const int* block_tables, int bt_stride, const int* ctx_lens, bf16_t* out,
                     long os, float* part_o, float* part_ml, int B, int Hq, int Hkv, int D, int BS,
                     int max_splits, int split, float scale, const int* k_start, const float* pp_o,
-                    const float* pp_ml, hipStream_t st, int* tickets) {
+                    const float* pp_ml, hipStream_t st, int* tickets, int reduce) {
   if (B == 0) return 0;
   if (Hq % Hkv || BS % 16 || split % 32 || split > kMaxSplit || split % BS) return -1;
   const int G = Hq / Hkv;
@@ -371,7 +371,9 @@ int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc
 #undef BY_G
 #undef LAUNCH
   LK_CHECK_LAUNCH();
-  if ((max_splits > 1 || pp_o) && tickets == nullptr) {  // (fused: the last split merges)
+  // (fused: the last split merges; reduce == 0: the consumer merges -- the O projection's
+  // weight-streaming prologue, lk_wsgemm_pro kind 2)
+  if ((max_splits > 1 || pp_o) && tickets == nullptr && reduce) {
     if (D == 128)
       decode_reduce_kernel<128><<<dim3(Hq, B), 128, 0, st>>>(part_o, part_ml, ctx_lens, out, os, Hq,
                                                              max_splits, split, k_start, pp_o, pp_ml);

@@ -270,6 +270,118 @@ at::Tensor ws_linear_rope_kv(const at::Tensor& x, const at::Tensor& w, const at:
   return qkv;
 }
 
+// Weight-streaming GEMM whose workgroups compute their own X rows first (lk_wsgemm_pro):
+//   kind 1: x (written) = RMSNorm(bf16(sum of pp's slabs) + res_in) * gamma; res_out = the summed
+//           residual (a tensor other than res_in)
+//   kind 2: x = the paged-decode output, rows with > 1 split merged from (po, pml) first
+// Returns the f32 partial slabs [S, M, N] when S > 1 (reduce == false), else the bf16 (SwiGLU)
+// output.
+at::Tensor ws_pro(at::Tensor& x, const at::Tensor& w, bool swiglu, int64_t bn, int64_t splits, int64_t kind,
+                  bool reduce, const c10::optional<at::Tensor>& pp, const c10::optional<at::Tensor>& res_in,
+                  const c10::optional<at::Tensor>& res_out, const c10::optional<at::Tensor>& gamma, double eps,
+                  const c10::optional<at::Tensor>& po, const c10::optional<at::Tensor>& pml,
+                  const c10::optional<at::Tensor>& ctx, int64_t split, int64_t max_splits, int64_t Hq) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "ws_pro: x [M,K], w [N,K]");
+  check_rows16(x, "x"); check_rows16(w, "w");
+  const int M = x.size(0), K = x.size(1), N = w.size(0), S = (int)splits;
+  TORCH_CHECK(M >= 1 && M <= 64 && S >= 1, "ws_pro: 1 <= M <= 64, splits >= 1");
+  const int n_out = swiglu ? N / 2 : N;
+  at::Tensor part, out;
+  if (S > 1) part = at::empty({(long)S, M, N}, x.options().dtype(at::kFloat));
+  if (kind == 0) {  // plain X: the partial slabs only (the producer of a kind-1 consumer)
+    TORCH_CHECK(S > 1 && !swiglu, "ws_pro kind 0: split-K partials (splits > 1, no SwiGLU)");
+    CHECK_RC(lk_wsgemm_part(bp(x), x.stride(0), bp(w), M, N, K, (int)bn, S, part.data_ptr<float>(), cur_stream()),
+             "ws_pro (part)");
+    return part;
+  }
+  if (S == 1 || reduce) out = at::empty({M, n_out}, x.options());
+  const float* ppp = nullptr;
+  int pS = 0;
+  const bf16_t* rin = nullptr;
+  bf16_t* rout = nullptr;
+  long rs = 0;
+  const bf16_t* g = nullptr;
+  if (kind == 1) {
+    TORCH_CHECK(pp && res_in && res_out && gamma, "ws_pro kind 1: pp, res_in, res_out, gamma");
+    CHECK_CUDA(*pp); CHECK_F32(*pp); CHECK_CONTIG(*pp);
+    TORCH_CHECK(pp->dim() == 3 && pp->size(1) == M && pp->size(2) == K, "pp must be [S, M, K]");
+    CHECK_BF16(*res_in); CHECK_BF16(*res_out); CHECK_CONTIG(*res_in); CHECK_CONTIG(*res_out);
+    TORCH_CHECK(res_in->size(0) == M && res_in->size(1) == K && res_out->sizes() == res_in->sizes(), "residual shapes");
+    TORCH_CHECK(res_in->data_ptr() != res_out->data_ptr(), "res_out must not alias res_in");
+    CHECK_BF16(*gamma); TORCH_CHECK(gamma->numel() == K && gamma->is_contiguous(), "gamma [K]");
+    ppp = pp->data_ptr<float>();
+    pS = pp->size(0);
+    rin = bp(*res_in);
+    rout = bp(*res_out);
+    rs = res_in->stride(0);
+    g = bp(*gamma);
+  }
+  const float* pop = nullptr;
+  const float* pmp = nullptr;
+  const int* cp = nullptr;
+  int D = 0;
+  if (kind == 2) {
+    TORCH_CHECK(po && pml && ctx, "ws_pro kind 2: po, pml, ctx");
+    CHECK_F32(*po); CHECK_F32(*pml); CHECK_CONTIG(*po); CHECK_CONTIG(*pml); CHECK_I32(*ctx); CHECK_CONTIG(*ctx);
+    TORCH_CHECK(Hq > 0 && K % Hq == 0, "Hq");
+    D = K / Hq;
+    TORCH_CHECK(po->numel() >= (long)M * Hq * max_splits * D && pml->numel() >= (long)M * Hq * max_splits * 2 &&
+                ctx->numel() >= M, "decode partials / ctx too small");
+    pop = po->data_ptr<float>();
+    pmp = pml->data_ptr<float>();
+    cp = ctx->data_ptr<int>();
+  }
+  int rc = lk_wsgemm_pro((int)kind, bp(x), bp(w), M, N, K, (int)bn, S, swiglu ? 1 : 0,
+                         out.defined() ? bp(out) : nullptr, out.defined() ? out.stride(0) : 0,
+                         S > 1 ? part.data_ptr<float>() : nullptr, ppp, pS, rin, rout, rs, g, (float)eps, pop, pmp, cp,
+                         (int)Hq, D, (int)max_splits, (int)split, cur_stream());
+  CHECK_RC(rc, "ws_pro");
+  return out.defined() ? out : part;
+}
+
+// rope_kv_ over the reduce of split-K QKV slabs part [S, M, N] (as ws_linear_rope_kv's second half)
+at::Tensor splitk_rope_kv(const at::Tensor& part, const at::Tensor& positions, const at::Tensor& cos_sin, int64_t Hq,
+                          int64_t Hkv, int64_t D, const c10::optional<at::Tensor>& k_cache,
+                          const c10::optional<at::Tensor>& v_cache, const c10::optional<at::Tensor>& slots, bool neox,
+                          bool write_k_inplace) {
+  CHECK_CUDA(part); CHECK_F32(part); CHECK_CONTIG(part);
+  TORCH_CHECK(part.dim() == 3 && part.size(2) == (Hq + 2 * Hkv) * D, "part must be [S, M, (Hq + 2 Hkv) * D]");
+  const int S = part.size(0), M = part.size(1), N = part.size(2);
+  CHECK_I32(positions); CHECK_F32(cos_sin); CHECK_CONTIG(cos_sin); CHECK_CONTIG(positions);
+  TORCH_CHECK(positions.numel() == M, "positions");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D, "cos_sin must be [max_pos, D]");
+  int BS = 1;
+  if (k_cache || v_cache) {
+    TORCH_CHECK(k_cache && v_cache && slots, "k_cache, v_cache and slots go together");
+    CHECK_BF16(*k_cache); CHECK_BF16(*v_cache); CHECK_CONTIG(*k_cache); CHECK_CONTIG(*v_cache);
+    CHECK_I32(*slots); TORCH_CHECK(slots->numel() == M, "slots");
+    TORCH_CHECK(k_cache->dim() == 4 && k_cache->size(1) == Hkv && k_cache->size(3) == D, "k_cache must be [NB, Hkv, BS, D]");
+    TORCH_CHECK(v_cache->sizes() == k_cache->sizes(), "v_cache shape");
+    BS = k_cache->size(2);
+  }
+  at::Tensor qkv = at::empty({M, N}, part.options().dtype(at::kBFloat16));
+  int rc = lk_splitk_rope_kv(part.data_ptr<float>(), S, bp(qkv), qkv.stride(0), ip(positions), cos_sin.data_ptr<float>(),
+                             M, (int)Hq, (int)Hkv, (int)D, bpo(k_cache), bpo(v_cache), ipo(slots), BS, neox ? 1 : 0,
+                             write_k_inplace ? 1 : 0, cur_stream());
+  CHECK_RC(rc, "splitk_rope_kv");
+  return qkv;
+}
+
+// RMSNorm(bf16(sum of part's slabs) + residual) * w, residual updated in place (lk_splitk_rmsnorm)
+at::Tensor splitk_rmsnorm(const at::Tensor& part, at::Tensor& residual, const at::Tensor& w, double eps) {
+  CHECK_CUDA(part); CHECK_F32(part); CHECK_CONTIG(part);
+  CHECK_BF16(residual); CHECK_LASTDIM(residual); CHECK_BF16(w); check_rows16(residual, "residual");
+  TORCH_CHECK(part.dim() == 3 && part.size(1) == residual.size(0) && part.size(2) == residual.size(1), "part [S, M, H]");
+  const long M = residual.size(0);
+  const int H = residual.size(1);
+  TORCH_CHECK(w.numel() == H && w.is_contiguous(), "w [H]");
+  at::Tensor out = at::empty({M, H}, residual.options());
+  CHECK_RC(lk_splitk_rmsnorm(bp(out), bp(residual), part.data_ptr<float>(), part.size(0), bp(w), M, H, (float)eps,
+                             out.stride(0), residual.stride(0), cur_stream()), "splitk_rmsnorm");
+  return out;
+}
+
 // Prefill / encoder-regime linear (csrc/gemm.hip): epi(x [M, K] . w[N, K]^T (+ bias)).
 // epi 0 none, 1 SwiGLU (w = [Wg; Wu], out [M, N/2]), 2 bias, 3 bias+GELU(erf), 4 bias+ReLU.
 at::Tensor gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t epi,
@@ -481,7 +593,8 @@ at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at
                         int64_t split, double scale, const c10::optional<at::Tensor>& part_o,
                         const c10::optional<at::Tensor>& part_ml, const c10::optional<at::Tensor>& out_,
                         const c10::optional<at::Tensor>& k_start, const c10::optional<at::Tensor>& pp_o,
-                        const c10::optional<at::Tensor>& pp_ml, const c10::optional<at::Tensor>& tickets) {
+                        const c10::optional<at::Tensor>& pp_ml, const c10::optional<at::Tensor>& tickets,
+                        bool reduce) {
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
   CHECK_I32(block_tables); CHECK_I32(ctx_lens); CHECK_CONTIG(ctx_lens);
   TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == q.size(2), "q must be [B, Hq, D] (row-strided)");
@@ -520,7 +633,7 @@ at::Tensor paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at
                            parts ? pm.data_ptr<float>() : nullptr, B, Hq, Hkv, D, BS, (int)max_splits,
                            (int)split, (float)scale, cascade ? ip(*k_start) : nullptr,
                            cascade ? pp_o->data_ptr<float>() : nullptr, cascade ? pp_ml->data_ptr<float>() : nullptr,
-                           cur_stream(), tickets ? tickets->data_ptr<int>() : nullptr);
+                           cur_stream(), tickets ? tickets->data_ptr<int>() : nullptr, reduce ? 1 : 0);
   CHECK_RC(rc, "paged_decode");
   return out;
 }
@@ -965,8 +1078,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("kv_write", &kv_write);
   m.def("decode_splits", &decode_splits);
   m.def("decode_split_size", &decode_split_size);
-  m.def("paged_decode", &paged_decode, "", py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("max_splits"), py::arg("split"), py::arg("scale"), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("out") = py::none(), py::arg("k_start") = py::none(), py::arg("pp_o") = py::none(), py::arg("pp_ml") = py::none(), py::arg("tickets") = py::none());
+  m.def("paged_decode", &paged_decode, "", py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("max_splits"), py::arg("split"), py::arg("scale"), py::arg("part_o") = py::none(), py::arg("part_ml") = py::none(), py::arg("out") = py::none(), py::arg("k_start") = py::none(), py::arg("pp_o") = py::none(), py::arg("pp_ml") = py::none(), py::arg("tickets") = py::none(), py::arg("reduce") = true);
   m.def("prefill_rows_per_tile", &prefill_rows_per_tile);
+  m.def("ws_pro", &ws_pro, "", py::arg("x"), py::arg("w"), py::arg("swiglu"), py::arg("bn"), py::arg("splits"),
+        py::arg("kind"), py::arg("reduce") = false, py::arg("pp") = py::none(), py::arg("res_in") = py::none(),
+        py::arg("res_out") = py::none(), py::arg("gamma") = py::none(), py::arg("eps") = 0.0,
+        py::arg("po") = py::none(), py::arg("pml") = py::none(), py::arg("ctx") = py::none(), py::arg("split") = 0,
+        py::arg("max_splits") = 0, py::arg("Hq") = 0);
+  m.def("splitk_rope_kv", &splitk_rope_kv);
+  m.def("splitk_rmsnorm", &splitk_rmsnorm);
   m.def("ws_set_variant", [](int64_t M, int64_t N, int64_t K, bool swiglu, int64_t v) {
     CHECK_RC(lk_wsgemm_set_variant((int)M, (int)N, (int)K, swiglu ? 1 : 0, (int)v), "ws_set_variant");
   }, "weight-streaming GEMM kernel for this (M bucket, N, K, swiglu): 0 ring, 1 loader waves, -1 default",

@@ -35,6 +35,10 @@ int lk_skinny_gemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int
                    bf16_t* out, long ldo, float* part, hipStream_t st);
 
 void lk_wsgemm_plan(int M, int N, int K, int swiglu, int* bn_out, int* s_out);
+int lk_wsgemm_pro(int kind, bf16_t* x, const bf16_t* w, int M, int N, int K, int BN, int S, int swiglu,
+                  bf16_t* out, long ldo, float* part, const float* pp, int pS, const bf16_t* res, bf16_t* res_out,
+                  long rs, const bf16_t* gamma, float eps, const float* po, const float* pml, const int* ctx, int Hq,
+                  int D, int max_splits, int split, hipStream_t st);
 int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, int swiglu,
               bf16_t* out, long ldo, float* part, hipStream_t st);
 
@@ -146,7 +150,7 @@ int lk_paged_decode(const bf16_t* q, long qs, const bf16_t* kc, const bf16_t* vc
                     const int* block_tables, int bt_stride, const int* ctx_lens, bf16_t* out,
                     long os, float* part_o, float* part_ml, int B, int Hq, int Hkv, int D, int BS,
                     int max_splits, int split, float scale, const int* k_start, const float* pp_o,
-                    const float* pp_ml, hipStream_t st, int* tickets = nullptr);
+                    const float* pp_ml, hipStream_t st, int* tickets = nullptr, int reduce = 1);
 
 // attn_prefill.hip
 int lk_prefill_rows_per_tile(int G, int D);

@@ -70,6 +70,104 @@ struct WsTail {
   float eps = 0.f;
 };
 
+// Consumer-side prologue of the weight-streaming GEMM (kind != 0, <= 64 rows): before its K walk
+// every workgroup computes the X rows of its K slice itself and stages them from the scratch
+// rows `x` it wrote, so the launch that would have produced X disappears from the decode step
+// (its W prefetch is issued before the prologue and flies under it):
+//   kind 1: x = RMSNorm(bf16(sum of the producer's split-K slabs) + res) * gamma -- exactly the
+//           rmsnorm_kernel<_, 4, S> arithmetic (256 threads slicing the row the same way, same
+//           block_sum), so the values are bit-identical to lk_splitk_rmsnorm; workgroup 0 also
+//           writes the summed residual row(s) to res_out (a buffer other than res: the other
+//           workgroups still read res);
+//   kind 2: the flash-decoding merge of a split-K paged-decode step's partials, exactly as
+//           decode_reduce_kernel, for the rows with more than one split (the others the
+//           attention kernel wrote into x itself).
+struct WsPro {
+  int kind = 0;
+  bf16_t* x = nullptr;  // [M, K] scratch rows (row stride K): written here, then staged as X
+  const float* part = nullptr;  // 1: producer slabs [S][M][K]
+  int S = 0;
+  long slab = 0;
+  const bf16_t* res = nullptr;
+  bf16_t* res_out = nullptr;
+  long rs = 0;  // row stride of res and res_out
+  const bf16_t* gamma = nullptr;
+  float eps = 0.f;
+  const float* po = nullptr;   // 2: [(row * Hq + qh) * max_splits + s][D]
+  const float* pml = nullptr;  // 2: [(row * Hq + qh) * max_splits + s][2]
+  const int* ctx = nullptr;
+  int Hq = 0, D = 0, max_splits = 0, split = 0;
+};
+
+template <int KIND>
+LK_DEVICE void ws_prologue(const WsPro& pr, int M, int K, long kbase, int ks) {
+  if constexpr (KIND == 1) {
+    __shared__ float red[4];
+    const int nvec = K >> 3;
+    for (int m = 0; m < M; ++m) {
+      float v[4][8];
+      float ss = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = threadIdx.x + i * 256;
+        if (c < nvec) {
+          const float* pp = pr.part + (long)m * K + c * 8;
+          floatx4 a = *reinterpret_cast<const floatx4*>(pp), b = *reinterpret_cast<const floatx4*>(pp + 4);
+          for (int q = 1; q < pr.S; ++q) {
+            a += *reinterpret_cast<const floatx4*>(pp + q * pr.slab);
+            b += *reinterpret_cast<const floatx4*>(pp + q * pr.slab + 4);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[i][j] = bf2f(f2bf(a[j]));
+            v[i][j + 4] = bf2f(f2bf(b[j]));
+          }
+          float r[8];
+          load8(pr.res + (long)m * pr.rs + c * 8, r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[i][j] = bf2f(f2bf(v[i][j] + r[j]));
+          if (blockIdx.x == 0) store8(pr.res_out + (long)m * pr.rs + c * 8, v[i]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+        }
+      }
+      ss = block_sum<4>(ss, red);
+      const float inv = rsqrtf(ss / (float)K + pr.eps);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = threadIdx.x + i * 256;
+        if (c < nvec && c * 8 >= kbase && c * 8 < kbase + ks) {
+          float g[8], y[8];
+          load8(pr.gamma + c * 8, g);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) y[j] = bf2f(f2bf(v[i][j] * inv)) * g[j];
+          store8(pr.x + (long)m * K + c * 8, y);
+        }
+      }
+    }
+  } else if constexpr (KIND == 2) {
+    for (int m = 0; m < M; ++m) {
+      const int nsplit = max(0, min((pr.ctx[m] + pr.split - 1) / pr.split, pr.max_splits));
+      if (nsplit <= 1) continue;  // (uniform) the attention kernel wrote this row into x
+      for (int e = threadIdx.x; e < ks; e += 256) {
+        const long col = kbase + e;
+        const int qh = (int)(col / pr.D), d = (int)(col - (long)qh * pr.D);
+        const long base = ((long)m * pr.Hq + qh) * pr.max_splits;
+        float Mx = -INFINITY;
+        for (int q = 0; q < nsplit; ++q) Mx = fmaxf(Mx, pr.pml[(base + q) * 2]);
+        if (Mx == -INFINITY) Mx = 0.f;
+        float den = 0.f, num = 0.f;
+        for (int q = 0; q < nsplit; ++q) {
+          const float f = exp2f(pr.pml[(base + q) * 2] - Mx);
+          den += f * pr.pml[(base + q) * 2 + 1];
+          num += f * pr.po[(base + q) * pr.D + d];
+        }
+        pr.x[(long)m * K + col] = f2bf(den > 0.f ? num / den : 0.f);
+      }
+    }
+  }
+}
+
 // 8 consecutive columns of one row: the S slabs summed in slab order, rounded to bf16 (the values
 // the unfused reduce stores); partials read past L1 / L2 (other workgroups wrote them through)
 LK_DEVICE void tail_ld8(__amdgpu_buffer_rsrc_t prs, int S, long slab, long off, float* f) {
@@ -436,12 +534,19 @@ LK_DEVICE void wait_ahead(int ahead) {  // vmcnt(ahead * L), ahead in [0, NS-2]
   }
 }
 
-template <int MT, int BN, bool SWIGLU, bool TAIL>
+// (PRO: a WsPro prologue computes X first -- the LDS ring leaves room for its static scratch)
+constexpr int ws_stages_pro(int MT, int BN, int PRO) {
+  const int sb = (16 * MT + BN) * 128;
+  const int n = (163840 - (PRO ? 1024 : 0)) / sb;
+  return n > 8 ? 8 : (n < 3 ? 3 : n);
+}
+
+template <int MT, int BN, bool SWIGLU, bool TAIL, int PRO = 0>
 __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict__ X, long ldx,
                                                         const bf16_t* __restrict__ W, int M, int K, int ks,
                                                         int n_tiles, int swiglu_I, bf16_t* __restrict__ out,
                                                         long ldo, float* __restrict__ part, long part_ld,
-                                                        long n_rows, int rot_mul, WsTail tl) {
+                                                        long n_rows, int rot_mul, WsTail tl, WsPro pr) {
   // n_rows: valid W rows (the last column tile may be partial: kNN over a corpus of
   // any size); loads clamp to the last row, stores are masked
   constexpr int ROWS = 16 * MT;          // padded M
@@ -450,7 +555,7 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
   constexpr int XB = ROWS * 128;         // X stage bytes
   constexpr int WB = BN * 128;           // W stage bytes
   constexpr int SB = XB + WB;            // stage bytes
-  constexpr int NS = ws_stages(MT, BN);  // ring depth: as many stages as 160 KB of LDS holds
+  constexpr int NS = ws_stages_pro(MT, BN, PRO);  // ring depth: as many stages as 160 KB of LDS holds
   constexpr int LX = ROWS / 32;          // X glds per wave per stage (8 rows each, 4 waves)
   constexpr int LW = BN / 32;            // W glds per wave per stage
   constexpr int L = LX + LW;
@@ -488,17 +593,25 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
     const int row = (w * LW + i) * 8 + lrow;
     wsrc[i] = W + min(wrow(row), n_rows - 1) * K + kbase + ((lch ^ wsz(row)) * 8);
   }
-  auto issue = [&](int st) {
+  auto issue_x = [&](int st) {
     unsigned char* base = smem + (st % NS) * SB;
     const int k = (st + rot < nst ? st + rot : st + rot - nst) * 64;
 #pragma unroll
     for (int i = 0; i < LX; ++i)
       __builtin_amdgcn_global_load_lds((gbl_void_ptr)(xsrc[i] + k),
                                        (lds_void_ptr)(base + (w * LX + i) * 8 * 128), 16, 0, 0);
+  };
+  auto issue_w = [&](int st) {
+    unsigned char* base = smem + (st % NS) * SB;
+    const int k = (st + rot < nst ? st + rot : st + rot - nst) * 64;
 #pragma unroll
     for (int i = 0; i < LW; ++i)
       __builtin_amdgcn_global_load_lds((gbl_void_ptr)(wsrc[i] + k),
                                        (lds_void_ptr)(base + XB + (w * LW + i) * 8 * 128), 16, 0, 2);
+  };
+  auto issue = [&](int st) {
+    issue_x(st);
+    issue_w(st);
   };
 
   floatx4 acc[MTW][NT];
@@ -535,9 +648,25 @@ __global__ __launch_bounds__(256, 1) void wsgemm_kernel(const bf16_t* __restrict
     }
   };
 
+  if constexpr (PRO != 0) {
+    // W of the first stages streams in while the workgroup computes its X slice; then X's
+    // first stages come from the rows just written (every wave waits for its own DMAs, the
+    // loop's barrier for everyone's)
 #pragma unroll
-  for (int p = 0; p < NS - 1; ++p)
-    if (p < nst) issue(p);
+    for (int p = 0; p < NS - 1; ++p)
+      if (p < nst) issue_w(p);
+    ws_prologue<PRO>(pr, M, K, kbase, ks);
+    wait_vmcnt<0>();
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+      if (p < nst) issue_x(p);
+    wait_vmcnt<0>();
+  } else {
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+      if (p < nst) issue(p);
+  }
   for (int st = 0; st < nst; ++st) {
     // stage st landed (this wave's DMAs); later stages may stay in flight
     wait_ahead<L, NS>(min(NS - 2, nst - 1 - st));
@@ -835,7 +964,20 @@ void launch_ws(const bf16_t* x, long ldx, const bf16_t* w, int M, int K, int ks,
   // kNN scores (n_rows given: a corpus, not a weight) walk K in one order in every tile, so
   // equal corpus rows score bit-identically and ties keep the stable id order
   const int rot_mul = n_rows < (1L << 40) ? 0 : g_ws_rot_mul >= 0 ? g_ws_rot_mul : (S == 1 ? 5 : 0);
-  kern<<<n_tiles * S, 256, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows, rot_mul, tl);
+  kern<<<n_tiles * S, 256, lds, st>>>(x, ldx, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, n_rows, rot_mul, tl,
+                                      WsPro{});
+}
+
+// the prologue instantiations (one LDS ring, 16-row tiles: M <= 64)
+template <int BN, bool SWIGLU, int PRO>
+void launch_ws_pro(const bf16_t* x, const bf16_t* w, int M, int K, int ks, int S, int n_tiles, int I, bf16_t* out,
+                   long ldo, float* part, long part_ld, hipStream_t st, const WsPro& pr) {
+  constexpr int MT = 4;
+  constexpr size_t lds = (size_t)ws_stages_pro(MT, BN, PRO) * (16 * MT * 128 + BN * 128);
+  LK_SET_MAX_LDS((wsgemm_kernel<MT, BN, SWIGLU, false, PRO>), (int)lds);
+  const int rot_mul = g_ws_rot_mul >= 0 ? g_ws_rot_mul : (S == 1 ? 5 : 0);
+  wsgemm_kernel<MT, BN, SWIGLU, false, PRO><<<n_tiles * S, 256, lds, st>>>(
+      x, K, w, M, K, ks, n_tiles, I, out, ldo, part, part_ld, 1L << 40, rot_mul, WsTail{}, pr);
 }
 
 template <int MT, int BN, bool SWIGLU>
@@ -1003,6 +1145,68 @@ int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, i
 }
 
 void lk_wsgemm_set_rot(int rot_mul) { g_ws_rot_mul = rot_mul < 0 ? -1 : rot_mul; }
+
+// Weight-streaming GEMM with a consumer-side X prologue (WsPro, one LDS ring, M <= 64): kind 1 =
+// residual add + RMSNorm of the producer's split-K slabs, kind 2 = flash-decoding merge of a
+// paged-decode step's split partials.  x: [M, K] bf16 rows (kind 1: written; kind 2: the
+// attention output, merged rows written).  S > 1: partial slabs into part, and with out also the
+// reduce (SwiGLU) into out; S == 1: out directly.
+int lk_wsgemm_pro(int kind, bf16_t* x, const bf16_t* w, int M, int N, int K, int BN, int S, int swiglu,
+                  bf16_t* out, long ldo, float* part, const float* pp, int pS, const bf16_t* res, bf16_t* res_out,
+                  long rs, const bf16_t* gamma, float eps, const float* po, const float* pml, const int* ctx, int Hq,
+                  int D, int max_splits, int split, hipStream_t st) {
+  if (M < 1 || M > 64 || S < 1 || K % (S * 64) || !x || (BN != 64 && BN != 128 && (BN != 96 || swiglu))) return -1;
+  const int per = swiglu ? BN / 2 : BN;
+  if (swiglu ? (N % 2 || (N / 2) % per) : N % BN) return -1;
+  if ((S > 1 && !part) || (S == 1 && !out)) return -1;
+  WsPro pr;
+  pr.kind = kind;
+  pr.x = x;
+  if (kind == 1) {
+    if (K % 8 || K > 8192 || !pp || pS < 1 || !res || !res_out || res == res_out || !gamma || rs % 8) return -1;
+    pr.part = pp;
+    pr.S = pS;
+    pr.slab = (long)M * K;
+    pr.res = res;
+    pr.res_out = res_out;
+    pr.rs = rs;
+    pr.gamma = gamma;
+    pr.eps = eps;
+  } else if (kind == 2) {
+    if (!po || !pml || !ctx || D <= 0 || Hq * D != K || max_splits < 1 || split < 1) return -1;
+    pr.po = po;
+    pr.pml = pml;
+    pr.ctx = ctx;
+    pr.Hq = Hq;
+    pr.D = D;
+    pr.max_splits = max_splits;
+    pr.split = split;
+  } else {
+    return -1;
+  }
+  const int I = swiglu ? N / 2 : 0;
+  const int n_tiles = (swiglu ? I : N) / per;
+  const int ks = K / S;
+  float* p = S > 1 ? part : nullptr;
+#define LK_PRO(bn, sw, kd) \
+  if (BN == bn && (swiglu != 0) == sw && kind == kd) launch_ws_pro<bn, sw, kd>(x, w, M, K, ks, S, n_tiles, I, out, ldo, p, N, st, pr); else
+  LK_PRO(64, false, 1) LK_PRO(96, false, 1) LK_PRO(128, false, 1) LK_PRO(64, true, 1) LK_PRO(128, true, 1)
+  LK_PRO(64, false, 2) LK_PRO(96, false, 2) LK_PRO(128, false, 2) return -2;
+#undef LK_PRO
+  LK_CHECK_LAUNCH();
+  if (S > 1 && out) {
+    const int n_out = swiglu ? I : N;
+    const long work = (long)M * (n_out / 4);
+    int grid = (int)((work + 255) / 256);
+    if (grid > 2048) grid = 2048;
+    if (swiglu)
+      splitk_reduce_kernel<true><<<grid, 256, 0, st>>>(part, S, M, N, n_out, I, out, ldo);
+    else
+      splitk_reduce_kernel<false><<<grid, 256, 0, st>>>(part, S, M, N, n_out, 0, out, ldo);
+    LK_CHECK_LAUNCH();
+  }
+  return 0;
+}
 
 int lk_wsgemm_part(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, float* part,
                    hipStream_t st) {

@@ -181,6 +181,8 @@ class LlamaModel(nn.Module):
         L0 = self.layers[0]
         if self.folded and not self.tp.enabled and ops.prefill_chain_ok(res, L0.qkv, L0.o, L0.gate_up, L0.down):
             return self._forward_chain(res, meta, kv_caches)
+        if self._xpro_ok(res, meta):
+            return self._forward_decode_xpro(res, meta, kv_caches)
         x = ops.rmsnorm(res, self.layers[0].input_norm, cfg.norm_eps)
         attn_out = None
         n = len(self.layers)
@@ -207,6 +209,83 @@ class LlamaModel(nn.Module):
             x = self.tp.all_reduce_rmsnorm(ops.linear(attn_out, L.o), res, L.post_norm, cfg.norm_eps)
             a = ops.linear_swiglu(x, L.gate_up)
             x = self.tp.all_reduce_rmsnorm(ops.linear(a, L.down), res, nxt, cfg.norm_eps)
+        if meta.logits_idx is not None:
+            x = ops.gather_rows(x, meta.logits_idx)
+        return x
+
+    def _xpro_plans(self, M: int):
+        """(qkv, o, gate_up, down) weight-streaming plans of a decode step of M rows when every
+        projection runs split-K where the consumer-side prologues need it, else None."""
+        cache = self.__dict__.setdefault("_xpro_cache", {})
+        if M in cache:
+            return cache[M]
+        L0 = self.layers[0]
+        H = L0.qkv.shape[1]
+        I = L0.down.shape[1]
+        x = torch.empty(M, H, dtype=torch.bfloat16, device=L0.qkv.device)
+        xi = torch.empty(M, I, dtype=torch.bfloat16, device=L0.qkv.device)
+        plans = None
+        kinds = (ops._decode_gemm_kind(x, L0.qkv, False), ops._decode_gemm_kind(x, L0.o, False),
+                 ops._decode_gemm_kind(x, L0.gate_up, True), ops._decode_gemm_kind(xi, L0.down, False))
+        if all(k == "ws" for k in kinds) and L0.o.shape[1] == self.hq * self.D:
+            p = (ops.ws_plan(M, *L0.qkv.shape), ops.ws_plan(M, *L0.o.shape), ops.ws_plan(M, *L0.gate_up.shape, True),
+                 ops.ws_plan(M, *L0.down.shape))
+            if p[0][1] in (2, 4, 8) and p[1][1] > 1 and p[3][1] > 1 and (L0.o.shape[1] // p[1][1]) % self.D == 0:
+                plans = p
+        cache[M] = plans
+        return plans
+
+    def _xpro_ok(self, res: torch.Tensor, meta: AttnMeta) -> bool:
+        M = res.shape[0]
+        return (ops.XPRO and res.is_cuda and not self.tp.enabled and self.cp_group is None
+                and M <= ops.XPRO_MAX_M and meta.num_prefill_tokens == 0 and meta.num_decode == M
+                and meta.shared_len is None and meta.block_tables_d is not None and ops.DECODE_FUSED_REDUCE != 2
+                and self._xpro_plans(M) is not None)
+
+    def _forward_decode_xpro(self, res: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
+        """Decode step of few rows (batch 1) with the consumer-side GEMM prologues
+        (``ops.ws_pro``): the O projection merges the paged-decode split partials itself, gate_up
+        and the next layer's QKV add the previous projection's split-K slabs to the residual and
+        RMSNorm them themselves -- no decode_reduce and no rmsnorm launch per layer.  The residual
+        stream alternates between two buffers (a prologue's workgroup 0 writes the new residual
+        while the others still read the old).  Bit-identical to the unfused step."""
+        cfg = self.cfg
+        eps = cfg.norm_eps
+        M = res.shape[0]
+        hq, hkv, D = self.hq, self.hkv, self.D
+        p_qkv, p_o, p_gu, p_dn = self._xpro_plans(M)
+        bufs = (res, torch.empty_like(res))
+        cur = 0
+        po, pml = meta.part_o, meta.part_ml
+        if po is None or po.shape[2] != meta.max_splits:
+            po = torch.empty(M, hq, meta.max_splits, D, dtype=torch.float32, device=res.device)
+            pml = torch.empty(M, hq, meta.max_splits, 2, dtype=torch.float32, device=res.device)
+        pp = None
+        n = len(self.layers)
+        for li, L in enumerate(self.layers):
+            kc, vc = kv_caches[li]
+            if pp is None:
+                x = ops.rmsnorm(res, L.input_norm, eps)
+                qp = ops.ws_pro(x, L.qkv, p_qkv, 0)
+            else:
+                x = torch.empty_like(res)
+                qp = ops.ws_pro(x, L.qkv, p_qkv, 1, pp=pp, res_in=bufs[cur], res_out=bufs[1 - cur],
+                                gamma=L.input_norm, eps=eps)
+                cur = 1 - cur
+            qkv = ops.splitk_rope_kv(qp, meta.positions, self.cos_sin, hq, hkv, D, kc, vc, meta.slots, self.rope_neox)
+            attn = torch.empty(M, hq * D, dtype=res.dtype, device=res.device)
+            ops.paged_decode(qkv[:, : hq * D].view(M, hq, D), kc, vc, meta.block_tables_d, meta.ctx_lens_d, self.scale,
+                             meta.max_splits, po, pml, out=attn.view(M, hq, D), split=meta.decode_split, reduce=False)
+            op = ops.ws_pro(attn, L.o, p_o, 2, po=po, pml=pml, ctx=meta.ctx_lens_d, split=meta.decode_split,
+                            max_splits=meta.max_splits, Hq=hq)
+            x2 = torch.empty_like(res)
+            a = ops.ws_pro(x2, L.gate_up, p_gu, 1, swiglu=True, reduce=True, pp=op, res_in=bufs[cur],
+                           res_out=bufs[1 - cur], gamma=L.post_norm, eps=eps)
+            cur = 1 - cur
+            pp = ops.ws_pro(a, L.down, p_dn, 0)
+        x = ops.splitk_rmsnorm(pp, bufs[cur], self.final_norm, eps)
+        if cur != 0:  # the residual stream ends where the unfused step leaves it
+            res.copy_(bufs[cur])
         if meta.logits_idx is not None:
             x = ops.gather_rows(x, meta.logits_idx)
         return x

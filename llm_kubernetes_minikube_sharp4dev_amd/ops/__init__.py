@@ -137,7 +137,8 @@ def decode_tickets(device, n: int):
 
 
 def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_splits: Optional[int] = None,
-                 part_o=None, part_ml=None, out=None, split: Optional[int] = None, k_start=None, prefix=None):
+                 part_o=None, part_ml=None, out=None, split: Optional[int] = None, k_start=None, prefix=None,
+                 reduce: bool = True):
     """q [B, Hq, D] -> [B, Hq, D].  ``split`` keys per workgroup (default from
     :func:`decode_split_size`), ``max_splits`` = splits covering the block-table width —
     both static, so the launch is hipGraph-capturable.
@@ -145,7 +146,9 @@ def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_
     Cascade: ``k_start`` (device int32 [1]) keys are a prefix shared by every row whose
     attention was computed once for the batch by :func:`flash_prefill` in partial mode
     into ``prefix`` = (o [B, Hq, D], ml [B, Hq, 2]); this call attends the rest and
-    merges (the CPU reference attends everything directly)."""
+    merges (the CPU reference attends everything directly).  ``reduce=False`` (GPU, no
+    tickets): rows with more than one split keep their partials in ``part_o`` / ``part_ml`` for
+    the consumer to merge (:func:`ws_pro` kind 2)."""
     if use_hip(q):
         BS = k_cache.shape[2]
         if split is None:
@@ -154,10 +157,10 @@ def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_
             max_splits = decode_splits(block_tables.shape[1] * BS, split)
         pp_o, pp_ml = prefix if prefix is not None else (None, None)
         bh = q.shape[0] * k_cache.shape[1]
-        fused = DECODE_FUSED_REDUCE == 2 or (DECODE_FUSED_REDUCE == 1 and bh >= 512)
+        fused = reduce and (DECODE_FUSED_REDUCE == 2 or (DECODE_FUSED_REDUCE == 1 and bh >= 512))
         tickets = decode_tickets(q.device, bh) if fused else None
         return lib().paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, max_splits, split, scale,
-                                  part_o, part_ml, out, k_start, pp_o, pp_ml, tickets)
+                                  part_o, part_ml, out, k_start, pp_o, pp_ml, tickets, reduce)
     y = ref.paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
     if out is not None:
         out.copy_(y)
@@ -829,6 +832,43 @@ def ws_tickets(device):
     if t is None:
         t = _WS_TICKETS[key] = torch.zeros(4096, dtype=torch.int32, device=device)
     return t
+
+
+# Consumer-side prologues in the decode step (csrc/skinny_gemm.hip WsPro, rows <= XPRO_MAX_M, one
+# GPU without TP): the O projection merges the paged-decode split partials itself (no
+# decode_reduce launch) and gate_up / the next layer's QKV compute residual add + RMSNorm of the
+# previous projection's split-K slabs themselves (no rmsnorm launch) -- three launches fewer per
+# layer, bit-identical values (models/llama.py _forward_decode_xpro).  LK_DECODE_XPRO=0: off.
+XPRO = os.environ.get("LK_DECODE_XPRO", "1") != "0"
+XPRO_MAX_M = int(os.environ.get("LK_DECODE_XPRO_MAX_M", "16"))
+_PLAN_CACHE: dict = {}
+
+
+def ws_plan(M: int, N: int, K: int, swiglu: bool = False) -> tuple:
+    """(BN, S) of the weight-streaming GEMM for this shape (lk_wsgemm_plan)."""
+    key = (M, N, K, swiglu)
+    p = _PLAN_CACHE.get(key)
+    if p is None:
+        p = _PLAN_CACHE[key] = tuple(lib().ws_plan(M, N, K, swiglu))
+    return p
+
+
+def ws_pro(x, w, plan, kind: int, swiglu: bool = False, reduce: bool = False, **kw):
+    """Weight-streaming GEMM with a consumer-side X prologue (``kind`` 1: x = RMSNorm(bf16(sum of
+    ``pp``) + ``res_in``) * ``gamma``, ``res_out`` = the summed residual; 2: x = the paged-decode
+    output with its split partials ``po`` / ``pml`` merged; 0: plain x).  Returns the f32 partial
+    slabs [S, M, N] (S > 1 and not ``reduce``) or the bf16 / SwiGLU output."""
+    return lib().ws_pro(x, w, swiglu, plan[0], plan[1], kind, reduce, **kw)
+
+
+def splitk_rope_kv(part, positions, cos_sin, Hq: int, Hkv: int, D: int, k_cache, v_cache, slots, neox: bool,
+                   write_k_inplace: bool = False):
+    return lib().splitk_rope_kv(part, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache, slots, neox, write_k_inplace)
+
+
+def splitk_rmsnorm(part, residual, w, eps: float):
+    """RMSNorm(bf16(sum of part's slabs) + residual) * w; residual updated in place."""
+    return lib().splitk_rmsnorm(part, residual, w, eps)
 
 
 def linear_add_rmsnorm(x, w, residual, norm_w, eps: float):

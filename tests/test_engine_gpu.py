@@ -405,3 +405,33 @@ def test_query_encoder_graphs_equal_eager():
     ref = [eager.embed_cpu([t]) for t in texts]
     for i in range(3):
         assert all(torch.equal(a, b) for a, b in zip(res[i], ref)), i
+
+
+def test_decode_xpro_tokens_equal(monkeypatch):
+    """Batch-1 / few-row decode steps with the consumer-side GEMM prologues (O merges the
+    attention splits, gate_up / QKV add + RMSNorm the previous projection's split-K slabs:
+    models/llama.py _forward_decode_xpro) emit exactly the tokens of the unfused step, eager and
+    in the decode hipGraphs, on a 2-layer Llama-3-8B-shaped model (the real projection shapes)."""
+    from llm_kubernetes_minikube_sharp4dev_amd import ops
+    from llm_kubernetes_minikube_sharp4dev_amd.models import llama as llama_mod
+
+    m = build_decoder("llama-3-8b", device=DEV, num_layers=2)
+    used = []
+    real = llama_mod.LlamaModel._forward_decode_xpro
+
+    def spy(self, *a, **kw):
+        used.append(a[0].shape[0])
+        return real(self, *a, **kw)
+
+    monkeypatch.setattr(llama_mod.LlamaModel, "_forward_decode_xpro", spy)
+    prompts = [list(range(100, 160)), [7, 8, 9, 10, 11], list(range(1000, 1400, 3))]
+    for graphs in (False, True):
+        outs = {}
+        for on in (True, False):
+            monkeypatch.setattr(ops, "XPRO", on)
+            used.clear()
+            eng = LLMEngine(m, None, block_size=16, max_model_len=2048, max_num_seqs=4, eos_ids=set(), num_blocks=512,
+                            use_graphs=graphs)
+            outs[on] = [[s.output_ids for s in eng.generate([p], SamplingParams.greedy(40))][0] for p in prompts]
+            assert bool(used) == on
+        assert outs[True] == outs[False], graphs

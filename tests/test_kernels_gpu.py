@@ -1193,3 +1193,64 @@ def test_knn_topk_config4_scale(hip, fused):
     assert i[0, :3].tolist() == list(dup), i[0].tolist()
     assert float(s[0, 0]) == float(s[0, 1]) == float(s[0, 2])
     assert int(i[1, 0]) == N - 1 and int(i[2, 0]) == 2_500_000
+
+
+# ---- consumer-side prologues of the weight-streaming GEMM (decode steps of few rows) ----
+@pytest.mark.parametrize("M", [1, 4, 16])
+@pytest.mark.parametrize("shape", ["qkv", "gate_up"])
+def test_ws_pro_norm_matches_unfused(hip, M, shape):
+    """ws_pro kind 1 (residual add + RMSNorm of the producer's split-K slabs computed by the GEMM's
+    own workgroups) == splitk_rmsnorm followed by the same GEMM, bit for bit: the normed rows, the
+    new residual (written by workgroup 0 into another buffer) and the GEMM output."""
+    H, eps = 4096, 1e-5
+    N, swiglu = (6144, False) if shape == "qkv" else (28672, True)
+    torch.manual_seed(M + N)
+    pp = torch.randn(4, M, H, device=DEV) * 0.5
+    res = torch.randn(M, H, device=DEV, dtype=torch.bfloat16)
+    g = (torch.rand(H, device=DEV) + 0.5).to(torch.bfloat16)
+    w = torch.randn(N, H, device=DEV, dtype=torch.bfloat16) * 0.02
+    bn, S = hip.ws_plan(M, N, H, swiglu)
+    hip.ws_set_variant(M, N, H, swiglu, 0)
+    try:
+        res_ref = res.clone()
+        x_ref = hip.splitk_rmsnorm(pp, res_ref, g, eps)
+        res_in, res_out, x = res.clone(), torch.full_like(res, 3.0), torch.empty_like(res)
+        if swiglu:
+            want = hip.ws_linear(x_ref, w, True, bn, S)
+            got = hip.ws_pro(x, w, True, bn, S, 1, True, pp, res_in, res_out, g, eps)
+        else:
+            want = hip.ws_pro(x_ref, w, False, bn, S, 0)
+            got = hip.ws_pro(x, w, False, bn, S, 1, False, pp, res_in, res_out, g, eps)
+        torch.cuda.synchronize()
+        assert torch.equal(x, x_ref) and torch.equal(res_out, res_ref) and torch.equal(res_in, res)
+        assert torch.equal(got, want), (got.float() - want.float()).abs().max()
+    finally:
+        hip.ws_set_variant(M, N, H, swiglu, -1)
+
+
+@pytest.mark.parametrize("M", [1, 3, 16])
+def test_ws_pro_merge_matches_decode_reduce(hip, M):
+    """ws_pro kind 2: the O projection's workgroups merge the split-K paged-decode partials of
+    their K slice (paged_decode(reduce=False): no decode_reduce launch) -- the attention rows
+    equal the reduce kernel's bit for bit (one-split rows written by the attention kernel itself)
+    and the O partial slabs equal the plain GEMM's over the reduced rows."""
+    Hkv, G, D, BS = 8, 4, 128, 16
+    Hq = Hkv * G
+    ctx = ([1, 700, 2100, 129, 5, 1000, 64, 3000, 17, 256, 900, 1500, 33, 2, 511, 800])[:M]
+    kc, vc, bt = _paged_setup(M, ctx, Hkv, D, BS, seed=21)
+    q = torch.randn(M, Hq, D, device=DEV, dtype=torch.bfloat16)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    split = 128
+    ms = ops.decode_splits(bt.shape[1] * BS, split)
+    w = torch.randn(4096, Hq * D, device=DEV, dtype=torch.bfloat16) * 0.02
+    bn, S = hip.ws_plan(M, 4096, Hq * D, False)
+    po = torch.empty(M, Hq, ms, D, device=DEV)
+    pml = torch.empty(M, Hq, ms, 2, device=DEV)
+    want_rows = hip.paged_decode(q, kc, vc, bt, cl, ms, split, 0.088, None, None, None).view(M, Hq * D)
+    rows = torch.full((M, Hq * D), 5.0, device=DEV, dtype=torch.bfloat16)
+    hip.paged_decode(q, kc, vc, bt, cl, ms, split, 0.088, po, pml, rows.view(M, Hq, D), None, None, None, None, False)
+    got = hip.ws_pro(rows, w, False, bn, S, 2, False, None, None, None, None, 0.0, po, pml, cl, split, ms, Hq)
+    want = hip.ws_pro(want_rows.contiguous(), w, False, bn, S, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(rows, want_rows)
+    assert torch.equal(got, want)
