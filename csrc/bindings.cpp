@@ -382,6 +382,63 @@ at::Tensor splitk_rmsnorm(const at::Tensor& part, at::Tensor& residual, const at
   return out;
 }
 
+// Decode GEMV for M <= 2 rows (csrc/gemv_decode.hip).  mode 0: returns x.w^T; 1: res += x.w^T in
+// place (returns res); 2: SwiGLU over w = [Wg; Wu] (returns [M, N/2]); 3: RoPE + paged-KV write of a
+// packed QKV projection (returns the qkv rows).  gamma: RMSNorm(x) * gamma is the GEMV's input.
+at::Tensor gemv_decode(int64_t mode, const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& gamma,
+                       double eps, const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& positions,
+                       const c10::optional<at::Tensor>& cos_sin, int64_t Hq, int64_t Hkv, int64_t D,
+                       const c10::optional<at::Tensor>& k_cache, const c10::optional<at::Tensor>& v_cache,
+                       const c10::optional<at::Tensor>& slots, bool neox) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_LASTDIM(x); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "gemv_decode: x [M,K], w [N,K]");
+  check_rows16(x, "x"); check_rows16(w, "w");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(lk_gemv_supported(M, N, K, (int)mode), "gemv_decode: unsupported shape M", M, " N", N, " K", K);
+  if (gamma) { CHECK_BF16(*gamma); TORCH_CHECK(gamma->numel() == K && gamma->is_contiguous(), "gamma [K]"); }
+  at::Tensor out;
+  bf16_t* rp = nullptr;
+  long ldr = 0;
+  const int *pos = nullptr, *sl = nullptr;
+  const float* cs = nullptr;
+  bf16_t *kc = nullptr, *vc = nullptr;
+  int BS = 0;
+  if (mode == 0) {
+    out = at::empty({M, N}, x.options());
+  } else if (mode == 1) {
+    TORCH_CHECK(res.has_value(), "gemv_decode mode 1: res");
+    CHECK_BF16(*res); CHECK_LASTDIM(*res);
+    TORCH_CHECK(res->size(0) == M && res->size(1) == N && res->stride(0) % 2 == 0, "res [M, N]");
+    out = *res;
+    rp = bp(*res);
+    ldr = res->stride(0);
+  } else if (mode == 2) {
+    out = at::empty({M, N / 2}, x.options());
+  } else if (mode == 3) {
+    TORCH_CHECK(positions && cos_sin && slots, "gemv_decode mode 3: positions, cos_sin, slots");
+    CHECK_I32(*positions); CHECK_I32(*slots); CHECK_F32(*cos_sin); CHECK_CONTIG(*cos_sin);
+    TORCH_CHECK(positions->numel() >= M && slots->numel() >= M, "positions / slots: one per row");
+    TORCH_CHECK(cos_sin->dim() == 2 && cos_sin->size(1) == D, "cos_sin [P, D]");
+    TORCH_CHECK(N == (Hq + 2 * Hkv) * D, "qkv rows = (Hq + 2 Hkv) D");
+    out = at::empty({M, N}, x.options());
+    pos = ip(*positions); sl = ip(*slots); cs = cos_sin->data_ptr<float>();
+    if (k_cache) {
+      TORCH_CHECK(v_cache.has_value(), "k_cache without v_cache");
+      CHECK_BF16(*k_cache); CHECK_BF16(*v_cache); CHECK_CONTIG(*k_cache); CHECK_CONTIG(*v_cache);
+      TORCH_CHECK(k_cache->dim() == 4 && k_cache->size(1) == Hkv && k_cache->size(3) == D &&
+                  v_cache->sizes() == k_cache->sizes(), "cache [blocks, Hkv, BS, D]");
+      kc = bp(*k_cache); vc = bp(*v_cache); BS = k_cache->size(2);
+    }
+  } else {
+    TORCH_CHECK(false, "gemv_decode: mode 0..3");
+  }
+  CHECK_RC(lk_gemv_decode((int)mode, bp(x), x.stride(0), bpo(gamma), (float)eps, bp(w), M, N, K,
+                          mode == 1 ? nullptr : bp(out), mode == 1 ? 0 : out.stride(0), rp, ldr, pos, cs, (int)Hq,
+                          (int)Hkv, (int)D, kc, vc, sl, BS, neox ? 1 : 0, cur_stream()),
+           "gemv_decode");
+  return out;
+}
+
 // Prefill / encoder-regime linear (csrc/gemm.hip): epi(x [M, K] . w[N, K]^T (+ bias)).
 // epi 0 none, 1 SwiGLU (w = [Wg; Wu], out [M, N/2]), 2 bias, 3 bias+GELU(erf), 4 bias+ReLU.
 at::Tensor gemm(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t epi,
@@ -1087,6 +1144,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("max_splits") = 0, py::arg("Hq") = 0);
   m.def("splitk_rope_kv", &splitk_rope_kv);
   m.def("splitk_rmsnorm", &splitk_rmsnorm);
+  m.def("gemv_decode", &gemv_decode, "", py::arg("mode"), py::arg("x"), py::arg("w"), py::arg("gamma") = py::none(),
+        py::arg("eps") = 1e-5, py::arg("res") = py::none(), py::arg("positions") = py::none(),
+        py::arg("cos_sin") = py::none(), py::arg("Hq") = 0, py::arg("Hkv") = 0, py::arg("D") = 0,
+        py::arg("k_cache") = py::none(), py::arg("v_cache") = py::none(), py::arg("slots") = py::none(),
+        py::arg("neox") = true);
+  m.def("gemv_supported", [](int64_t M, int64_t N, int64_t K, int64_t mode) {
+    return lk_gemv_supported((int)M, (int)N, (int)K, (int)mode) != 0;
+  });
+  m.def("gemv_set_wgs", [](int64_t n) { lk_gemv_set_wgs((int)n); });
   m.def("ws_set_variant", [](int64_t M, int64_t N, int64_t K, bool swiglu, int64_t v) {
     CHECK_RC(lk_wsgemm_set_variant((int)M, (int)N, (int)K, swiglu ? 1 : 0, (int)v), "ws_set_variant");
   }, "weight-streaming GEMM kernel for this (M bucket, N, K, swiglu): 0 ring, 1 loader waves, -1 default",

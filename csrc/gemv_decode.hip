@@ -1,0 +1,320 @@
+// Decode-step GEMV for one or two rows (batch-1 / batch-2 decode), with the neighbouring
+// elementwise work of a Llama block folded into its prologue and epilogue.
+//
+// At M <= 2 a projection is a pure weight stream (16 GB per Llama-3-8B step), so the MFMA tile
+// machinery of the weight-streaming GEMM (skinny_gemm.hip: 16-row padded tiles, split-K slabs
+// reduced by a second kernel) buys nothing, while the kernels around it (split-K reduce,
+// residual add + RMSNorm, RoPE + KV write) each cost a dependent ~5 us launch.  Here:
+//   * one wave owns a PAIR of W rows at a time and splits K over its 64 lanes in 16-B chunks
+//     (lane l: chunks l, l + 64, ...: every wave load is one contiguous 1-KB segment of a row),
+//     U chunks of both rows in flight per lane; fp32 FMAs, 64-lane butterfly at the end -- no
+//     split-K, no partial slabs;
+//   * X (the M input rows) is staged once per workgroup in LDS; the NORM prologue computes
+//     RMSNorm(res) * gamma there itself (the rmsnorm kernel's exact arithmetic), so the
+//     producer of res never launches a norm;
+//   * epilogues on the pair's two dot products: 0 plain bf16 out, 1 res += out (the residual
+//     stream updated in place, each element owned by one wave), 2 SwiGLU (pair = gate row p,
+//     up row I + p: the splitk_reduce_kernel<true> arithmetic), 3 RoPE + paged-KV write (pair =
+//     the two rows one rotation mixes: (2i, 2i+1) for weights permuted by fold_norms, (i,
+//     i + D/2) rotate-half otherwise; q rotated into out, k rotated into the cache and kept
+//     unrotated in out, v copied -- the rope_kv_kernel contract).
+// A Llama block's decode step becomes QKV(norm, rope/kv) -> paged decode -> O(+res) ->
+// gate_up(norm, swiglu) -> down(+res): no reduce, norm or RoPE launches
+// (models/llama.py _forward_decode_gemv; the block it computes is the reference's generate
+// call, Minimal_RAG/Helpers/Helpers.cs:116, served by Ollama).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+struct GemvArgs {
+  const bf16_t* x = nullptr;  // [M, K] input rows (NORM: the residual rows to normalise)
+  long ldx = 0;
+  const bf16_t* gamma = nullptr;  // NORM weights [K]
+  float eps = 0.f;
+  const bf16_t* w = nullptr;  // [N, K] row-major
+  int M = 0, N = 0, K = 0;
+  int npairs = 0;
+  bf16_t* out = nullptr;  // modes 0 / 2 / 3
+  long ldo = 0;
+  bf16_t* res = nullptr;  // mode 1
+  long ldr = 0;
+  int I = 0;  // mode 2: gate rows [0, I), up rows [I, 2I)
+  // mode 3
+  const int* positions = nullptr;
+  const float* cos_sin = nullptr;
+  int Hq = 0, Hkv = 0, D = 0, BS = 0, neox = 0;
+  bf16_t* kc = nullptr;
+  bf16_t* vc = nullptr;
+  const int* slots = nullptr;
+};
+
+LK_DEVICE float rbf(float x) { return bf2f(f2bf(x)); }
+LK_DEVICE float silu_f(float x) { return x / (1.f + __expf(-x)); }
+
+// 8 bf16 (one 16-B chunk, as 4 dwords) -> fp32 pairs: lo = w << 16, hi = w & 0xffff0000
+LK_DEVICE void dot8(const uint4_t wv, const uint4_t xv, float& acc) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const unsigned a = wv[j], b = xv[j];
+    acc = fmaf(__uint_as_float(a << 16), __uint_as_float(b << 16), acc);
+    acc = fmaf(__uint_as_float(a & 0xffff0000u), __uint_as_float(b & 0xffff0000u), acc);
+  }
+}
+
+template <int MR, bool NORM, int MODE, int U>
+__global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* xs = reinterpret_cast<bf16_t*>(smem);  // [MR][K]
+  __shared__ float red[4 * MR];
+  const int K = g.K;
+  const int nch = K >> 3;  // 16-B chunks per row
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+
+  // ---- stage X (with the RMSNorm prologue) into LDS
+#pragma unroll
+  for (int m = 0; m < MR; ++m) {
+    const bf16_t* xr = g.x + (long)m * g.ldx;
+    float ss = 0.f;
+    for (int c = threadIdx.x; c < nch; c += 256) {
+      const uint4_t v = *reinterpret_cast<const uint4_t*>(xr + c * 8);
+      *reinterpret_cast<uint4_t*>(xs + m * K + c * 8) = v;
+      if constexpr (NORM) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float lo = __uint_as_float(v[j] << 16), hi = __uint_as_float(v[j] & 0xffff0000u);
+          ss += lo * lo + hi * hi;
+        }
+      }
+    }
+    if constexpr (NORM) {
+      ss = wave_sum(ss);
+      if (lane == 0) red[m * 4 + wv] = ss;
+    }
+  }
+  if constexpr (NORM) {
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      const float tot = red[m * 4] + red[m * 4 + 1] + red[m * 4 + 2] + red[m * 4 + 3];
+      const float inv = rsqrtf(tot / (float)K + g.eps);
+      for (int c = threadIdx.x; c < nch; c += 256) {
+        float v[8], gm[8], y[8];
+        load8(xs + m * K + c * 8, v);
+        load8(g.gamma + c * 8, gm);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = rbf(v[j] * inv) * gm[j];
+        store8(xs + m * K + c * 8, y);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- stream W: one pair of rows per wave at a time
+  const int nwaves = gridDim.x * 4;
+  const int kc_lane = nch >> 6;  // chunks per lane (K % 512 == 0)
+  for (int p = blockIdx.x * 4 + wv; p < g.npairs; p += nwaves) {
+    long ra, rb;
+    int hd = 0, head = 0, ip = 0;
+    if constexpr (MODE == 2) {
+      ra = p;
+      rb = (long)g.I + p;
+    } else if constexpr (MODE == 3) {
+      hd = g.D >> 1;
+      head = p / hd;
+      ip = p - head * hd;
+      if (g.neox && head < g.Hq + g.Hkv) {
+        ra = (long)head * g.D + ip;
+        rb = ra + hd;
+      } else {
+        ra = (long)head * g.D + 2 * ip;
+        rb = ra + 1;
+      }
+    } else {
+      ra = 2L * p;
+      rb = ra + 1;
+    }
+    const uint4_t* wa = reinterpret_cast<const uint4_t*>(g.w + ra * K) + lane;
+    const uint4_t* wb = reinterpret_cast<const uint4_t*>(g.w + rb * K) + lane;
+    const uint4_t* xl = reinterpret_cast<const uint4_t*>(xs) + lane;
+    float acc_a[MR], acc_b[MR];
+#pragma unroll
+    for (int m = 0; m < MR; ++m) acc_a[m] = acc_b[m] = 0.f;
+    for (int j0 = 0; j0 < kc_lane; j0 += U) {
+      uint4_t va[U], vb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        va[u] = __builtin_nontemporal_load(wa + (j0 + u) * 64);
+        vb[u] = __builtin_nontemporal_load(wb + (j0 + u) * 64);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+          const uint4_t xv = xl[m * nch + (j0 + u) * 64];
+          dot8(va[u], xv, acc_a[m]);
+          dot8(vb[u], xv, acc_b[m]);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      acc_a[m] = wave_sum(acc_a[m]);
+      acc_b[m] = wave_sum(acc_b[m]);
+    }
+    if (lane != 0) continue;
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      const float da = acc_a[m], db = acc_b[m];
+      if constexpr (MODE == 0) {
+        g.out[(long)m * g.ldo + ra] = f2bf(da);
+        g.out[(long)m * g.ldo + rb] = f2bf(db);
+      } else if constexpr (MODE == 1) {
+        bf16_t* rr = g.res + (long)m * g.ldr;
+        const unsigned old = *reinterpret_cast<const unsigned*>(rr + ra);  // (ra even: rb = ra + 1)
+        const float va = rbf(rbf(da) + __uint_as_float(old << 16));
+        const float vb = rbf(rbf(db) + __uint_as_float(old & 0xffff0000u));
+        *reinterpret_cast<unsigned*>(rr + ra) = pack_bf2(va, vb);
+      } else if constexpr (MODE == 2) {
+        g.out[(long)m * g.ldo + p] = f2bf(rbf(silu_f(rbf(da))) * rbf(db));
+      } else {
+        bf16_t* orow = g.out + (long)m * g.ldo;
+        const float x1 = rbf(da), x2 = rbf(db);
+        const int slot = g.slots ? g.slots[m] : -1;
+        const long blk = slot >= 0 ? slot / g.BS : 0;
+        const int off = slot >= 0 ? slot % g.BS : 0;
+        const int d0 = (int)(ra - (long)head * g.D), d1 = (int)(rb - (long)head * g.D);
+        if (head >= g.Hq + g.Hkv) {  // V: copied (into the row and the cache)
+          const int h = head - g.Hq - g.Hkv;
+          orow[ra] = f2bf(x1);
+          orow[rb] = f2bf(x2);
+          if (g.vc && slot >= 0) {
+            bf16_t* vd = g.vc + ((blk * g.Hkv + h) * g.BS + off) * g.D;
+            vd[d0] = f2bf(x1);
+            vd[d1] = f2bf(x2);
+          }
+        } else {
+          const float* cs = g.cos_sin + (long)g.positions[m] * g.D;  // [cos(D/2) | sin(D/2)]
+          const float c = cs[ip], s = cs[hd + ip];
+          const float y1 = x1 * c - x2 * s, y2 = x2 * c + x1 * s;
+          if (head < g.Hq) {
+            orow[ra] = f2bf(y1);
+            orow[rb] = f2bf(y2);
+          } else {  // K: unrotated in the row, rotated in the cache
+            orow[ra] = f2bf(x1);
+            orow[rb] = f2bf(x2);
+            if (g.kc && slot >= 0) {
+              bf16_t* kd = g.kc + ((blk * g.Hkv + (head - g.Hq)) * g.BS + off) * g.D;
+              kd[d0] = f2bf(y1);
+              kd[d1] = f2bf(y2);
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+int g_gemv_wgs = 0;  // target workgroup count (0: the default below)
+
+template <int MR, bool NORM, int MODE>
+int launch_u(const GemvArgs& a, int U, hipStream_t st) {
+  int target = g_gemv_wgs > 0 ? g_gemv_wgs : 512;
+  int wgs = (a.npairs + 3) / 4;
+  if (wgs > target) wgs = target;
+  const size_t lds = (size_t)MR * a.K * 2;
+  if (lds > 65536) return -3;
+#define LK_GEMV_U(UU)                                                                  \
+  if (U == UU) {                                                                       \
+    gemv_decode_kernel<MR, NORM, MODE, UU><<<wgs, 256, lds, st>>>(a);                  \
+  } else
+  LK_GEMV_U(8) LK_GEMV_U(7) LK_GEMV_U(4) return -4;
+#undef LK_GEMV_U
+  LK_CHECK_LAUNCH();
+  return 0;
+}
+
+int pick_u(int K) {
+  const int kc = K / 512;
+  if (kc % 8 == 0) return 8;
+  if (kc % 7 == 0) return 7;
+  if (kc % 4 == 0) return 4;
+  return 0;
+}
+
+template <bool NORM, int MODE>
+int launch_m(const GemvArgs& a, hipStream_t st) {
+  const int U = pick_u(a.K);
+  if (!U || a.K % 512) return -2;
+  if (a.M == 1) return launch_u<1, NORM, MODE>(a, U, st);
+  if (a.M == 2) return launch_u<2, NORM, MODE>(a, U, st);
+  return -2;
+}
+
+}  // namespace
+
+int lk_gemv_supported(int M, int N, int K, int mode) {
+  if (M < 1 || M > 2 || K % 512 || !pick_u(K) || (long)M * K * 2 > 65536) return 0;
+  if (mode == 2) return N % 2 == 0;
+  return N % 2 == 0;
+}
+
+void lk_gemv_set_wgs(int wgs) { g_gemv_wgs = wgs; }
+
+int lk_gemv_decode(int mode, const bf16_t* x, long ldx, const bf16_t* gamma, float eps, const bf16_t* w, int M, int N,
+                   int K, bf16_t* out, long ldo, bf16_t* res, long ldr, const int* positions, const float* cos_sin,
+                   int Hq, int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,
+                   hipStream_t st) {
+  if (!lk_gemv_supported(M, N, K, mode) || !x || !w || ldx % 8) return -1;
+  GemvArgs a;
+  a.x = x;
+  a.ldx = ldx;
+  a.gamma = gamma;
+  a.eps = eps;
+  a.w = w;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.out = out;
+  a.ldo = ldo;
+  a.res = res;
+  a.ldr = ldr;
+  switch (mode) {
+    case 0:
+      if (!out) return -1;
+      a.npairs = N / 2;
+      break;
+    case 1:
+      if (!res || ldr % 2) return -1;
+      a.npairs = N / 2;
+      break;
+    case 2:
+      if (!out) return -1;
+      a.I = N / 2;
+      a.npairs = N / 2;
+      break;
+    case 3:
+      if (!out || !positions || !cos_sin || D % 2 || D <= 0 || N != (Hq + 2 * Hkv) * D || (kc && BS <= 0))
+        return -1;
+      a.positions = positions;
+      a.cos_sin = cos_sin;
+      a.Hq = Hq;
+      a.Hkv = Hkv;
+      a.D = D;
+      a.BS = BS;
+      a.neox = neox;
+      a.kc = kc;
+      a.vc = vc;
+      a.slots = slots;
+      a.npairs = N / 2;
+      break;
+    default:
+      return -1;
+  }
+  const bool norm = gamma != nullptr;
+#define LK_GEMV_MODE(MD)                                             \
+  if (mode == MD) return norm ? launch_m<true, MD>(a, st) : launch_m<false, MD>(a, st);
+  LK_GEMV_MODE(0) LK_GEMV_MODE(1) LK_GEMV_MODE(2) LK_GEMV_MODE(3)
+#undef LK_GEMV_MODE
+  return -1;
+}

@@ -42,6 +42,15 @@ int lk_wsgemm_pro(int kind, bf16_t* x, const bf16_t* w, int M, int N, int K, int
 int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, int BN, int S, int swiglu,
               bf16_t* out, long ldo, float* part, hipStream_t st);
 
+// gemv_decode.hip (decode GEMV for M <= 2 rows; mode 0 out, 1 res += out, 2 SwiGLU, 3 RoPE + paged KV;
+// gamma != nullptr: RMSNorm prologue over x)
+int lk_gemv_supported(int M, int N, int K, int mode);
+void lk_gemv_set_wgs(int wgs);
+int lk_gemv_decode(int mode, const bf16_t* x, long ldx, const bf16_t* gamma, float eps, const bf16_t* w, int M, int N,
+                   int K, bf16_t* out, long ldo, bf16_t* res, long ldr, const int* positions, const float* cos_sin,
+                   int Hq, int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,
+                   hipStream_t st);
+
 // GEMM part only (S >= 2): f32 partial slabs part[S][M][N], for a consumer that fuses the
 // split-K reduction (lk_splitk_rmsnorm, lk_splitk_rope_kv)
 int lk_wsgemm_set_variant(int M, int N, int K, int swiglu, int variant);  // -1 = back to the default

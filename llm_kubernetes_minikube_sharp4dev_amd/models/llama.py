@@ -181,6 +181,8 @@ class LlamaModel(nn.Module):
         L0 = self.layers[0]
         if self.folded and not self.tp.enabled and ops.prefill_chain_ok(res, L0.qkv, L0.o, L0.gate_up, L0.down):
             return self._forward_chain(res, meta, kv_caches)
+        if self._gemv_ok(res, meta):
+            return self._forward_decode_gemv(res, meta, kv_caches)
         if self._xpro_ok(res, meta):
             return self._forward_decode_xpro(res, meta, kv_caches)
         x = ops.rmsnorm(res, self.layers[0].input_norm, cfg.norm_eps)
@@ -209,6 +211,43 @@ class LlamaModel(nn.Module):
             x = self.tp.all_reduce_rmsnorm(ops.linear(attn_out, L.o), res, L.post_norm, cfg.norm_eps)
             a = ops.linear_swiglu(x, L.gate_up)
             x = self.tp.all_reduce_rmsnorm(ops.linear(a, L.down), res, nxt, cfg.norm_eps)
+        if meta.logits_idx is not None:
+            x = ops.gather_rows(x, meta.logits_idx)
+        return x
+
+    def _gemv_ok(self, res: torch.Tensor, meta: AttnMeta) -> bool:
+        """Decode steps of <= 2 rows on one GPU run the GEMV block (``_forward_decode_gemv``)."""
+        M = res.shape[0]
+        if not (ops.GEMV and res.is_cuda and not self.tp.enabled and self.cp_group is None
+                and M <= ops.GEMV_MAX_M and meta.num_prefill_tokens == 0 and meta.num_decode == M
+                and meta.shared_len is None and meta.cu_u is None):
+            return False
+        L0 = self.layers[0]
+        return (ops.gemv_supported(M, L0.qkv.shape[0], L0.qkv.shape[1], 3)
+                and ops.gemv_supported(M, L0.o.shape[0], L0.o.shape[1], 1)
+                and ops.gemv_supported(M, L0.gate_up.shape[0], L0.gate_up.shape[1], 2)
+                and ops.gemv_supported(M, L0.down.shape[0], L0.down.shape[1], 1))
+
+    def _forward_decode_gemv(self, res: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
+        """Decode step of one or two rows as GEMVs (csrc/gemv_decode.hip): per layer QKV (RMSNorm
+        prologue, RoPE + paged-KV epilogue) -> paged decode -> O (residual add) -> gate_up (RMSNorm
+        prologue, SwiGLU) -> down (residual add).  Weight streaming without split-K slabs, so no
+        reduce, norm or RoPE launch sits between the projections; same rounding points as the
+        unfused step (fp32 dot products in another order)."""
+        cfg = self.cfg
+        eps = cfg.norm_eps
+        hq, hkv, D = self.hq, self.hkv, self.D
+        attn_out = None
+        for li, L in enumerate(self.layers):
+            kc, vc = kv_caches[li]
+            qkv = ops.gemv_decode(3, res, L.qkv, L.input_norm, eps, positions=meta.positions, cos_sin=self.cos_sin,
+                                  Hq=hq, Hkv=hkv, D=D, k_cache=kc, v_cache=vc, slots=meta.slots,
+                                  neox=self.rope_neox)
+            attn_out = paged_attention(qkv, kc, vc, meta, hq, hkv, D, self.scale, attn_out)
+            ops.gemv_decode(1, attn_out, L.o, res=res)
+            a = ops.gemv_decode(2, res, L.gate_up, L.post_norm, eps)
+            ops.gemv_decode(1, a, L.down, res=res)
+        x = ops.rmsnorm(res, self.final_norm, eps)
         if meta.logits_idx is not None:
             x = ops.gather_rows(x, meta.logits_idx)
         return x

@@ -761,6 +761,8 @@ def linear(x, w, b=None, act: Optional[str] = None):
             y = ref.activation_(y, None, 0 if act == "gelu" else 2)
         return y
     if b is None and act is None:
+        if _gemv_ok(x, w, 0):
+            return lib().gemv_decode(0, x, w)
         kind = _decode_gemm_kind(x, w, False)
         if kind == "skinny":
             return lib().skinny_linear(x, w)
@@ -782,6 +784,8 @@ def linear_swiglu(x, w_gate_up):
     SwiGLU epilogue) in every regime."""
     if not use_hip(x):
         return silu_mul(linear(x, w_gate_up))
+    if _gemv_ok(x, w_gate_up, 2):
+        return lib().gemv_decode(2, x, w_gate_up)
     kind = _decode_gemm_kind(x, w_gate_up, True)
     if kind == "skinny":
         return lib().skinny_linear(x, w_gate_up, True)
@@ -838,8 +842,10 @@ def ws_tickets(device):
 # GPU without TP): the O projection merges the paged-decode split partials itself (no
 # decode_reduce launch) and gate_up / the next layer's QKV compute residual add + RMSNorm of the
 # previous projection's split-K slabs themselves (no rmsnorm launch) -- three launches fewer per
-# layer, bit-identical values (models/llama.py _forward_decode_xpro).  LK_DECODE_XPRO=0: off.
-XPRO = os.environ.get("LK_DECODE_XPRO", "1") != "0"
+# layer, bit-identical values (models/llama.py _forward_decode_xpro).  Measured slower at batch 1
+# (decode step 4.23 vs 3.58 ms: every workgroup re-reads and re-normalises the producer's fp32 slabs,
+# and the O projection's merge prologue costs 17 us; profiles/r6_xpro/): off unless LK_DECODE_XPRO=1.
+XPRO = os.environ.get("LK_DECODE_XPRO", "0") == "1"
 XPRO_MAX_M = int(os.environ.get("LK_DECODE_XPRO_MAX_M", "16"))
 _PLAN_CACHE: dict = {}
 
@@ -859,6 +865,56 @@ def ws_pro(x, w, plan, kind: int, swiglu: bool = False, reduce: bool = False, **
     output with its split partials ``po`` / ``pml`` merged; 0: plain x).  Returns the f32 partial
     slabs [S, M, N] (S > 1 and not ``reduce``) or the bf16 / SwiGLU output."""
     return lib().ws_pro(x, w, swiglu, plan[0], plan[1], kind, reduce, **kw)
+
+
+# Decode GEMV for one or two rows (csrc/gemv_decode.hip): no split-K slabs, the RMSNorm in the
+# consumer's prologue, residual add / SwiGLU / RoPE + paged-KV write in the epilogue -- a Llama
+# block's batch-1 decode step is QKV -> paged decode -> O -> gate_up -> down, with no reduce, norm
+# or RoPE launch (models/llama.py _forward_decode_gemv).  LK_DECODE_GEMV=0: the weight-streaming path.
+GEMV = os.environ.get("LK_DECODE_GEMV", "1") != "0"
+GEMV_MAX_M = 2
+_GEMV_OK: dict = {}
+
+
+def gemv_supported(M: int, N: int, K: int, mode: int) -> bool:
+    key = (M, N, K, mode)
+    ok = _GEMV_OK.get(key)
+    if ok is None:
+        ok = _GEMV_OK[key] = bool(lib().gemv_supported(M, N, K, mode))
+    return ok
+
+
+def _gemv_ok(x, w, mode: int) -> bool:
+    """A plain / SwiGLU projection of <= 2 rows goes to the decode GEMV (faster than the weight-
+    streaming kernels at every decode shape measured: benchmarks/gemv_bench.py, profiles/r6_gemv/)."""
+    M = x.shape[0]
+    return (GEMV and M <= GEMV_MAX_M and x.dim() == 2 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and w.is_contiguous() and x.stride(-1) == 1
+            and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and gemv_supported(M, w.shape[0], w.shape[1], mode))
+
+
+def gemv_decode(mode: int, x, w, gamma=None, eps: float = 1e-5, res=None, positions=None, cos_sin=None,
+                Hq: int = 0, Hkv: int = 0, D: int = 0, k_cache=None, v_cache=None, slots=None, neox: bool = True):
+    """mode 0: x W^T; 1: ``res`` += x W^T in place (returned); 2: SwiGLU(x [Wg; Wu]^T) [M, N/2];
+    3: packed QKV with RoPE applied to q (and to k in the paged cache, k kept unrotated in the
+    row), K/V written at ``slots``.  ``gamma``: the GEMV's input is RMSNorm(x) * gamma."""
+    if use_hip(x):
+        return lib().gemv_decode(mode, x, w, gamma, eps, res, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache,
+                                 slots, neox)
+    xin = ref.rmsnorm(x, gamma, eps) if gamma is not None else x
+    y = xin.float() @ w.float().t()
+    if mode == 0:
+        return y.to(x.dtype)
+    if mode == 1:
+        res.copy_((y.to(res.dtype).float() + res.float()).to(res.dtype))
+        return res
+    if mode == 2:
+        I = w.shape[0] // 2
+        g, u = y[:, :I].to(x.dtype).float(), y[:, I:].to(x.dtype).float()
+        return (torch.nn.functional.silu(g).to(x.dtype).float() * u).to(x.dtype)
+    qkv = y.to(x.dtype)
+    rope_kv_(qkv, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache, slots, neox, False)
+    return qkv
 
 
 def splitk_rope_kv(part, positions, cos_sin, Hq: int, Hkv: int, D: int, k_cache, v_cache, slots, neox: bool,
