@@ -1153,6 +1153,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return lk_gemv_supported((int)M, (int)N, (int)K, (int)mode) != 0;
   });
   m.def("gemv_set_wgs", [](int64_t n) { lk_gemv_set_wgs((int)n); });
+  m.def("gemv_set_prefetch", [](bool on) { lk_gemv_set_prefetch(on ? 1 : 0); });
+  // read rows [r0, r1) of a contiguous 2-D tensor through the Infinity Cache (lk_l3_prefetch)
+  m.def("l3_prefetch", [](const at::Tensor& t, int64_t r0, int64_t r1, int64_t wgs, at::Tensor& sink) {
+    CHECK_CUDA(t); CHECK_CONTIG(t); CHECK_CUDA(sink);
+    TORCH_CHECK(sink.scalar_type() == at::kInt && sink.numel() >= 1, "sink: int32 [>= 1]");
+    TORCH_CHECK(t.dim() == 2 && 0 <= r0 && r0 <= r1 && r1 <= t.size(0), "rows out of range");
+    const long row = t.size(1) * t.element_size();
+    const char* base = reinterpret_cast<const char*>(t.data_ptr()) + r0 * row;
+    CHECK_RC(lk_l3_prefetch(base, (r1 - r0) * row, (int)wgs, reinterpret_cast<unsigned*>(sink.data_ptr<int>()),
+                            cur_stream()), "l3_prefetch");
+  });
   m.def("ws_set_variant", [](int64_t M, int64_t N, int64_t K, bool swiglu, int64_t v) {
     CHECK_RC(lk_wsgemm_set_variant((int)M, (int)N, (int)K, swiglu ? 1 : 0, (int)v), "ws_set_variant");
   }, "weight-streaming GEMM kernel for this (M bucket, N, K, swiglu): 0 ring, 1 loader waves, -1 default",

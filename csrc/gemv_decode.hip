@@ -62,7 +62,7 @@ LK_DEVICE void dot8(const uint4_t wv, const uint4_t xv, float& acc) {
   }
 }
 
-template <int MR, bool NORM, int MODE, int U>
+template <int MR, bool NORM, int MODE, int U, bool PF>
 __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* xs = reinterpret_cast<bf16_t*>(smem);  // [MR][K]
@@ -70,6 +70,47 @@ __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
   const int K = g.K;
   const int nch = K >> 3;  // 16-B chunks per row
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+
+  // rows of pair p (see the header)
+  auto pair_rows = [&](int p, long& ra, long& rb, int& hd, int& head, int& ip) {
+    if constexpr (MODE == 2) {
+      ra = p;
+      rb = (long)g.I + p;
+    } else if constexpr (MODE == 3) {
+      hd = g.D >> 1;
+      head = p / hd;
+      ip = p - head * hd;
+      if (g.neox && head < g.Hq + g.Hkv) {
+        ra = (long)head * g.D + ip;
+        rb = ra + hd;
+      } else {
+        ra = (long)head * g.D + 2 * ip;
+        rb = ra + 1;
+      }
+    } else {
+      ra = 2L * p;
+      rb = ra + 1;
+    }
+  };
+  // PF: the first K block of this wave's first pair is requested before X is staged, so the W
+  // stream starts at the kernel's first instruction instead of after the prologue's loads and
+  // barriers (costs VGPRs: the block stays live across the prologue)
+  const int nwaves = gridDim.x * 4;
+  const int kc_lane = nch >> 6;  // chunks per lane (K % 512 == 0)
+  const int p0 = blockIdx.x * 4 + wv;
+  uint4_t va[U], vb[U];
+  if (PF && p0 < g.npairs) {
+    long ra, rb;
+    int hd, head, ip;
+    pair_rows(p0, ra, rb, hd, head, ip);
+    const uint4_t* wa = reinterpret_cast<const uint4_t*>(g.w + ra * K) + lane;
+    const uint4_t* wb = reinterpret_cast<const uint4_t*>(g.w + rb * K) + lane;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      va[u] = __builtin_nontemporal_load(wa + u * 64);
+      vb[u] = __builtin_nontemporal_load(wb + u * 64);
+    }
+  }
 
   // ---- stage X (with the RMSNorm prologue) into LDS
 #pragma unroll
@@ -111,29 +152,10 @@ __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
   __syncthreads();
 
   // ---- stream W: one pair of rows per wave at a time
-  const int nwaves = gridDim.x * 4;
-  const int kc_lane = nch >> 6;  // chunks per lane (K % 512 == 0)
-  for (int p = blockIdx.x * 4 + wv; p < g.npairs; p += nwaves) {
+  for (int p = p0; p < g.npairs; p += nwaves) {
     long ra, rb;
     int hd = 0, head = 0, ip = 0;
-    if constexpr (MODE == 2) {
-      ra = p;
-      rb = (long)g.I + p;
-    } else if constexpr (MODE == 3) {
-      hd = g.D >> 1;
-      head = p / hd;
-      ip = p - head * hd;
-      if (g.neox && head < g.Hq + g.Hkv) {
-        ra = (long)head * g.D + ip;
-        rb = ra + hd;
-      } else {
-        ra = (long)head * g.D + 2 * ip;
-        rb = ra + 1;
-      }
-    } else {
-      ra = 2L * p;
-      rb = ra + 1;
-    }
+    pair_rows(p, ra, rb, hd, head, ip);
     const uint4_t* wa = reinterpret_cast<const uint4_t*>(g.w + ra * K) + lane;
     const uint4_t* wb = reinterpret_cast<const uint4_t*>(g.w + rb * K) + lane;
     const uint4_t* xl = reinterpret_cast<const uint4_t*>(xs) + lane;
@@ -141,11 +163,12 @@ __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
 #pragma unroll
     for (int m = 0; m < MR; ++m) acc_a[m] = acc_b[m] = 0.f;
     for (int j0 = 0; j0 < kc_lane; j0 += U) {
-      uint4_t va[U], vb[U];
+      if (!PF || p != p0 || j0 != 0) {  // (PF: the first block came in before the prologue)
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        va[u] = __builtin_nontemporal_load(wa + (j0 + u) * 64);
-        vb[u] = __builtin_nontemporal_load(wb + (j0 + u) * 64);
+        for (int u = 0; u < U; ++u) {
+          va[u] = __builtin_nontemporal_load(wa + (j0 + u) * 64);
+          vb[u] = __builtin_nontemporal_load(wb + (j0 + u) * 64);
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -215,7 +238,31 @@ __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
   }
 }
 
+// Infinity-Cache (L3) prefetch: default-policy 16-B loads over [p, p + bytes) whose values are
+// folded into one word that is stored only if it equals a value no sum of these loads takes in
+// practice (the loads cannot be dropped).  Launched on a side stream while the latency-bound
+// attention kernels leave HBM idle, so the next projection's weights are read from the 256 MiB L3.
+__global__ __launch_bounds__(256) void l3_prefetch_kernel(const uint4_t* __restrict__ p, long n16,
+                                                          unsigned* __restrict__ sink) {
+  unsigned acc = 0;
+  const long stride = (long)gridDim.x * 256;
+  long i = (long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 7 * stride < n16; i += 8 * stride) {
+    uint4_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc ^= v[u][0] ^ v[u][3];
+  }
+  for (; i < n16; i += stride) {
+    const uint4_t v = p[i];
+    acc ^= v[0] ^ v[3];
+  }
+  if (acc == 0x9e3779b9u) sink[0] = acc;
+}
+
 int g_gemv_wgs = 0;  // target workgroup count (0: the default below)
+int g_gemv_pf = 0;   // W prefetch before the prologue (ops.GEMV_PREFETCH)
 
 template <int MR, bool NORM, int MODE>
 int launch_u(const GemvArgs& a, int U, hipStream_t st) {
@@ -226,7 +273,10 @@ int launch_u(const GemvArgs& a, int U, hipStream_t st) {
   if (lds > 65536) return -3;
 #define LK_GEMV_U(UU)                                                                  \
   if (U == UU) {                                                                       \
-    gemv_decode_kernel<MR, NORM, MODE, UU><<<wgs, 256, lds, st>>>(a);                  \
+    if (g_gemv_pf)                                                                     \
+      gemv_decode_kernel<MR, NORM, MODE, UU, true><<<wgs, 256, lds, st>>>(a);          \
+    else                                                                               \
+      gemv_decode_kernel<MR, NORM, MODE, UU, false><<<wgs, 256, lds, st>>>(a);         \
   } else
   LK_GEMV_U(8) LK_GEMV_U(7) LK_GEMV_U(4) return -4;
 #undef LK_GEMV_U
@@ -260,6 +310,14 @@ int lk_gemv_supported(int M, int N, int K, int mode) {
 }
 
 void lk_gemv_set_wgs(int wgs) { g_gemv_wgs = wgs; }
+
+int lk_l3_prefetch(const void* p, long bytes, int wgs, unsigned* sink, hipStream_t st) {
+  if (!p || bytes < 16 || ((uintptr_t)p & 15) || !sink || wgs < 1) return bytes < 16 ? 0 : -1;
+  l3_prefetch_kernel<<<wgs, 256, 0, st>>>(reinterpret_cast<const uint4_t*>(p), bytes / 16, sink);
+  LK_CHECK_LAUNCH();
+  return 0;
+}
+void lk_gemv_set_prefetch(int on) { g_gemv_pf = on ? 1 : 0; }
 
 int lk_gemv_decode(int mode, const bf16_t* x, long ldx, const bf16_t* gamma, float eps, const bf16_t* w, int M, int N,
                    int K, bf16_t* out, long ldo, bf16_t* res, long ldr, const int* positions, const float* cos_sin,

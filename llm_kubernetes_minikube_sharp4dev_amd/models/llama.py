@@ -238,15 +238,32 @@ class LlamaModel(nn.Module):
         eps = cfg.norm_eps
         hq, hkv, D = self.hq, self.hkv, self.D
         attn_out = None
+        side = None
+        if ops.GEMV_L3_MB >= 0:  # Infinity-Cache prefetch beside the attention (ops.GEMV_L3_MB)
+            side = self.__dict__.get("_l3_side")
+            if side is None:
+                side = self._l3_side = torch.cuda.Stream(res.device)
+            I = self.layers[0].gate_up.shape[0] // 2
+            rows = min(I, (ops.GEMV_L3_MB << 20) // (2 * self.layers[0].gate_up.stride(0) * 2))
+        main = torch.cuda.current_stream(res.device) if side is not None else None
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
             qkv = ops.gemv_decode(3, res, L.qkv, L.input_norm, eps, positions=meta.positions, cos_sin=self.cos_sin,
                                   Hq=hq, Hkv=hkv, D=D, k_cache=kc, v_cache=vc, slots=meta.slots,
                                   neox=self.rope_neox)
+            if side is not None:
+                side.wait_stream(main)  # (after the QKV stream: HBM is free from here)
+                with torch.cuda.stream(side):
+                    ops.l3_prefetch(L.o, 0, L.o.shape[0])
+                    if rows:
+                        ops.l3_prefetch(L.gate_up, 0, rows)
+                        ops.l3_prefetch(L.gate_up, I, I + rows)
             attn_out = paged_attention(qkv, kc, vc, meta, hq, hkv, D, self.scale, attn_out)
             ops.gemv_decode(1, attn_out, L.o, res=res)
             a = ops.gemv_decode(2, res, L.gate_up, L.post_norm, eps)
             ops.gemv_decode(1, a, L.down, res=res)
+        if side is not None:
+            main.wait_stream(side)
         x = ops.rmsnorm(res, self.final_norm, eps)
         if meta.logits_idx is not None:
             x = ops.gather_rows(x, meta.logits_idx)

@@ -876,10 +876,37 @@ GEMV_MAX_M = 2
 _GEMV_OK: dict = {}
 
 
+# W prefetch before the GEMV's X prologue (LK_GEMV_PREFETCH=1: on; measured slower -- the block
+# held across the prologue costs a wave per SIMD: batch-1 decode step 3.199 vs 3.17 ms,
+# profiles/r6_gemv/), workgroup target (0: 512)
+GEMV_PREFETCH = os.environ.get("LK_GEMV_PREFETCH", "0") == "1"
+GEMV_WGS = int(os.environ.get("LK_GEMV_WGS", "0") or 0)
+
+
+# Batch-1 decode: while the latency-bound paged-decode kernels leave HBM idle, a side stream reads
+# the O projection's weights (and the first LK_GEMV_L3_PREFETCH_MB of gate_up's gate / up rows)
+# through the 256 MiB Infinity Cache so the GEMVs behind the attention read them from L3.
+# -1: off; 0: O only.
+GEMV_L3_MB = int(os.environ.get("LK_GEMV_L3_PREFETCH_MB", "-1") or -1)
+GEMV_L3_WGS = int(os.environ.get("LK_GEMV_L3_WGS", "128") or 128)
+_L3_SINK: dict = {}
+
+
+def l3_prefetch(t, r0: int, r1: int):
+    """Read rows [r0, r1) of a contiguous 2-D GPU tensor (values unused) on the current stream."""
+    s = _L3_SINK.get(t.device)
+    if s is None:
+        s = _L3_SINK[t.device] = torch.zeros(1, dtype=torch.int32, device=t.device)
+    lib().l3_prefetch(t, r0, r1, GEMV_L3_WGS, s)
+
+
 def gemv_supported(M: int, N: int, K: int, mode: int) -> bool:
     key = (M, N, K, mode)
     ok = _GEMV_OK.get(key)
     if ok is None:
+        if not _GEMV_OK:  # first use: the launch knobs
+            lib().gemv_set_prefetch(GEMV_PREFETCH)
+            lib().gemv_set_wgs(GEMV_WGS)
         ok = _GEMV_OK[key] = bool(lib().gemv_supported(M, N, K, mode))
     return ok
 

@@ -1,0 +1,13 @@
+# Batch-1: Infinity-Cache prefetch of the O / gate_up weights beside the attention
+# (LK_GEMV_L3_PREFETCH_MB: -1 off, 0 O only, 48 / 112 MB of gate_up too), interleaved, twice.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R && mkdir -p gpurun_out/l3pf
+timeout -k 10 400 python -u -m pytest tests/test_gemv_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/l3pf/pytest.log 2>&1 || { tail -40 gpurun_out/l3pf/pytest.log; exit 91; }
+tail -1 gpurun_out/l3pf/pytest.log
+for i in 1 2; do
+  for x in -1 0 48 112; do
+    LK_GEMV_L3_PREFETCH_MB=$x timeout -k 10 300 python bench.py --batch 1 --steps 16 --warmup 2 --json-out gpurun_out/l3pf/b1_${x}_$i.json > gpurun_out/l3pf/b1_${x}_$i.log 2>&1 || { tail gpurun_out/l3pf/b1_${x}_$i.log; exit 93; }
+    python -c "import json; d=json.load(open('gpurun_out/l3pf/b1_${x}_$i.json')); m=d['config']['step_mix_rank0']; print('b1 l3 $x', d['value'], d['p50_latency_ms'], d['p90_latency_ms'], round(1e3 * m['decode_only_gpu_s'] / max(1, m['decode_only_steps']), 3))"
+  done
+done

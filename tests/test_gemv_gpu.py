@@ -173,7 +173,12 @@ def test_decode_step_gemv_equals_ws(monkeypatch, folded):
         kv = [(k.clone(), v.clone()) for k, v in saved["kv"]]
         outs[on] = real_fwd(m, saved["ids"].clone(), _clone_meta(saved["meta"]), kv)
         kvs[on] = kv
+    monkeypatch.setattr(ops, "GEMV", True)
+    monkeypatch.setattr(ops, "GEMV_L3_MB", 16)  # Infinity-Cache prefetch beside the attention: same values
+    kv = [(k.clone(), v.clone()) for k, v in saved["kv"]]
+    pf = real_fwd(m, saved["ids"].clone(), _clone_meta(saved["meta"]), kv)
     torch.cuda.synchronize()
+    assert torch.equal(pf, outs[True])
     _close(outs[True], outs[False], 0.06, 0.02, "final hidden")
     for (k1, v1), (k2, v2) in zip(kvs[True], kvs[False]):
         _close(k1, k2, 0.05, 0.01, "k cache")
