@@ -100,13 +100,15 @@ def kv_write(k, v, k_cache, v_cache, slots):
 # bench's ~1k-key rows stay in one split, so no step launches the split-merge kernel (same box,
 # interleaved: mixed-step GPU time 9.21 / 9.18 vs 9.25 / 9.25 s, 108.2 / 108.3 vs 108.2 / 107.8 q/s)
 DECODE_SPLIT_LARGE = int(os.environ.get("LK_DECODE_SPLIT", "2048"))
+# keys per decode workgroup below 32 (sequence, kv head) pairs (batch 1: 8 kv heads)
+DECODE_SPLIT_SMALL = int(os.environ.get("LK_DECODE_SPLIT_SMALL", "128"))
 
 
 def decode_split_size(B: int, Hkv: int) -> int:
     """Keys per decode workgroup (mirrors lk_decode_split_size): small batches split the
     context finer so 256 CUs stay busy; static per (B, Hkv) for hipGraph capture."""
     bh = B * Hkv
-    return DECODE_SPLIT_LARGE if bh >= 512 else 512 if bh >= 128 else 256 if bh >= 32 else 128
+    return DECODE_SPLIT_LARGE if bh >= 512 else 512 if bh >= 128 else 256 if bh >= 32 else DECODE_SPLIT_SMALL
 
 
 def decode_splits(max_context: int, split: int) -> int:
