@@ -49,6 +49,9 @@ struct GemvArgs {
   const int* slots = nullptr;
 };
 
+typedef __attribute__((address_space(3))) void* gemv_lptr;
+typedef const __attribute__((address_space(1))) void* gemv_gptr;
+
 LK_DEVICE float rbf(float x) { return bf2f(f2bf(x)); }
 LK_DEVICE float silu_f(float x) { return x / (1.f + __expf(-x)); }
 
@@ -112,44 +115,57 @@ __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
     }
   }
 
-  // ---- stage X (with the RMSNorm prologue) into LDS
+  // ---- stage X (with the RMSNorm prologue) into LDS.  The rows (and gamma) come in by LDS-DMA
+  // (global_load_lds: no registers, every chunk's load in flight at once, one memory round trip
+  // for the whole prologue -- a load -> store loop serialised K / 2048 of them); chunk c of row m
+  // lands at xs + m * K + 8 c (64 consecutive chunks per wave instruction: nch % 64 == 0)
+  bf16_t* gs = xs + MR * K;  // NORM: gamma [K]
+  for (int c0 = wv * 64; c0 < nch; c0 += 256) {
 #pragma unroll
-  for (int m = 0; m < MR; ++m) {
-    const bf16_t* xr = g.x + (long)m * g.ldx;
-    float ss = 0.f;
-    for (int c = threadIdx.x; c < nch; c += 256) {
-      const uint4_t v = *reinterpret_cast<const uint4_t*>(xr + c * 8);
-      *reinterpret_cast<uint4_t*>(xs + m * K + c * 8) = v;
-      if constexpr (NORM) {
+    for (int m = 0; m < MR; ++m)
+      __builtin_amdgcn_global_load_lds((gemv_gptr)(g.x + (long)m * g.ldx + (c0 + lane) * 8),
+                                       (gemv_lptr)(xs + m * K + c0 * 8), 16, 0, 0);
+    if constexpr (NORM)
+      __builtin_amdgcn_global_load_lds((gemv_gptr)(g.gamma + (c0 + lane) * 8), (gemv_lptr)(gs + c0 * 8), 16, 0, 0);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (lgkmcnt / expcnt untouched)
+  __syncthreads();
+  if constexpr (NORM) {
+    // RMSNorm with rmsnorm_kernel's rounding: y = bf16(bf16(v * inv) * g), in place in LDS
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      float ss = 0.f;
+      for (int c = threadIdx.x; c < nch; c += 256) {
+        const uint4_t v = *reinterpret_cast<const uint4_t*>(xs + m * K + c * 8);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float lo = __uint_as_float(v[j] << 16), hi = __uint_as_float(v[j] & 0xffff0000u);
           ss += lo * lo + hi * hi;
         }
       }
-    }
-    if constexpr (NORM) {
       ss = wave_sum(ss);
       if (lane == 0) red[m * 4 + wv] = ss;
     }
-  }
-  if constexpr (NORM) {
     __syncthreads();
 #pragma unroll
     for (int m = 0; m < MR; ++m) {
       const float tot = red[m * 4] + red[m * 4 + 1] + red[m * 4 + 2] + red[m * 4 + 3];
       const float inv = rsqrtf(tot / (float)K + g.eps);
       for (int c = threadIdx.x; c < nch; c += 256) {
-        float v[8], gm[8], y[8];
-        load8(xs + m * K + c * 8, v);
-        load8(g.gamma + c * 8, gm);
+        const uint4_t v = *reinterpret_cast<const uint4_t*>(xs + m * K + c * 8);
+        const uint4_t gv = *reinterpret_cast<const uint4_t*>(gs + c * 8);
+        uint4_t o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) y[j] = rbf(v[j] * inv) * gm[j];
-        store8(xs + m * K + c * 8, y);
+        for (int j = 0; j < 4; ++j) {
+          const float y0 = rbf(__uint_as_float(v[j] << 16) * inv) * __uint_as_float(gv[j] << 16);
+          const float y1 = rbf(__uint_as_float(v[j] & 0xffff0000u) * inv) * __uint_as_float(gv[j] & 0xffff0000u);
+          o[j] = pack_bf2(y0, y1);
+        }
+        *reinterpret_cast<uint4_t*>(xs + m * K + c * 8) = o;
       }
     }
+    __syncthreads();
   }
-  __syncthreads();
 
   // ---- stream W: one pair of rows per wave at a time
   for (int p = p0; p < g.npairs; p += nwaves) {
@@ -261,6 +277,7 @@ __global__ __launch_bounds__(256) void l3_prefetch_kernel(const uint4_t* __restr
   if (acc == 0x9e3779b9u) sink[0] = acc;
 }
 
+constexpr int kGemvMaxLds = 163840 - 1024;  // dynamic LDS opt-in (the static `red` stays below)
 int g_gemv_wgs = 0;  // target workgroup count (0: the default below)
 int g_gemv_pf = 0;   // W prefetch before the prologue (ops.GEMV_PREFETCH)
 
@@ -269,14 +286,17 @@ int launch_u(const GemvArgs& a, int U, hipStream_t st) {
   int target = g_gemv_wgs > 0 ? g_gemv_wgs : 512;
   int wgs = (a.npairs + 3) / 4;
   if (wgs > target) wgs = target;
-  const size_t lds = (size_t)MR * a.K * 2;
-  if (lds > 65536) return -3;
+  const size_t lds = (size_t)(MR + (NORM ? 1 : 0)) * a.K * 2;  // X rows (+ gamma)
+  if (lds > kGemvMaxLds) return -3;
 #define LK_GEMV_U(UU)                                                                  \
   if (U == UU) {                                                                       \
-    if (g_gemv_pf)                                                                     \
+    if (g_gemv_pf) {                                                                   \
+      LK_SET_MAX_LDS((gemv_decode_kernel<MR, NORM, MODE, UU, true>), kGemvMaxLds);     \
       gemv_decode_kernel<MR, NORM, MODE, UU, true><<<wgs, 256, lds, st>>>(a);          \
-    else                                                                               \
+    } else {                                                                           \
+      LK_SET_MAX_LDS((gemv_decode_kernel<MR, NORM, MODE, UU, false>), kGemvMaxLds);    \
       gemv_decode_kernel<MR, NORM, MODE, UU, false><<<wgs, 256, lds, st>>>(a);         \
+    }                                                                                  \
   } else
   LK_GEMV_U(8) LK_GEMV_U(7) LK_GEMV_U(4) return -4;
 #undef LK_GEMV_U
@@ -304,7 +324,9 @@ int launch_m(const GemvArgs& a, hipStream_t st) {
 }  // namespace
 
 int lk_gemv_supported(int M, int N, int K, int mode) {
-  if (M < 1 || M > 2 || K % 512 || !pick_u(K) || (long)M * K * 2 > 65536) return 0;
+  // (K <= 16384: the prologue's SCH = 8 staging chunks per thread)
+  // (X rows and, for the RMSNorm prologue, gamma in LDS)
+  if (M < 1 || M > 2 || K % 512 || !pick_u(K) || (long)(M + 1) * K * 2 > kGemvMaxLds) return 0;
   if (mode == 2) return N % 2 == 0;
   return N % 2 == 0;
 }
