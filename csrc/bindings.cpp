@@ -389,9 +389,20 @@ at::Tensor gemv_decode(int64_t mode, const at::Tensor& x, const at::Tensor& w, c
                        double eps, const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& positions,
                        const c10::optional<at::Tensor>& cos_sin, int64_t Hq, int64_t Hkv, int64_t D,
                        const c10::optional<at::Tensor>& k_cache, const c10::optional<at::Tensor>& v_cache,
-                       const c10::optional<at::Tensor>& slots, bool neox) {
+                       const c10::optional<at::Tensor>& slots, bool neox, const c10::optional<at::Tensor>& po,
+                       const c10::optional<at::Tensor>& pml, const c10::optional<at::Tensor>& ctx,
+                       int64_t max_splits, int64_t split) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_LASTDIM(x); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "gemv_decode: x [M,K], w [N,K]");
+  if (po) {  // the O projection merging the paged-decode split partials of x's rows
+    TORCH_CHECK(mode == 1 && pml && ctx && !gamma, "gemv_decode merge prologue: mode 1 with pml, ctx, no gamma");
+    CHECK_F32(*po); CHECK_F32(*pml); CHECK_I32(*ctx); CHECK_CONTIG(*po); CHECK_CONTIG(*pml);
+    TORCH_CHECK(po->dim() == 4 && po->size(0) >= x.size(0) && po->size(1) == Hq && po->size(2) == max_splits &&
+                    po->size(3) == D && Hq * D == x.size(1), "po [M, Hq, max_splits, D]");
+    TORCH_CHECK(pml->dim() == 4 && pml->size(0) == po->size(0) && pml->size(1) == Hq && pml->size(2) == max_splits &&
+                    pml->size(3) == 2, "pml [M, Hq, max_splits, 2]");
+    TORCH_CHECK(ctx->numel() >= x.size(0) && split > 0, "ctx: one per row; split > 0");
+  }
   check_rows16(x, "x"); check_rows16(w, "w");
   const int M = x.size(0), K = x.size(1), N = w.size(0);
   TORCH_CHECK(lk_gemv_supported(M, N, K, (int)mode), "gemv_decode: unsupported shape M", M, " N", N, " K", K);
@@ -434,7 +445,9 @@ at::Tensor gemv_decode(int64_t mode, const at::Tensor& x, const at::Tensor& w, c
   }
   CHECK_RC(lk_gemv_decode((int)mode, bp(x), x.stride(0), bpo(gamma), (float)eps, bp(w), M, N, K,
                           mode == 1 ? nullptr : bp(out), mode == 1 ? 0 : out.stride(0), rp, ldr, pos, cs, (int)Hq,
-                          (int)Hkv, (int)D, kc, vc, sl, BS, neox ? 1 : 0, cur_stream()),
+                          (int)Hkv, (int)D, kc, vc, sl, BS, neox ? 1 : 0, po ? po->data_ptr<float>() : nullptr,
+                          pml ? pml->data_ptr<float>() : nullptr, ctx ? ip(*ctx) : nullptr, (int)max_splits,
+                          (int)split, cur_stream()),
            "gemv_decode");
   return out;
 }
@@ -1148,7 +1161,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("eps") = 1e-5, py::arg("res") = py::none(), py::arg("positions") = py::none(),
         py::arg("cos_sin") = py::none(), py::arg("Hq") = 0, py::arg("Hkv") = 0, py::arg("D") = 0,
         py::arg("k_cache") = py::none(), py::arg("v_cache") = py::none(), py::arg("slots") = py::none(),
-        py::arg("neox") = true);
+        py::arg("neox") = true, py::arg("po") = py::none(), py::arg("pml") = py::none(), py::arg("ctx") = py::none(),
+        py::arg("max_splits") = 0, py::arg("split") = 0);
   m.def("gemv_supported", [](int64_t M, int64_t N, int64_t K, int64_t mode) {
     return lk_gemv_supported((int)M, (int)N, (int)K, (int)mode) != 0;
   });

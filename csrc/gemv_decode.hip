@@ -47,6 +47,11 @@ struct GemvArgs {
   bf16_t* kc = nullptr;
   bf16_t* vc = nullptr;
   const int* slots = nullptr;
+  // PRO 2 (O projection): the paged-decode split partials of X's rows, merged in the prologue
+  const float* po = nullptr;   // [(row * Hq + h) * max_splits + s][D]
+  const float* pml = nullptr;  // [(row * Hq + h) * max_splits + s][2] (max in the log2 domain, sum)
+  const int* ctx = nullptr;
+  int max_splits = 0, split = 0;
 };
 
 typedef __attribute__((address_space(3))) void* gemv_lptr;
@@ -65,8 +70,9 @@ LK_DEVICE void dot8(const uint4_t wv, const uint4_t xv, float& acc) {
   }
 }
 
-template <int MR, bool NORM, int MODE, int U, bool PF>
+template <int MR, int PRO, int MODE, int U, bool PF>
 __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
+  constexpr bool NORM = PRO == 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* xs = reinterpret_cast<bf16_t*>(smem);  // [MR][K]
   __shared__ float red[4 * MR];
@@ -120,13 +126,51 @@ __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
   // for the whole prologue -- a load -> store loop serialised K / 2048 of them); chunk c of row m
   // lands at xs + m * K + 8 c (64 consecutive chunks per wave instruction: nch % 64 == 0)
   bf16_t* gs = xs + MR * K;  // NORM: gamma [K]
+  // PRO 2: rows whose attention ran in more than one split are merged below (flash-decoding merge,
+  // decode_reduce_kernel's arithmetic); the attention kernel wrote the others into x itself
+  int nsp[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+    nsp[m] = PRO == 2 ? max(0, min((g.ctx[m] + g.split - 1) / g.split, g.max_splits)) : 1;
   for (int c0 = wv * 64; c0 < nch; c0 += 256) {
 #pragma unroll
     for (int m = 0; m < MR; ++m)
-      __builtin_amdgcn_global_load_lds((gemv_gptr)(g.x + (long)m * g.ldx + (c0 + lane) * 8),
-                                       (gemv_lptr)(xs + m * K + c0 * 8), 16, 0, 0);
+      if (nsp[m] <= 1)
+        __builtin_amdgcn_global_load_lds((gemv_gptr)(g.x + (long)m * g.ldx + (c0 + lane) * 8),
+                                         (gemv_lptr)(xs + m * K + c0 * 8), 16, 0, 0);
     if constexpr (NORM)
       __builtin_amdgcn_global_load_lds((gemv_gptr)(g.gamma + (c0 + lane) * 8), (gemv_lptr)(gs + c0 * 8), 16, 0, 0);
+  }
+  if constexpr (PRO == 2) {
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      const int ns = nsp[m];
+      if (ns <= 1) continue;
+      for (int c = threadIdx.x; c < nch; c += 256) {
+        const int e0 = c * 8, h = e0 / g.D, d0 = e0 - h * g.D;
+        const long base = ((long)m * g.Hq + h) * g.max_splits;
+        float Mx = -INFINITY;
+        for (int q = 0; q < ns; ++q) Mx = fmaxf(Mx, g.pml[(base + q) * 2]);
+        if (Mx == -INFINITY) Mx = 0.f;
+        float den = 0.f, num[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+        for (int q = 0; q < ns; ++q) {
+          const float f = exp2f(g.pml[(base + q) * 2] - Mx);
+          den += f * g.pml[(base + q) * 2 + 1];
+          const floatx4 a = *reinterpret_cast<const floatx4*>(g.po + (base + q) * g.D + d0);
+          const floatx4 b = *reinterpret_cast<const floatx4*>(g.po + (base + q) * g.D + d0 + 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            num[j] += f * a[j];
+            num[j + 4] += f * b[j];
+          }
+        }
+        float y[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = den > 0.f ? num[j] / den : 0.f;
+        store8(xs + m * K + e0, y);
+      }
+    }
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (lgkmcnt / expcnt untouched)
   __syncthreads();
@@ -281,8 +325,9 @@ constexpr int kGemvMaxLds = 163840 - 1024;  // dynamic LDS opt-in (the static `r
 int g_gemv_wgs = 0;  // target workgroup count (0: the default below)
 int g_gemv_pf = 0;   // W prefetch before the prologue (ops.GEMV_PREFETCH)
 
-template <int MR, bool NORM, int MODE>
+template <int MR, int PRO, int MODE>
 int launch_u(const GemvArgs& a, int U, hipStream_t st) {
+  constexpr bool NORM = PRO == 1;
   int target = g_gemv_wgs > 0 ? g_gemv_wgs : 512;
   int wgs = (a.npairs + 3) / 4;
   if (wgs > target) wgs = target;
@@ -291,11 +336,11 @@ int launch_u(const GemvArgs& a, int U, hipStream_t st) {
 #define LK_GEMV_U(UU)                                                                  \
   if (U == UU) {                                                                       \
     if (g_gemv_pf) {                                                                   \
-      LK_SET_MAX_LDS((gemv_decode_kernel<MR, NORM, MODE, UU, true>), kGemvMaxLds);     \
-      gemv_decode_kernel<MR, NORM, MODE, UU, true><<<wgs, 256, lds, st>>>(a);          \
+      LK_SET_MAX_LDS((gemv_decode_kernel<MR, PRO, MODE, UU, true>), kGemvMaxLds);     \
+      gemv_decode_kernel<MR, PRO, MODE, UU, true><<<wgs, 256, lds, st>>>(a);          \
     } else {                                                                           \
-      LK_SET_MAX_LDS((gemv_decode_kernel<MR, NORM, MODE, UU, false>), kGemvMaxLds);    \
-      gemv_decode_kernel<MR, NORM, MODE, UU, false><<<wgs, 256, lds, st>>>(a);         \
+      LK_SET_MAX_LDS((gemv_decode_kernel<MR, PRO, MODE, UU, false>), kGemvMaxLds);    \
+      gemv_decode_kernel<MR, PRO, MODE, UU, false><<<wgs, 256, lds, st>>>(a);         \
     }                                                                                  \
   } else
   LK_GEMV_U(8) LK_GEMV_U(7) LK_GEMV_U(4) return -4;
@@ -312,12 +357,12 @@ int pick_u(int K) {
   return 0;
 }
 
-template <bool NORM, int MODE>
+template <int PRO, int MODE>
 int launch_m(const GemvArgs& a, hipStream_t st) {
   const int U = pick_u(a.K);
   if (!U || a.K % 512) return -2;
-  if (a.M == 1) return launch_u<1, NORM, MODE>(a, U, st);
-  if (a.M == 2) return launch_u<2, NORM, MODE>(a, U, st);
+  if (a.M == 1) return launch_u<1, PRO, MODE>(a, U, st);
+  if (a.M == 2) return launch_u<2, PRO, MODE>(a, U, st);
   return -2;
 }
 
@@ -344,7 +389,7 @@ void lk_gemv_set_prefetch(int on) { g_gemv_pf = on ? 1 : 0; }
 int lk_gemv_decode(int mode, const bf16_t* x, long ldx, const bf16_t* gamma, float eps, const bf16_t* w, int M, int N,
                    int K, bf16_t* out, long ldo, bf16_t* res, long ldr, const int* positions, const float* cos_sin,
                    int Hq, int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,
-                   hipStream_t st) {
+                   const float* po, const float* pml, const int* ctx, int max_splits, int split, hipStream_t st) {
   if (!lk_gemv_supported(M, N, K, mode) || !x || !w || ldx % 8) return -1;
   GemvArgs a;
   a.x = x;
@@ -392,8 +437,21 @@ int lk_gemv_decode(int mode, const bf16_t* x, long ldx, const bf16_t* gamma, flo
       return -1;
   }
   const bool norm = gamma != nullptr;
+  if (po) {  // the split merge prologue: the O projection (mode 1) only, no norm
+    if (mode != 1 || norm || !pml || !ctx || Hq <= 0 || D <= 0 || D % 8 || Hq * D != K || max_splits < 1 ||
+        split < 1)
+      return -1;
+    a.po = po;
+    a.pml = pml;
+    a.ctx = ctx;
+    a.Hq = Hq;
+    a.D = D;
+    a.max_splits = max_splits;
+    a.split = split;
+    return launch_m<2, 1>(a, st);
+  }
 #define LK_GEMV_MODE(MD)                                             \
-  if (mode == MD) return norm ? launch_m<true, MD>(a, st) : launch_m<false, MD>(a, st);
+  if (mode == MD) return norm ? launch_m<1, MD>(a, st) : launch_m<0, MD>(a, st);
   LK_GEMV_MODE(0) LK_GEMV_MODE(1) LK_GEMV_MODE(2) LK_GEMV_MODE(3)
 #undef LK_GEMV_MODE
   return -1;

@@ -43,7 +43,7 @@ int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, i
               bf16_t* out, long ldo, float* part, hipStream_t st);
 
 // gemv_decode.hip (decode GEMV for M <= 2 rows; mode 0 out, 1 res += out, 2 SwiGLU, 3 RoPE + paged KV;
-// gamma != nullptr: RMSNorm prologue over x)
+// gamma != nullptr: RMSNorm prologue over x; po != nullptr (mode 1): x = the paged-decode split merge)
 int lk_gemv_supported(int M, int N, int K, int mode);
 void lk_gemv_set_wgs(int wgs);
 void lk_gemv_set_prefetch(int on);
@@ -51,7 +51,7 @@ int lk_l3_prefetch(const void* p, long bytes, int wgs, unsigned* sink, hipStream
 int lk_gemv_decode(int mode, const bf16_t* x, long ldx, const bf16_t* gamma, float eps, const bf16_t* w, int M, int N,
                    int K, bf16_t* out, long ldo, bf16_t* res, long ldr, const int* positions, const float* cos_sin,
                    int Hq, int Hkv, int D, bf16_t* kc, bf16_t* vc, const int* slots, int BS, int neox,
-                   hipStream_t st);
+                   const float* po, const float* pml, const int* ctx, int max_splits, int split, hipStream_t st);
 
 // GEMM part only (S >= 2): f32 partial slabs part[S][M][N], for a consumer that fuses the
 // split-K reduction (lk_splitk_rmsnorm, lk_splitk_rope_kv)

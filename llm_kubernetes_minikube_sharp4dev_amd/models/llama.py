@@ -246,6 +246,14 @@ class LlamaModel(nn.Module):
             I = self.layers[0].gate_up.shape[0] // 2
             rows = min(I, (ops.GEMV_L3_MB << 20) // (2 * self.layers[0].gate_up.stride(0) * 2))
         main = torch.cuda.current_stream(res.device) if side is not None else None
+        # O merges the split partials itself (ops.GEMV_MERGE): paged decode without its reduce launch
+        M = res.shape[0]
+        po, pml = meta.part_o, meta.part_ml
+        merge = (ops.GEMV_MERGE and ops.DECODE_FUSED_REDUCE != 2 and meta.max_splits is not None
+                 and meta.decode_split is not None and meta.block_tables_d is not None)
+        if merge and (po is None or po.shape[0] < M or po.shape[2] != meta.max_splits):
+            po = torch.empty(M, hq, meta.max_splits, D, dtype=torch.float32, device=res.device)
+            pml = torch.empty(M, hq, meta.max_splits, 2, dtype=torch.float32, device=res.device)
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
             qkv = ops.gemv_decode(3, res, L.qkv, L.input_norm, eps, positions=meta.positions, cos_sin=self.cos_sin,
@@ -258,8 +266,17 @@ class LlamaModel(nn.Module):
                     if rows:
                         ops.l3_prefetch(L.gate_up, 0, rows)
                         ops.l3_prefetch(L.gate_up, I, I + rows)
-            attn_out = paged_attention(qkv, kc, vc, meta, hq, hkv, D, self.scale, attn_out)
-            ops.gemv_decode(1, attn_out, L.o, res=res)
+            if merge:
+                attn_out = attn_out if attn_out is not None else torch.empty(M, hq * D, dtype=res.dtype,
+                                                                              device=res.device)
+                ops.paged_decode(qkv[:, : hq * D].view(M, hq, D), kc, vc, meta.block_tables_d, meta.ctx_lens_d,
+                                 self.scale, meta.max_splits, po, pml, out=attn_out.view(M, hq, D),
+                                 split=meta.decode_split, reduce=False)
+                ops.gemv_decode(1, attn_out, L.o, res=res, po=po, pml=pml, ctx=meta.ctx_lens_d,
+                                max_splits=meta.max_splits, split=meta.decode_split, Hq=hq, D=D)
+            else:
+                attn_out = paged_attention(qkv, kc, vc, meta, hq, hkv, D, self.scale, attn_out)
+                ops.gemv_decode(1, attn_out, L.o, res=res)
             a = ops.gemv_decode(2, res, L.gate_up, L.post_norm, eps)
             ops.gemv_decode(1, a, L.down, res=res)
         if side is not None:

@@ -875,6 +875,10 @@ def ws_pro(x, w, plan, kind: int, swiglu: bool = False, reduce: bool = False, **
 # or RoPE launch (models/llama.py _forward_decode_gemv).  LK_DECODE_GEMV=0: the weight-streaming path.
 GEMV = os.environ.get("LK_DECODE_GEMV", "1") != "0"
 GEMV_MAX_M = 2
+# LK_GEMV_MERGE=1: the O projection's GEMV merges the paged-decode split partials itself (no
+# decode_reduce launch).  Measured slightly slower at batch 1 (decode step 3.129 / 3.133 vs 3.104 /
+# 3.110 ms: every workgroup re-reads all split partials), so the reduce kernel stays the default
+GEMV_MERGE = os.environ.get("LK_GEMV_MERGE", "0") == "1"
 _GEMV_OK: dict = {}
 
 
@@ -923,13 +927,18 @@ def _gemv_ok(x, w, mode: int) -> bool:
 
 
 def gemv_decode(mode: int, x, w, gamma=None, eps: float = 1e-5, res=None, positions=None, cos_sin=None,
-                Hq: int = 0, Hkv: int = 0, D: int = 0, k_cache=None, v_cache=None, slots=None, neox: bool = True):
+                Hq: int = 0, Hkv: int = 0, D: int = 0, k_cache=None, v_cache=None, slots=None, neox: bool = True,
+                po=None, pml=None, ctx=None, max_splits: int = 0, split: int = 0):
     """mode 0: x W^T; 1: ``res`` += x W^T in place (returned); 2: SwiGLU(x [Wg; Wu]^T) [M, N/2];
     3: packed QKV with RoPE applied to q (and to k in the paged cache, k kept unrotated in the
-    row), K/V written at ``slots``.  ``gamma``: the GEMV's input is RMSNorm(x) * gamma."""
+    row), K/V written at ``slots``.  ``gamma``: the GEMV's input is RMSNorm(x) * gamma.  ``po`` /
+    ``pml`` (mode 1, GPU): x's rows that :func:`paged_decode` (``reduce=False``) left as split
+    partials are merged in the GEMV's prologue (no decode_reduce launch)."""
     if use_hip(x):
         return lib().gemv_decode(mode, x, w, gamma, eps, res, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache,
-                                 slots, neox)
+                                 slots, neox, po, pml, ctx, max_splits, split)
+    if po is not None:
+        raise NotImplementedError("gemv_decode: the split-merge prologue is a GPU kernel")
     xin = ref.rmsnorm(x, gamma, eps) if gamma is not None else x
     y = xin.float() @ w.float().t()
     if mode == 0:

@@ -105,6 +105,50 @@ def test_gemv_qkv_rope_kv(hip, M, neox, heads):
     assert kc.float().abs().sum() > 0 and torch.count_nonzero(kc.float()) == Hkv * D
 
 
+@pytest.mark.parametrize("M", [1, 2])
+@pytest.mark.parametrize("ctx", [(700, 100), (1000, 2000), (64, 90)])
+def test_gemv_o_merges_decode_splits(hip, M, ctx):
+    """Mode 1 with the split-merge prologue: paged_decode(reduce=False) leaves multi-split rows as
+    partials, the O projection's GEMV merges them (decode_reduce_kernel's arithmetic) -- the new
+    residual equals decode_reduce -> plain GEMV; one-split rows pass through unmerged."""
+    Hkv, G, D, BS = 8, 4, 128, 16
+    Hq = Hkv * G
+    g = torch.Generator().manual_seed(sum(ctx) + M)
+    ctx = list(ctx)[:M]
+    nblk = [(c + BS - 1) // BS for c in ctx]
+    NB = sum(nblk) + 2
+    kc = torch.randn(NB, Hkv, BS, D, generator=g).to(DEV, torch.bfloat16)
+    vc = torch.randn(NB, Hkv, BS, D, generator=g).to(DEV, torch.bfloat16)
+    width = 2048 // BS
+    bt = torch.zeros(M, width, dtype=torch.int32)
+    p = 0
+    for b in range(M):
+        for j in range(nblk[b]):
+            bt[b, j] = p
+            p += 1
+    bt = bt.to(DEV)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    q = torch.randn(M, Hq, D, generator=g).to(DEV, torch.bfloat16)
+    split = 128
+    ms = ops.decode_splits(width * BS, split)
+    w = (torch.randn(4096, Hq * D, generator=g) * 0.02).to(DEV, torch.bfloat16)
+    res = torch.randn(M, 4096, generator=g).to(DEV, torch.bfloat16)
+    scale = 1.0 / D ** 0.5
+    po = torch.empty(M, Hq, ms, D, device=DEV)
+    pml = torch.empty(M, Hq, ms, 2, device=DEV)
+    attn_ref = torch.empty(M, Hq, D, device=DEV, dtype=torch.bfloat16)
+    ops.paged_decode(q, kc, vc, bt, cl, scale, ms, po.clone(), pml.clone(), out=attn_ref, split=split)
+    want = res.clone()
+    hip.gemv_decode(1, attn_ref.view(M, Hq * D), w, res=want)
+    attn = torch.full((M, Hq, D), 7.0, device=DEV, dtype=torch.bfloat16)
+    ops.paged_decode(q, kc, vc, bt, cl, scale, ms, po, pml, out=attn, split=split, reduce=False)
+    got = res.clone()
+    hip.gemv_decode(1, attn.view(M, Hq * D), w, res=got, po=po, pml=pml, ctx=cl, max_splits=ms, split=split,
+                    Hq=Hq, D=D)
+    torch.cuda.synchronize()
+    _close(got, want, 0.02, 0.005, f"merged O M{M} ctx{ctx}")
+
+
 def test_gemv_rejects_unsupported(hip):
     x = torch.randn(3, 4096, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(4096, 4096, device=DEV, dtype=torch.bfloat16)
