@@ -101,25 +101,13 @@ __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
       rb = ra + 1;
     }
   };
-  // PF: the first K block of this wave's first pair is requested before X is staged, so the W
-  // stream starts at the kernel's first instruction instead of after the prologue's loads and
-  // barriers (costs VGPRs: the block stays live across the prologue)
   const int nwaves = gridDim.x * 4;
   const int kc_lane = nch >> 6;  // chunks per lane (K % 512 == 0)
   const int p0 = blockIdx.x * 4 + wv;
-  uint4_t va[U], vb[U];
-  if (PF && p0 < g.npairs) {
-    long ra, rb;
-    int hd, head, ip;
-    pair_rows(p0, ra, rb, hd, head, ip);
-    const uint4_t* wa = reinterpret_cast<const uint4_t*>(g.w + ra * K) + lane;
-    const uint4_t* wb = reinterpret_cast<const uint4_t*>(g.w + rb * K) + lane;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      va[u] = __builtin_nontemporal_load(wa + u * 64);
-      vb[u] = __builtin_nontemporal_load(wb + u * 64);
-    }
-  }
+  // PF: the first K block of this wave's first pair comes in by LDS-DMA (into a wave-private LDS
+  // slot, no registers) issued right behind X's, so the W stream starts with the prologue instead
+  // of after its loads and barriers
+  bf16_t* wpf = xs + (MR + (NORM ? 1 : 0)) * K + wv * (2 * U * 512);  // [2U][64 lanes x 8]
 
   // ---- stage X (with the RMSNorm prologue) into LDS.  The rows (and gamma) come in by LDS-DMA
   // (global_load_lds: no registers, every chunk's load in flight at once, one memory round trip
@@ -140,6 +128,18 @@ __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
                                          (gemv_lptr)(xs + m * K + c0 * 8), 16, 0, 0);
     if constexpr (NORM)
       __builtin_amdgcn_global_load_lds((gemv_gptr)(g.gamma + (c0 + lane) * 8), (gemv_lptr)(gs + c0 * 8), 16, 0, 0);
+  }
+  if (PF && p0 < g.npairs) {
+    long ra, rb;
+    int hd, head, ip;
+    pair_rows(p0, ra, rb, hd, head, ip);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      __builtin_amdgcn_global_load_lds((gemv_gptr)(g.w + ra * K + (lane + 64 * u) * 8), (gemv_lptr)(wpf + u * 512),
+                                       16, 0, 2);
+      __builtin_amdgcn_global_load_lds((gemv_gptr)(g.w + rb * K + (lane + 64 * u) * 8),
+                                       (gemv_lptr)(wpf + (U + u) * 512), 16, 0, 2);
+    }
   }
   if constexpr (PRO == 2) {
 #pragma unroll
@@ -172,7 +172,13 @@ __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
       }
     }
   }
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (lgkmcnt / expcnt untouched)
+  // X (and gamma) landed; the W block issued after them may stay in flight (vmcnt retires in order)
+  if (PF && p0 < g.npairs) {
+    constexpr int n = 2 * U;  // vmcnt(n): bits 3:0 and 15:14
+    __builtin_amdgcn_s_waitcnt(0x0F70 | (n & 0xF) | ((n >> 4) << 14));
+  } else {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (lgkmcnt / expcnt untouched)
+  }
   __syncthreads();
   if constexpr (NORM) {
     // RMSNorm with rmsnorm_kernel's rounding: y = bf16(bf16(v * inv) * g), in place in LDS
@@ -223,7 +229,15 @@ __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
 #pragma unroll
     for (int m = 0; m < MR; ++m) acc_a[m] = acc_b[m] = 0.f;
     for (int j0 = 0; j0 < kc_lane; j0 += U) {
-      if (!PF || p != p0 || j0 != 0) {  // (PF: the first block came in before the prologue)
+      uint4_t va[U], vb[U];
+      if (PF && p == p0 && j0 == 0) {  // the block prefetched into this wave's LDS slot
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMAs landed
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          va[u] = *reinterpret_cast<const uint4_t*>(wpf + u * 512 + lane * 8);
+          vb[u] = *reinterpret_cast<const uint4_t*>(wpf + (U + u) * 512 + lane * 8);
+        }
+      } else {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           va[u] = __builtin_nontemporal_load(wa + (j0 + u) * 64);
@@ -323,7 +337,7 @@ __global__ __launch_bounds__(256) void l3_prefetch_kernel(const uint4_t* __restr
 
 constexpr int kGemvMaxLds = 163840 - 1024;  // dynamic LDS opt-in (the static `red` stays below)
 int g_gemv_wgs = 0;  // target workgroup count (0: the default below)
-int g_gemv_pf = 0;   // W prefetch before the prologue (ops.GEMV_PREFETCH)
+int g_gemv_pf = 0;   // W prefetch (LDS-DMA) beside the prologue (ops.GEMV_PREFETCH; slower)
 
 template <int MR, int PRO, int MODE>
 int launch_u(const GemvArgs& a, int U, hipStream_t st) {
@@ -331,11 +345,15 @@ int launch_u(const GemvArgs& a, int U, hipStream_t st) {
   int target = g_gemv_wgs > 0 ? g_gemv_wgs : 512;
   int wgs = (a.npairs + 3) / 4;
   if (wgs > target) wgs = target;
-  const size_t lds = (size_t)(MR + (NORM ? 1 : 0)) * a.K * 2;  // X rows (+ gamma)
-  if (lds > kGemvMaxLds) return -3;
+  const size_t lds0 = (size_t)(MR + (NORM ? 1 : 0)) * a.K * 2;  // X rows (+ gamma)
+  if (lds0 > kGemvMaxLds) return -3;
+  // the W prefetch slots (4 waves x 2U KB) only where two workgroups per CU still fit
+  const size_t lds_pf = lds0 + (size_t)4 * 2 * U * 1024;
+  const bool pf = g_gemv_pf && lds_pf <= 81920;
+  const size_t lds = pf ? lds_pf : lds0;
 #define LK_GEMV_U(UU)                                                                  \
   if (U == UU) {                                                                       \
-    if (g_gemv_pf) {                                                                   \
+    if (pf) {                                                                          \
       LK_SET_MAX_LDS((gemv_decode_kernel<MR, PRO, MODE, UU, true>), kGemvMaxLds);     \
       gemv_decode_kernel<MR, PRO, MODE, UU, true><<<wgs, 256, lds, st>>>(a);          \
     } else {                                                                           \

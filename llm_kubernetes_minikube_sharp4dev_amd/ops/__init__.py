@@ -882,9 +882,10 @@ GEMV_MERGE = os.environ.get("LK_GEMV_MERGE", "0") == "1"
 _GEMV_OK: dict = {}
 
 
-# W prefetch before the GEMV's X prologue (LK_GEMV_PREFETCH=1: on; measured slower -- the block
-# held across the prologue costs a wave per SIMD: batch-1 decode step 3.199 vs 3.17 ms,
-# profiles/r6_gemv/), workgroup target (0: 512)
+# W prefetch beside the GEMV's X prologue: the first K block of each wave's first pair by LDS-DMA
+# into a wave-private LDS slot where two workgroups per CU still fit (LK_GEMV_PREFETCH=1).  Measured
+# slower (batch-1 decode step 3.31 vs 3.10 ms; QKV 16.5 vs 11.7 us; a register-held version: 3.199
+# vs 3.17 ms; profiles/r6_gemv/): off.  Workgroup target (LK_GEMV_WGS, 0: 512)
 GEMV_PREFETCH = os.environ.get("LK_GEMV_PREFETCH", "0") == "1"
 GEMV_WGS = int(os.environ.get("LK_GEMV_WGS", "0") or 0)
 
