@@ -44,7 +44,7 @@ def main():
     ap.add_argument("--shapes", default="qkv,o,gate_up,down,lm_head")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--md", default=None)
-    ap.add_argument("--prefetch", default="1,0", help="GEMV W prefetch before the prologue: arms")
+    ap.add_argument("--ksplit", default="1,0", help="GEMV two waves per pair on long-K shapes: arms")
     a = ap.parse_args()
     L = ops.lib()
     M, dev, eps = a.m, "cuda", 1e-5
@@ -54,8 +54,8 @@ def main():
     slots = torch.arange(M, dtype=torch.int32, device=dev) + 5 * BS
     kc = torch.zeros(64, Hkv, BS, D, device=dev, dtype=torch.bfloat16)
     vc = torch.zeros_like(kc)
-    arms = [(w, pf) for pf in a.prefetch.split(",") for w in a.wgs.split(",")]
-    lines = ["| shape | MB | ws path us (TB/s) | " + " | ".join(f"gemv wgs {w} pf {pf} us (TB/s)" for w, pf in arms) + " |",
+    arms = [(w, pf) for pf in a.ksplit.split(",") for w in a.wgs.split(",")]
+    lines = ["| shape | MB | ws path us (TB/s) | " + " | ".join(f"gemv wgs {w} ksplit {pf} us (TB/s)" for w, pf in arms) + " |",
              "|---|---|---|" + "---|" * len(arms)]
     for name in a.shapes.split(","):
         N, K, mode, norm = SHAPES[name]
@@ -89,16 +89,16 @@ def main():
             else:
                 L.gemv_decode(0, x, w)
 
-        arms = [(w, pf) for pf in a.prefetch.split(",") for w in a.wgs.split(",")]
+        arms = [(w, pf) for pf in a.ksplit.split(",") for w in a.wgs.split(",")]
         t_ws, t_gv = [], {arm: [] for arm in arms}
         for _ in range(a.rounds):
             t_ws.append(timed(ws, copies))
             for wg, pf in t_gv:
                 L.gemv_set_wgs(int(wg))
-                L.gemv_set_prefetch(pf == "1")
+                L.gemv_set_ksplit(pf == "1")
                 t_gv[(wg, pf)].append(timed(gv, copies))
         L.gemv_set_wgs(0)
-        L.gemv_set_prefetch(True)
+        L.gemv_set_ksplit(True)
         mb = wb / 2**20
 
         def fmt(ts):

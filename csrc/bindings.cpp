@@ -1167,7 +1167,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return lk_gemv_supported((int)M, (int)N, (int)K, (int)mode) != 0;
   });
   m.def("gemv_set_wgs", [](int64_t n) { lk_gemv_set_wgs((int)n); });
-  m.def("gemv_set_prefetch", [](bool on) { lk_gemv_set_prefetch(on ? 1 : 0); });
+  m.def("gemv_set_ksplit", [](bool on) { lk_gemv_set_ksplit(on ? 1 : 0); });
   // read rows [r0, r1) of a contiguous 2-D tensor through the Infinity Cache (lk_l3_prefetch)
   m.def("l3_prefetch", [](const at::Tensor& t, int64_t r0, int64_t r1, int64_t wgs, at::Tensor& sink) {
     CHECK_CUDA(t); CHECK_CONTIG(t); CHECK_CUDA(sink);

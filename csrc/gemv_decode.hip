@@ -70,7 +70,7 @@ LK_DEVICE void dot8(const uint4_t wv, const uint4_t xv, float& acc) {
   }
 }
 
-template <int MR, int PRO, int MODE, int U, bool PF>
+template <int MR, int PRO, int MODE, int U, int KW>
 __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
   constexpr bool NORM = PRO == 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -101,13 +101,7 @@ __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
       rb = ra + 1;
     }
   };
-  const int nwaves = gridDim.x * 4;
   const int kc_lane = nch >> 6;  // chunks per lane (K % 512 == 0)
-  const int p0 = blockIdx.x * 4 + wv;
-  // PF: the first K block of this wave's first pair comes in by LDS-DMA (into a wave-private LDS
-  // slot, no registers) issued right behind X's, so the W stream starts with the prologue instead
-  // of after its loads and barriers
-  bf16_t* wpf = xs + (MR + (NORM ? 1 : 0)) * K + wv * (2 * U * 512);  // [2U][64 lanes x 8]
 
   // ---- stage X (with the RMSNorm prologue) into LDS.  The rows (and gamma) come in by LDS-DMA
   // (global_load_lds: no registers, every chunk's load in flight at once, one memory round trip
@@ -128,18 +122,6 @@ __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
                                          (gemv_lptr)(xs + m * K + c0 * 8), 16, 0, 0);
     if constexpr (NORM)
       __builtin_amdgcn_global_load_lds((gemv_gptr)(g.gamma + (c0 + lane) * 8), (gemv_lptr)(gs + c0 * 8), 16, 0, 0);
-  }
-  if (PF && p0 < g.npairs) {
-    long ra, rb;
-    int hd, head, ip;
-    pair_rows(p0, ra, rb, hd, head, ip);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      __builtin_amdgcn_global_load_lds((gemv_gptr)(g.w + ra * K + (lane + 64 * u) * 8), (gemv_lptr)(wpf + u * 512),
-                                       16, 0, 2);
-      __builtin_amdgcn_global_load_lds((gemv_gptr)(g.w + rb * K + (lane + 64 * u) * 8),
-                                       (gemv_lptr)(wpf + (U + u) * 512), 16, 0, 2);
-    }
   }
   if constexpr (PRO == 2) {
 #pragma unroll
@@ -172,13 +154,7 @@ __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
       }
     }
   }
-  // X (and gamma) landed; the W block issued after them may stay in flight (vmcnt retires in order)
-  if (PF && p0 < g.npairs) {
-    constexpr int n = 2 * U;  // vmcnt(n): bits 3:0 and 15:14
-    __builtin_amdgcn_s_waitcnt(0x0F70 | (n & 0xF) | ((n >> 4) << 14));
-  } else {
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (lgkmcnt / expcnt untouched)
-  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (lgkmcnt / expcnt untouched)
   __syncthreads();
   if constexpr (NORM) {
     // RMSNorm with rmsnorm_kernel's rounding: y = bf16(bf16(v * inv) * g), in place in LDS
@@ -217,40 +193,42 @@ __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
     __syncthreads();
   }
 
-  // ---- stream W: one pair of rows per wave at a time
-  for (int p = p0; p < g.npairs; p += nwaves) {
-    long ra, rb;
+  // ---- stream W: one pair of rows per KW waves at a time (KW = 2: the two waves take one half of
+  // K each and their sums meet in LDS -- twice the loads in flight for the long-K projections).
+  // The round loop is uniform over the workgroup (its barriers), a wave past the last pair idles.
+  constexpr int PPW = 4 / KW;  // pairs per workgroup per round
+  const int ps = wv / KW, kh = wv % KW;
+  const int kc_w = kc_lane / KW;  // chunks per lane of this wave's part of K
+  const int jb = kh * kc_w;
+  __shared__ float red2[KW > 1 ? PPW : 1][MR][2];
+  for (int pb = blockIdx.x * PPW; pb < g.npairs; pb += gridDim.x * PPW) {
+    const int p = pb + ps;
+    const bool valid = p < g.npairs;
+    long ra = 0, rb = 0;
     int hd = 0, head = 0, ip = 0;
-    pair_rows(p, ra, rb, hd, head, ip);
-    const uint4_t* wa = reinterpret_cast<const uint4_t*>(g.w + ra * K) + lane;
-    const uint4_t* wb = reinterpret_cast<const uint4_t*>(g.w + rb * K) + lane;
-    const uint4_t* xl = reinterpret_cast<const uint4_t*>(xs) + lane;
     float acc_a[MR], acc_b[MR];
 #pragma unroll
     for (int m = 0; m < MR; ++m) acc_a[m] = acc_b[m] = 0.f;
-    for (int j0 = 0; j0 < kc_lane; j0 += U) {
-      uint4_t va[U], vb[U];
-      if (PF && p == p0 && j0 == 0) {  // the block prefetched into this wave's LDS slot
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMAs landed
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          va[u] = *reinterpret_cast<const uint4_t*>(wpf + u * 512 + lane * 8);
-          vb[u] = *reinterpret_cast<const uint4_t*>(wpf + (U + u) * 512 + lane * 8);
-        }
-      } else {
+    if (valid) {
+      pair_rows(p, ra, rb, hd, head, ip);
+      const uint4_t* wa = reinterpret_cast<const uint4_t*>(g.w + ra * K) + lane;
+      const uint4_t* wb = reinterpret_cast<const uint4_t*>(g.w + rb * K) + lane;
+      const uint4_t* xl = reinterpret_cast<const uint4_t*>(xs) + lane;
+      for (int j0 = jb; j0 < jb + kc_w; j0 += U) {
+        uint4_t va[U], vb[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           va[u] = __builtin_nontemporal_load(wa + (j0 + u) * 64);
           vb[u] = __builtin_nontemporal_load(wb + (j0 + u) * 64);
         }
-      }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < U; ++u) {
 #pragma unroll
-        for (int m = 0; m < MR; ++m) {
-          const uint4_t xv = xl[m * nch + (j0 + u) * 64];
-          dot8(va[u], xv, acc_a[m]);
-          dot8(vb[u], xv, acc_b[m]);
+          for (int m = 0; m < MR; ++m) {
+            const uint4_t xv = xl[m * nch + (j0 + u) * 64];
+            dot8(va[u], xv, acc_a[m]);
+            dot8(vb[u], xv, acc_b[m]);
+          }
         }
       }
     }
@@ -259,6 +237,25 @@ __global__ __launch_bounds__(256) void gemv_decode_kernel(GemvArgs g) {
       acc_a[m] = wave_sum(acc_a[m]);
       acc_b[m] = wave_sum(acc_b[m]);
     }
+    if constexpr (KW > 1) {
+      static_assert(KW == 2, "two K halves");
+      if (kh == 1 && lane == 0)
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+          red2[ps][m][0] = acc_a[m];
+          red2[ps][m][1] = acc_b[m];
+        }
+      __syncthreads();
+      if (kh == 0)
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+          acc_a[m] += red2[ps][m][0];
+          acc_b[m] += red2[ps][m][1];
+        }
+      __syncthreads();  // (red2 is rewritten next round)
+      if (kh != 0) continue;
+    }
+    if (!valid) continue;
     if (lane != 0) continue;
 #pragma unroll
     for (int m = 0; m < MR; ++m) {
@@ -337,7 +334,7 @@ __global__ __launch_bounds__(256) void l3_prefetch_kernel(const uint4_t* __restr
 
 constexpr int kGemvMaxLds = 163840 - 1024;  // dynamic LDS opt-in (the static `red` stays below)
 int g_gemv_wgs = 0;  // target workgroup count (0: the default below)
-int g_gemv_pf = 0;   // W prefetch (LDS-DMA) beside the prologue (ops.GEMV_PREFETCH; slower)
+int g_gemv_ksplit = 1;  // two waves per pair on the long-K projections (ops.GEMV_KSPLIT)
 
 template <int MR, int PRO, int MODE>
 int launch_u(const GemvArgs& a, int U, hipStream_t st) {
@@ -345,20 +342,23 @@ int launch_u(const GemvArgs& a, int U, hipStream_t st) {
   int target = g_gemv_wgs > 0 ? g_gemv_wgs : 512;
   int wgs = (a.npairs + 3) / 4;
   if (wgs > target) wgs = target;
-  const size_t lds0 = (size_t)(MR + (NORM ? 1 : 0)) * a.K * 2;  // X rows (+ gamma)
-  if (lds0 > kGemvMaxLds) return -3;
-  // the W prefetch slots (4 waves x 2U KB) only where two workgroups per CU still fit
-  const size_t lds_pf = lds0 + (size_t)4 * 2 * U * 1024;
-  const bool pf = g_gemv_pf && lds_pf <= 81920;
-  const size_t lds = pf ? lds_pf : lds0;
+  const size_t lds = (size_t)(MR + (NORM ? 1 : 0)) * a.K * 2;  // X rows (+ gamma)
+  if (lds > kGemvMaxLds) return -3;
+  // two waves per pair (a K half each) where a pair's K walk is an even number >= 2 of U-blocks
+  const int blocks = a.K / 512 / U;
+  const bool ks2 = g_gemv_ksplit && blocks >= 2 && blocks % 2 == 0;
+  if (ks2) {
+    wgs = (a.npairs + 1) / 2;
+    if (wgs > 2 * target) wgs = 2 * target;
+  }
 #define LK_GEMV_U(UU)                                                                  \
   if (U == UU) {                                                                       \
-    if (pf) {                                                                          \
-      LK_SET_MAX_LDS((gemv_decode_kernel<MR, PRO, MODE, UU, true>), kGemvMaxLds);     \
-      gemv_decode_kernel<MR, PRO, MODE, UU, true><<<wgs, 256, lds, st>>>(a);          \
+    if (ks2) {                                                                         \
+      LK_SET_MAX_LDS((gemv_decode_kernel<MR, PRO, MODE, UU, 2>), kGemvMaxLds);        \
+      gemv_decode_kernel<MR, PRO, MODE, UU, 2><<<wgs, 256, lds, st>>>(a);             \
     } else {                                                                           \
-      LK_SET_MAX_LDS((gemv_decode_kernel<MR, PRO, MODE, UU, false>), kGemvMaxLds);    \
-      gemv_decode_kernel<MR, PRO, MODE, UU, false><<<wgs, 256, lds, st>>>(a);         \
+      LK_SET_MAX_LDS((gemv_decode_kernel<MR, PRO, MODE, UU, 1>), kGemvMaxLds);        \
+      gemv_decode_kernel<MR, PRO, MODE, UU, 1><<<wgs, 256, lds, st>>>(a);             \
     }                                                                                  \
   } else
   LK_GEMV_U(8) LK_GEMV_U(7) LK_GEMV_U(4) return -4;
@@ -402,7 +402,7 @@ int lk_l3_prefetch(const void* p, long bytes, int wgs, unsigned* sink, hipStream
   LK_CHECK_LAUNCH();
   return 0;
 }
-void lk_gemv_set_prefetch(int on) { g_gemv_pf = on ? 1 : 0; }
+void lk_gemv_set_ksplit(int on) { g_gemv_ksplit = on ? 1 : 0; }
 
 int lk_gemv_decode(int mode, const bf16_t* x, long ldx, const bf16_t* gamma, float eps, const bf16_t* w, int M, int N,
                    int K, bf16_t* out, long ldo, bf16_t* res, long ldr, const int* positions, const float* cos_sin,

@@ -46,7 +46,7 @@ int lk_wsgemm(const bf16_t* x, long ldx, const bf16_t* w, int M, int N, int K, i
 // gamma != nullptr: RMSNorm prologue over x; po != nullptr (mode 1): x = the paged-decode split merge)
 int lk_gemv_supported(int M, int N, int K, int mode);
 void lk_gemv_set_wgs(int wgs);
-void lk_gemv_set_prefetch(int on);
+void lk_gemv_set_ksplit(int on);
 int lk_l3_prefetch(const void* p, long bytes, int wgs, unsigned* sink, hipStream_t st);
 int lk_gemv_decode(int mode, const bf16_t* x, long ldx, const bf16_t* gamma, float eps, const bf16_t* w, int M, int N,
                    int K, bf16_t* out, long ldo, bf16_t* res, long ldr, const int* positions, const float* cos_sin,

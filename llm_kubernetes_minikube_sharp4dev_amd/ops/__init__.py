@@ -882,11 +882,12 @@ GEMV_MERGE = os.environ.get("LK_GEMV_MERGE", "0") == "1"
 _GEMV_OK: dict = {}
 
 
-# W prefetch beside the GEMV's X prologue: the first K block of each wave's first pair by LDS-DMA
-# into a wave-private LDS slot where two workgroups per CU still fit (LK_GEMV_PREFETCH=1).  Measured
-# slower (batch-1 decode step 3.31 vs 3.10 ms; QKV 16.5 vs 11.7 us; a register-held version: 3.199
-# vs 3.17 ms; profiles/r6_gemv/): off.  Workgroup target (LK_GEMV_WGS, 0: 512)
-GEMV_PREFETCH = os.environ.get("LK_GEMV_PREFETCH", "0") == "1"
+# The long-K projections (K split into an even number >= 2 of streaming blocks: down at K 14,336,
+# the 70B QKV / gate_up at K 8,192) take two waves per pair of W rows, a K half each, their sums
+# joined in LDS (LK_GEMV_KSPLIT=0: one wave per pair).  Tried and removed: the first W block
+# prefetched before the X prologue, in registers (batch-1 decode step 3.199 vs 3.17 ms) and by
+# LDS-DMA (3.31 vs 3.10; profiles/r6_gemv/).  Workgroup target (LK_GEMV_WGS, 0: 512)
+GEMV_KSPLIT = os.environ.get("LK_GEMV_KSPLIT", "1") != "0"
 GEMV_WGS = int(os.environ.get("LK_GEMV_WGS", "0") or 0)
 
 
@@ -912,7 +913,7 @@ def gemv_supported(M: int, N: int, K: int, mode: int) -> bool:
     ok = _GEMV_OK.get(key)
     if ok is None:
         if not _GEMV_OK:  # first use: the launch knobs
-            lib().gemv_set_prefetch(GEMV_PREFETCH)
+            lib().gemv_set_ksplit(GEMV_KSPLIT)
             lib().gemv_set_wgs(GEMV_WGS)
         ok = _GEMV_OK[key] = bool(lib().gemv_supported(M, N, K, mode))
     return ok

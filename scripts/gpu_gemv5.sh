@@ -4,7 +4,7 @@ R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out/gemv5
 timeout -k 10 400 python -u -m pytest tests/test_gemv_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/gemv5/pytest.log 2>&1 || { tail -40 gpurun_out/gemv5/pytest.log; exit 91; }
 tail -1 gpurun_out/gemv5/pytest.log
-timeout -k 10 300 python benchmarks/gemv_bench.py --m 1 --wgs 512 --prefetch 1,0 --md gpurun_out/gemv5/bench_m1.md > gpurun_out/gemv5/bench.log 2>&1 || { tail gpurun_out/gemv5/bench.log; exit 92; }
+timeout -k 10 300 python benchmarks/gemv_bench.py --m 1 --wgs 512 --ksplit 1,0 --md gpurun_out/gemv5/bench_m1.md > gpurun_out/gemv5/bench.log 2>&1 || { tail gpurun_out/gemv5/bench.log; exit 92; }
 cat gpurun_out/gemv5/bench_m1.md
 for i in 1 2; do
   for x in 1 0; do

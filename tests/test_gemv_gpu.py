@@ -61,6 +61,28 @@ def test_gemv_residual(hip, M, NK):
 
 
 @pytest.mark.parametrize("M", [1, 2])
+@pytest.mark.parametrize("NK", [(4096, 14336), (1280, 8192)])
+def test_gemv_ksplit_arms_agree(hip, M, NK):
+    """Long-K shapes run two waves per pair (a K half each, joined in LDS); with the split off one
+    wave walks all of K -- both against the fp32 reference and each other."""
+    N, K = NK
+    torch.manual_seed(N + M)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.02
+    want = x.float() @ w.float().t()
+    try:
+        outs = []
+        for on in (True, False):
+            hip.gemv_set_ksplit(on)
+            outs.append(hip.gemv_decode(0, x, w))
+    finally:
+        hip.gemv_set_ksplit(ops.GEMV_KSPLIT)
+    for y in outs:
+        _close(y, want, 0.02, 0.01, f"gemv M{M} N{N} K{K}")
+    _close(outs[0], outs[1], 0.01, 0.005, "ksplit arms")
+
+
+@pytest.mark.parametrize("M", [1, 2])
 @pytest.mark.parametrize("IK", [(14336, 4096), (3584, 8192)])
 def test_gemv_swiglu_norm(hip, M, IK):
     I, K = IK
