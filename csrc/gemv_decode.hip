@@ -9,9 +9,12 @@
 //     (lane l: chunks l, l + 64, ...: every wave load is one contiguous 1-KB segment of a row),
 //     U chunks of both rows in flight per lane; fp32 FMAs, 64-lane butterfly at the end -- no
 //     split-K, no partial slabs;
-//   * X (the M input rows) is staged once per workgroup in LDS; the NORM prologue computes
-//     RMSNorm(res) * gamma there itself (the rmsnorm kernel's exact arithmetic), so the
-//     producer of res never launches a norm;
+//   * long-K projections (an even number >= 2 of U-chunk blocks per row: down at K 14,336) give
+//     each pair two waves, a K half each, joined in LDS (KW = 2);
+//   * X (the M input rows) is staged once per workgroup in LDS by LDS-DMA; the NORM prologue
+//     computes RMSNorm(res) * gamma there itself (the rmsnorm kernel's exact arithmetic), so the
+//     producer of res never launches a norm; PRO 2 (the O projection, opt-in: measured slower)
+//     merges the paged-decode split partials there instead of a decode_reduce launch;
 //   * epilogues on the pair's two dot products: 0 plain bf16 out, 1 res += out (the residual
 //     stream updated in place, each element owned by one wave), 2 SwiGLU (pair = gate row p,
 //     up row I + p: the splitk_reduce_kernel<true> arithmetic), 3 RoPE + paged-KV write (pair =
