@@ -982,7 +982,12 @@ def linear_rope_kv(x, w, positions, cos_sin, Hq: int, Hkv: int, D: int, k_cache=
     """qkv = x W^T, then :func:`rope_kv_` on it (one launch fewer on split-K decode shapes; on
     prefill-sized steps of a folded model -- interleaved RoPE, e.g. the tensor-parallel block,
     where the whole fused chain does not apply -- the QKV GEMM's epilogue does the RoPE and the
-    paged-KV write)."""
+    paged-KV write).  Rows <= 2 (the tensor-parallel decode step at batch 1-2): the decode GEMV
+    with its RoPE + paged-KV epilogue."""
+    if (not write_k_inplace and k_cache is not None and slots is not None and _gemv_ok(x, w, 3)
+            and w.shape[0] == (Hq + 2 * Hkv) * D):
+        return lib().gemv_decode(3, x, w, None, 1e-5, None, positions, cos_sin, Hq, Hkv, D, k_cache, v_cache,
+                                 slots, neox)
     plan = _ws_split_plan(x, w)
     if plan is not None:
         # (rows <= 64: past that the last workgroup of a head reduces >= 128 KB of partials alone,

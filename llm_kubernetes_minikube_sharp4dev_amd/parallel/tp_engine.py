@@ -392,8 +392,12 @@ def make_tp_engine(model, tp: TPGroup, tokenizer=None, engine_kw: Optional[dict]
     return eng
 
 
+@torch.inference_mode()
 def tp_capture_all(engine, max_batch: Optional[int] = None, variants=(False, True)):
-    """Capture decode graphs on every rank in lockstep."""
+    """Capture decode graphs on every rank in lockstep -- under inference mode like the workers'
+    side and ModelRunner.capture_all: a graph captured earlier in the process under inference mode
+    (the batch-1 query-encoder graphs) leaves the CUDA generator's graph-state tensors as inference
+    tensors, which a capture outside inference mode may not update (capture_begin raised)."""
     r = engine.runner
     for B in r.graph_sizes:
         for v in variants:
