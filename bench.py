@@ -276,7 +276,7 @@ def main():
     # ---- embedder + index build (embedding work sharded over ALL ranks, all-gather over RCCL;
     # every replica driver then holds the whole corpus in HBM: 1M x 768 bf16 = 1.5 GB)
     enc = build_encoder(args.embedder, device=dev, seed=args.seed, dtype=wdtype)
-    emb_engine = EmbeddingEngine(enc, tok, name=args.embedder, max_tokens_per_batch=131072)
+    emb_engine = EmbeddingEngine(enc, tok, name=args.embedder, max_tokens_per_batch=262144)
     n = len(chunks)
     per = (n + world - 1) // world
     lo, hi = min(n, rank * per), min(n, (rank + 1) * per)

@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--docs", type=int, default=100000)
     ap.add_argument("--embedder", default="bge-base")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--budget", type=int, default=131072, help="tokens per encoder micro-batch")
+    ap.add_argument("--budget", type=int, default=262144, help="tokens per encoder micro-batch")
     a = ap.parse_args()
     from llm_kubernetes_minikube_sharp4dev_amd.rag.corpus import build_chunks
 
