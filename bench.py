@@ -295,6 +295,8 @@ def main():
     del full, shard, mine
     sync()
     t_index = time.perf_counter() - t0
+    if on_gpu:  # the encoder's micro-batch activations go back to the device before the KV pool is sized
+        torch.cuda.empty_cache()
     if on_gpu and not args.no_graphs and args.admit_chunk == 1:
         # one query per retrieval (batch 1): its encoder pass replays a hipGraph per length
         t_cap = time.perf_counter()
