@@ -50,9 +50,15 @@ FOLD_NORMS = os.environ.get("LK_FOLD_NORMS", "1") != "0"
 # step, ~17 ms two-shot against 50.7 ms of compute when serialised).  The o tail
 # alone cannot hide behind its own GEMM (o's shard is 1/8 the FLOPs of the MLP's): the MLP of
 # the previous chunk covers it.  LK_TP_OVERLAP=0: whole-step GEMMs, then their tails.
+# Chunking costs GEMM efficiency: the 70B TP=8 rank-0 shard (--tp-sim 8, collectives elided, same
+# box, twice) ran its mixed steps in 60.8-64.2 ms with 4 chunks from 1,024 rows against 45.3-45.7
+# ms unchunked (48.5-48.9 vs 62.5-63.0 q/s: ~650-row chunks leave the O / MLP shard GEMMs with a
+# fraction of a wave of tiles), more than the collectives it hides at those step sizes; 2 chunks
+# from 4,096 rows cost 3 % (46.8-47.3 ms) and keep the overlap where a chunk still fills the chip
+# (profiles/r6_tpsim_overlap/).
 TP_OVERLAP = os.environ.get("LK_TP_OVERLAP", "1") != "0"
-TP_OVERLAP_MIN_ROWS = int(os.environ.get("LK_TP_OVERLAP_MIN_ROWS", "1024"))
-TP_OVERLAP_CHUNKS = int(os.environ.get("LK_TP_OVERLAP_CHUNKS", "4"))
+TP_OVERLAP_MIN_ROWS = int(os.environ.get("LK_TP_OVERLAP_MIN_ROWS", "4096"))
+TP_OVERLAP_CHUNKS = int(os.environ.get("LK_TP_OVERLAP_CHUNKS", "2"))
 TP_OVERLAP_ALIGN = int(os.environ.get("LK_TP_OVERLAP_ALIGN", "256"))
 
 

@@ -142,9 +142,10 @@ def test_tp_sim_estimate_counts_only_exposed_collectives():
     spec.loader.exec_module(b)
     floor = b._collective_floor(None, 8192)  # the measured per-call floor (profiles/r4_tp_collectives)
     lc = decoder_config("llama-3-70b")
-    assert overlap_chunks(64) is None and overlap_chunks(4096) == [(0, 1024), (1024, 2048), (2048, 3072), (3072, 4096)]
+    assert overlap_chunks(64) is None and overlap_chunks(2048) is None
+    assert overlap_chunks(4096) == [(0, 2048), (2048, 4096)]
     for up in (True, False):
         serial = lambda rows: (2 * lc.num_layers + 1) * b._per_call_us(floor, rows, lc.hidden, 8, up)  # noqa: E731
         assert abs(b._exposed_step_us(floor, 64, lc, 8, up) - serial(64)) < 1e-6
         exposed = b._exposed_step_us(floor, 4096, lc, 8, up)
-        assert exposed < 0.6 * serial(4096), (up, exposed, serial(4096))
+        assert 0 < exposed < 0.7 * serial(4096), (up, exposed, serial(4096))  # (2 chunks: ~0.62 / ~0.5)
